@@ -1,0 +1,231 @@
+"""Benchmark of the IWAE hot path on MI355X (BASELINE.json metric:
+"train images*k/sec and k=5000 test-NLL images/sec, 1-8 MI355X").
+
+Workload (BASELINE.json configs[1], fits one GPU): IWAE, k=50, 2 stochastic
+layers 784-200-200-100-100-50, batch 20 per GPU, one full train step (forward,
+IWAE bound, backward, Adam) per step, device Philox noise, hipGraph replay.
+Data: synthetic fixed-binarised 784-pixel images (MNIST-like pixel means,
+mean ~0.13) resident in HBM; Glorot weights.  `value` = sample-rows (images*k)
+per second over all ranks (weak scaling: 20 images per GPU, RCCL gradient
+all-reduce for N > 1).  The k=5000 NLL over 10k synthetic images (configs[2],
+sharded by image) is reported beside it under "nll".
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...    (one process per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HE, HD, LE, LD = [200, 100], [100, 200], [100, 50], [100, 784]
+B_PER_GPU, K = 20, 50
+# algorithmic train FLOP per image*sample, 2L k=50
+TRAIN_FLOP_PER_ROW = 1_712_944
+NLL_FLOP_PER_IMAGE = 2.818e9
+FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec peak
+HBM_PEAK_GBS = 8000.0
+
+
+def pixel_profile():
+    """Fixed smooth MNIST-like per-pixel 'on' probability, mean ~0.13 (seed 0)."""
+    rng = np.random.default_rng(0)
+    yy, xx = np.mgrid[0:28, 0:28]
+    r = np.sqrt((yy - 13.5) ** 2 + (xx - 13.5) ** 2)
+    base = 0.355 * np.exp(-((r - 5.5) ** 2) / 18.0)
+    pi = np.clip(base + 0.03 * rng.random((28, 28)), 0.0, 0.95).reshape(-1)
+    return pi
+
+
+def synthetic_images(n, seed):
+    pi = pixel_profile()
+    rng = np.random.default_rng(seed)
+    return (rng.random((n, 784)) < pi).astype(np.float32), pi
+
+
+def cpu_baseline(seconds=12.0):
+    """The oracle (numpy restatement of the reference's op sequence, incl. the
+    duplicate decoder pass at F:340) timed on host cores: IWAE train steps at
+    the bench workload (B=20, k=50, 2L), float32."""
+    from oracle import iwae_oracle as O
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:          # pragma: no cover
+        threadpool_limits = None
+    cores = min(16, os.cpu_count() or 1)
+    ctx = threadpool_limits(limits=cores) if threadpool_limits else None
+    try:
+        spec = O.ModelSpec(HE, HD, LE, LD)
+        x, pi = synthetic_images(B_PER_GPU, 1)
+        rng = np.random.default_rng(2)
+        params = O.cast_params(O.glorot_init(spec, rng, out_bias=O.output_bias_from_mean(pi)), np.float32)
+        opt = O.Adam(1e-3, 0.9, 0.999, 1e-4)
+        xf = x.astype(np.float32)
+        steps, t0 = 0, time.perf_counter()
+        while True:
+            eps = O.draw_eps(spec, K, B_PER_GPU, rng, np.float32)
+            J, g = O.objective_and_grads(params, spec, xf, eps, "IWAE", K, dup_decoder=True)
+            flat = O.flatten_params(spec, params)
+            new = opt.apply(flat, -O.flatten_params(spec, g).astype(np.float32))
+            params = O.unflatten_params(spec, new, dtype=np.float32)
+            steps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    finally:
+        if ctx is not None:
+            ctx.__exit__(None, None, None)
+    return dict(value=steps * B_PER_GPU * K / el, unit="image*samples/s", cores=cores, kind="port",
+                sample=f"{steps} IWAE train steps (2L, k={K}, batch {B_PER_GPU}, float32 numpy, incl. the "
+                       f"F:340 duplicate decoder pass) in {el:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--nll-images", type=int, default=10000)
+    ap.add_argument("--nll-k", type=int, default=5000)
+    ap.add_argument("--no-nll", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-graphs", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from iwae_replication_project_amd import Adam, Flexible_Model, distributed
+
+    x_all, pi = synthetic_images(50_000, 1 + rank)
+    model = Flexible_Model(HE, HD, LE, LD, dataset_bias=pi, loss_function="IWAE", k=K, seed=2,
+                           use_graphs=not args.no_graphs)
+    model.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+    if world > 1:
+        distributed.enable_data_parallel(model)
+    xd = model._x(x_all)
+    nb = xd.shape[0] // B_PER_GPU
+    batches = [xd[i * B_PER_GPU:(i + 1) * B_PER_GPU] for i in range(nb)]
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def run(n, off=0):
+        for i in range(n):
+            model.train_step(batches[(off + i) % nb], sync=False)
+
+    # ---- warmup
+    run(args.warmup)
+    model._stream.synchronize()
+    torch.cuda.synchronize()
+    # ---- timed region: K train steps
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps, args.warmup)
+    model._stream.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    loss = float(model._loss_buf.item())
+    rows = world * B_PER_GPU * K * args.steps
+    value = rows / el
+    ms_per_step = 1e3 * el / args.steps
+
+    # ---- dominant kernel live timing: HIP events on the library stream around
+    # every launch of the decoder output GEMM (200 -> 784, fused Bernoulli
+    # epilogue) over K eager steps of the same workload
+    model._call(model._lib.iwae_profile_gemm(model._h, 0, 2))
+    run(args.steps, args.warmup + args.steps)
+    import ctypes
+    ms, fl, nl = ctypes.c_double(), ctypes.c_double(), ctypes.c_longlong()
+    model._call(model._lib.iwae_profile_read(model._h, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(nl)))
+    model._call(model._lib.iwae_profile_gemm(model._h, -1, -1))
+    avg_ms = ms.value / max(1, nl.value)
+    flop_per_launch = fl.value / max(1, nl.value)
+    achieved = flop_per_launch / (avg_ms * 1e-3) / 1e12
+    roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
+                    frac=round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), traffic=None,
+                    kernel="gemm_kernel<FWD, EPI_BERN> (decoder 200->784 + Bernoulli log-prob)",
+                    avg_us=round(avg_ms * 1e3, 3), flop_per_launch=flop_per_launch, launches=int(nl.value),
+                    step_tflops=round(TRAIN_FLOP_PER_ROW * rows / el / 1e12, 3))
+
+    # ---- k=5000 NLL over the test images, sharded by image
+    nll = None
+    if not args.no_nll:
+        xt, _ = synthetic_images(args.nll_images, 99)
+        lo, hi = distributed.shard_range(args.nll_images, rank, world)
+        xs = model._x(xt[lo:hi])
+        model.log_px(xs[: max(1, min(64, hi - lo))], args.nll_k)      # warm the NLL workspace
+        barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        lp = model.log_px(xs, args.nll_k)
+        tot = torch.stack([lp.sum(), torch.tensor(float(hi - lo), device=lp.device)])
+        torch.cuda.synchronize()
+        barrier()
+        el2 = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([el2], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el2 = float(t.item())
+            dist.all_reduce(tot)
+        nll = dict(value=round(args.nll_images / el2, 2), unit="images/s", images=args.nll_images, k=args.nll_k,
+                   seconds=round(el2, 4), nll=round(float(-(tot[0] / tot[1]).item()), 4), shard="image",
+                   tflops=round(NLL_FLOP_PER_IMAGE * (args.nll_k / 5000) * args.nll_images / el2 / 1e12, 3))
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": "train images*k/sec and k=5000 test-NLL images/sec, 1-8 MI355X",
+            "value": round(value, 1),
+            "unit": "image*samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": "IWAE train step (fwd+bound+bwd+Adam), k=50, 2 stochastic layers "
+                                   "784-200-200-100-100-50, batch 20 per GPU (BASELINE configs[1])",
+                       "global_batch": B_PER_GPU * world, "k": K, "parallelism": f"dp{world}",
+                       "noise": "device Philox", "graphs": not args.no_graphs},
+            "loss": round(loss, 4),
+            "nll": nll,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

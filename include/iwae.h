@@ -1,0 +1,178 @@
+/*
+ * iwae.h -- C ABI of libiwae_hip.so, the MI355X (gfx950) IWAE train-step and
+ * k-sample NLL hot path.
+ *
+ * This is the drop-in boundary for the reference's model API
+ * (/root/reference/flexible_IWAE.py, "F:" below).  The reference has no native
+ * code and no FFI: its "interface" is the Python class Flexible_Model.  Each
+ * entry point below replaces the TensorFlow op sequence behind one method of
+ * that class; the Python facade iwae_replication_project_amd.Flexible_Model
+ * binds them with ctypes (see INTEGRATION.md for the binding a maintainer of
+ * the reference would add).
+ *
+ * Conventions
+ *  - Every function returns 0 on success, a negative IWAE_E* code on error;
+ *    iwae_last_error(h) then holds a message.  Nothing throws across the ABI.
+ *  - Tensors are plain float32.  Pointers marked [dev] are device (HBM)
+ *    pointers; [host] are host pointers.  The caller owns all inputs/outputs;
+ *    the handle owns weights, Adam state, workspace and RNG state.
+ *  - Device work is enqueued on the handle's HIP stream (iwae_set_stream) and
+ *    is asynchronous w.r.t. the host, except functions documented as
+ *    synchronous (parameter/gradient/state copies to/from host).
+ *  - One handle per GPU / rank; a handle is not thread-safe.
+ *  - Noise: eps == NULL -> on-device Philox4x32-10 (key = iwae_set_seed,
+ *    counter advanced once per forward pass).  Otherwise eps[] holds one
+ *    [dev] buffer per stochastic layer in the reference's sample-major layout
+ *    [k][B][d_i] (F:59 qh1Ix.sample(n), F:68 .sample()); CIWAE takes 2*L
+ *    buffers: draw 1 feeds the VAE term, draw 2 the IWAE term (F:383).
+ *  - Internally rows are image-major (row = b*k + s).  Outputs documented as
+ *    [B][k] use that layout.
+ */
+#ifndef IWAE_H
+#define IWAE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IWAE_MAX_LAYERS 8
+
+/* error codes */
+#define IWAE_OK 0
+#define IWAE_EINVAL (-1)   /* bad argument / unknown loss (reference: UnboundLocalError at F:242) */
+#define IWAE_EHIP (-2)     /* HIP runtime error */
+#define IWAE_ENOMEM (-3)
+
+/* loss ids: Flexible_Model.train_step dispatch F:228-F:241, plus MIWAE/PIWAE
+ * (IWAE_replication.pdf p7 s2.4 / Rainforth et al.), absent from the code. */
+enum iwae_loss_id {
+  IWAE_LOSS_VAE = 0,        /* -get_L        F:229, F:419 */
+  IWAE_LOSS_IWAE = 1,       /* -get_L_k      F:231, F:354 */
+  IWAE_LOSS_VAE_V1 = 2,     /* -get_L_V1     F:233, F:434 */
+  IWAE_LOSS_L_ALPHA = 3,    /* -get_L_alpha  F:235, F:386 */
+  IWAE_LOSS_L_POWER_P = 4,  /* -get_L_power_p F:237, F:405 */
+  IWAE_LOSS_L_MEDIAN = 5,   /* -get_L_median F:239, F:373 */
+  IWAE_LOSS_CIWAE = 6,      /* -get_L_CIWAE  F:241, F:382 */
+  IWAE_LOSS_MIWAE = 7,      /* MIWAE(k1,k2), PDF p7 */
+  IWAE_LOSS_PIWAE = 8       /* decoder: IWAE_{k1 k2}, encoder: MIWAE(k1,k2) */
+};
+
+/* Architecture knobs of Flexible_Model.__init__ (F:178-F:180). */
+typedef struct iwae_config {
+  int n_stochastic;                         /* len(n_hidden_encoder) */
+  int x_dim;                                /* 784 (F:57, F:94) */
+  int n_hidden_encoder[IWAE_MAX_LAYERS];
+  int n_latent_encoder[IWAE_MAX_LAYERS];
+  int n_hidden_decoder[IWAE_MAX_LAYERS];
+  int n_latent_decoder[IWAE_MAX_LAYERS];
+} iwae_config;
+
+/* Loss knobs of Flexible_Model (loss_function, k, p, alpha, beta; F:179-F:217)
+ * plus the MIWAE/PIWAE split k = k1*k2 (sample s = j*k1 + i, j < k2). */
+typedef struct iwae_loss_config {
+  int loss;
+  int k;
+  float p;
+  float alpha;
+  float beta;
+  int k1;
+  int k2;
+} iwae_loss_config;
+
+typedef struct iwae_handle iwae_handle;
+
+/* --- lifetime ------------------------------------------------------------ */
+/* Replaces Flexible_Model.__init__ (F:178-F:218).  Weights are zero until
+ * iwae_set_params (the reference draws Glorot weights lazily inside Keras;
+ * the facade draws them on the host and uploads them).  NULL on error. */
+iwae_handle* iwae_create(const iwae_config* cfg, int device);
+const char* iwae_create_error(void);
+void iwae_destroy(iwae_handle* h);
+const char* iwae_last_error(const iwae_handle* h);
+/* Enqueue on this stream (hipStream_t); NULL = the handle's own stream. */
+int iwae_set_stream(iwae_handle* h, void* hip_stream);
+int iwae_synchronize(iwae_handle* h);
+int iwae_set_seed(iwae_handle* h, unsigned long long seed);
+/* 1 = capture the Philox train step in a hipGraph per shape and replay it. */
+int iwae_set_graphs(iwae_handle* h, int enable);
+
+/* --- parameters (synchronous host copies) --------------------------------- */
+/* Flat float32 in Keras trainable_weights order: encoder then decoder, per
+ * Stochastic_layer l1,l2,lmu,lstd (F:26-F:29), decoder prior layers then the
+ * output Sequential (F:86-F:96); per Dense kernel [in][out] then bias [out]. */
+long long iwae_num_params(const iwae_handle* h);
+int iwae_set_params(iwae_handle* h, const float* host, long long n);
+int iwae_get_params(iwae_handle* h, float* host, long long n);
+/* Gradient of the LOSS (-bound) from the last iwae_forward_backward, same order. */
+int iwae_get_grads(iwae_handle* h, float* host, long long n);
+
+/* --- optimizer: Keras Adam (E:36-E:40), TF ResourceApplyAdam semantics ----- */
+int iwae_set_adam(iwae_handle* h, float lr, float beta1, float beta2, float epsilon);
+int iwae_get_adam_state(iwae_handle* h, float* m_host, float* v_host, long long n,
+                        long long* step);
+int iwae_set_adam_state(iwae_handle* h, const float* m_host, const float* v_host,
+                        long long n, long long step);
+
+/* --- training (device pointers, stream-ordered) --------------------------- */
+/* Flexible_Model.train_step (F:221-F:247): forward, loss, backward, Adam.
+ * x [dev] is [B][x_dim] in {0,1}.  loss_dev [dev, may be NULL] receives the
+ * scalar loss (= -bound, the value train_step returns in {loss: ...}). */
+int iwae_train_step(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,
+                    const float* const* eps, int n_eps, float* loss_dev);
+/* The same without the Adam update (gradient kept on device).  For data
+ * parallelism: forward_backward -> all-reduce(grad buffer) -> apply_adam. */
+int iwae_forward_backward(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,
+                          const float* const* eps, int n_eps, float* loss_dev);
+/* Device gradient buffer (internal padded layout, elementwise-summable).  The
+ * caller may bind its own buffer (e.g. a torch tensor used for RCCL). */
+int iwae_grad_buffer(iwae_handle* h, float** grad_dev, long long* n);
+int iwae_bind_grad_buffer(iwae_handle* h, float* grad_dev, long long n);
+/* Adam over the gradient buffer times grad_scale (1/world_size under DP). */
+int iwae_apply_adam(iwae_handle* h, float grad_scale);
+
+/* --- evaluation ----------------------------------------------------------- */
+/* get_log_weights (F:327-F:351): lw [dev] [B][k] (image-major). */
+int iwae_log_weights(iwae_handle* h, const float* x, int B, int k,
+                     const float* const* eps, int n_eps, float* lw);
+/* The bound (= -loss) of lc on x without a backward pass: get_L, get_L_k,
+ * get_L_CIWAE, get_L_power_p, get_L_median, get_L_alpha, get_L_V1 (F:354-F:460).
+ * value_dev [dev] receives one float. */
+int iwae_bound(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,
+               const float* const* eps, int n_eps, float* value_dev);
+/* E_q(h|x)[log p(x|h)] with Keras BCE (get_E_qhIx_log_pxIh, F:304-F:325). */
+int iwae_e_log_px(iwae_handle* h, const float* x, int B, int k,
+                  const float* const* eps, int n_eps, float* value_dev);
+/* k-sample log p(x) estimate per image (get_NLL = -mean of it, F:463-F:464).
+ * Images are processed in chunks of `chunk` images (0 = auto) so that
+ * chunk*k rows fit the workspace; out_logpx [dev] is [N]. */
+int iwae_nll(iwae_handle* h, const float* x, int N, int k, int chunk, float* out_logpx);
+/* Log-sum-exp partials for sample-sharded NLL: over k_local Philox samples per
+ * image, out_m[i] = max_s lw, out_s[i] = sum_s exp(lw - out_m[i]) ([dev], [N]).
+ * Partials from several ranks merge as M = max m, S = sum s*exp(m-M),
+ * log p(x) = M + log S - log(k_total). */
+int iwae_nll_partials(iwae_handle* h, const float* x, int N, int k_local, int chunk,
+                      float* out_m, float* out_s);
+/* Same as iwae_nll with injected noise (parity tests): eps[i] is [k][N][d_i]. */
+int iwae_nll_eps(iwae_handle* h, const float* x, int N, int k, const float* const* eps,
+                 int n_eps, float* out_logpx);
+
+/* --- diagnostics ---------------------------------------------------------- */
+/* C[M][N] = A[M][K] @ B[K][N] (all [dev], row-major, leading dims given) via
+ * the f32 MFMA GEMM used on the hot path (unit-test entry). */
+int iwae_debug_gemm(iwae_handle* h, const float* A, int lda, const float* B, int ldb,
+                    float* C, int ldc, int M, int N, int K);
+/* Bytes of device workspace currently allocated by the handle. */
+double iwae_workspace_bytes(const iwae_handle* h);
+/* Live kernel timing: bracket every launch of one GEMM class (kind: 0 forward,
+ * 1 backward-data, 2 backward-weight; epi: 0 store, 1 tanh, 2 Bernoulli,
+ * 3 tanh-grad; kind = -1 disables) with HIP events on the handle's stream.
+ * Disables hipGraph replay while active.  iwae_profile_read synchronizes and
+ * returns the summed kernel milliseconds, the algorithmic FLOPs of those
+ * launches (2*rows*fan_in*fan_out each) and the launch count. */
+int iwae_profile_gemm(iwae_handle* h, int kind, int epi);
+int iwae_profile_read(iwae_handle* h, double* total_ms, double* total_flop, long long* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IWAE_H */

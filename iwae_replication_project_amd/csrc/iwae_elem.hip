@@ -1,0 +1,540 @@
+// Sampling, Gaussian log-densities, bound reductions, NLL log-sum-exp and
+// Adam for the IWAE hot path (gfx950).  All are wave64 row kernels: one wave
+// per row (or per image), lanes over the latent dimension (or over samples),
+// reductions by __shfl_xor butterflies -- HBM/latency-bound by design.
+#include "iwae_kernels.h"
+
+namespace iwae {
+
+// ----------------------------------------------------------------- helpers
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Philox4x32-10 (Salmon et al. 2011), one normal per (row, layer, column)
+// via Box-Muller; counter = (row, layer<<20 | col, base_lo, base_hi).
+__device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t base, unsigned row,
+                                               unsigned layer, unsigned col) {
+  unsigned c0 = row, c1 = (layer << 20) | col, c2 = (unsigned)base, c3 = (unsigned)(base >> 32);
+  unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const unsigned lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const unsigned lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  const float u0 = ((float)c0 + 0.5f) * 2.3283064365386963e-10f;  // (0,1)
+  const float u1 = ((float)c1 + 0.5f) * 2.3283064365386963e-10f;
+  return sqrtf(-2.f * logf(u0)) * cospif(2.f * u1);
+}
+
+__device__ __forceinline__ float eps_at(const float* ea, const float* eb, int kS, int Bsplit, int Bimg,
+                                        int d, int r, int j, uint64_t seed, uint64_t base, int layer) {
+  const int bi = r / kS, s = r - bi * kS;
+  if (bi < Bsplit) {
+    if (ea) return ea[((size_t)s * Bsplit + bi) * d + j];
+  } else {
+    if (eb) return eb[((size_t)s * (Bimg - Bsplit) + (bi - Bsplit)) * d + j];
+  }
+  return philox_normal(seed, base, (unsigned)r, (unsigned)layer, (unsigned)j);
+}
+
+// Last-arriving workgroup detection (agent-scope release/acquire, counter form).
+__device__ __forceinline__ bool last_block_arrive(unsigned* ticket) {
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == nb - 1);
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
+// ------------------------------------------------------- Gaussian forward
+// TFP Normal._log_prob: -0.5*(x/s - loc/s)^2 - (0.5*log(2pi) + log(s)),
+// Normal.sample: eps*s + loc, with s = exp(zs) + 1e-6 (F:29, F:37).
+template <int MODE>
+__global__ __launch_bounds__(256) void gauss_fwd_kernel(GaussArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.M) return;
+  uint64_t base = 0;
+  if (MODE == 0 && a.rng_base) base = *a.rng_base;
+  float acc = 0.f;
+  for (int j = lane; j < a.d; j += 64) {
+    float lp;
+    if (MODE == 2) {
+      const float h = a.H[(size_t)r * a.ldH + j];
+      lp = __fsub_rn(-0.5f * (h * h), kHalfLog2Pi);
+    } else {
+      const int pr = r / a.prow_div;
+      const float mu = a.P[(size_t)pr * a.ldP + j];
+      const float zs = a.P[(size_t)pr * a.ldP + a.d + j];
+      const float sc = __fadd_rn(expf(zs), kScaleEps);
+      float h;
+      if (MODE == 0) {
+        const float e = eps_at(a.eps_a, a.eps_b, a.kS, a.Bsplit, a.Bimg, a.d, r, j, a.seed, base, a.layer);
+        h = __fadd_rn(__fmul_rn(e, sc), mu);
+        a.H[(size_t)r * a.ldH + j] = h;
+      } else {
+        h = a.H[(size_t)r * a.ldH + j];
+      }
+      const float z = __fsub_rn(h / sc, mu / sc);
+      lp = __fsub_rn(-0.5f * (z * z), __fadd_rn(kHalfLog2Pi, logf(sc)));
+    }
+    acc += lp;
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) a.out[r] = a.accumulate ? a.out[r] + acc : acc;
+}
+
+hipError_t launch_gauss_fwd(hipStream_t st, int mode, const GaussArgs& a) {
+  if (a.M <= 0) return hipSuccess;
+  dim3 grid((a.M + 3) / 4);
+  if (mode == 0) hipLaunchKernelGGL(gauss_fwd_kernel<0>, grid, dim3(256), 0, st, a);
+  else if (mode == 1) hipLaunchKernelGGL(gauss_fwd_kernel<1>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(gauss_fwd_kernel<2>, grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------ Gaussian backward
+// GradientTape semantics of log N(h; mu, s) with h = eps*s + mu: partials
+// through h AND through (mu, s) (F:59-F:73), chained into zs via ds/dzs = exp(zs).
+// Mode 0 (encoder sampling layer): block = 4 P-rows (prow_div == 1) or one
+// image (prow_div > 1; waves split its rows, LDS combine).
+__global__ __launch_bounds__(256) void gauss_bwd_enc_kernel(GaussBwdArgs a) {
+  __shared__ float red[2][4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool per_image = a.prow_div > 1;
+  const int pr = per_image ? blockIdx.x : blockIdx.x * 4 + wave;
+  const int nP = (a.M + a.prow_div - 1) / a.prow_div;
+  const bool row_ok = pr < nP;
+  uint64_t base = 0;
+  if (a.rng_base && !(a.eps_a)) base = *a.rng_base;
+  for (int j0 = 0; j0 < a.d; j0 += 64) {
+    const int j = j0 + lane;
+    const bool act = row_ok && j < a.d;
+    float mu = 0.f, zs = 0.f, e = 0.f, sc = 1.f;
+    if (act) {
+      mu = a.P[(size_t)pr * a.ldP + j];
+      zs = a.P[(size_t)pr * a.ldP + a.d + j];
+      e = expf(zs);
+      sc = __fadd_rn(e, kScaleEps);
+    }
+    float amu = 0.f, asc = 0.f;
+    if (act) {
+      const int r_begin = pr * a.prow_div;
+      const int s_begin = per_image ? wave : 0, s_step = per_image ? 4 : 1;
+      for (int s = s_begin; s < a.prow_div; s += s_step) {
+        const int r = r_begin + s;
+        if (r >= a.M) break;
+        const float h = a.H[(size_t)r * a.ldH + j];
+        const float ev = eps_at(a.eps_a, a.eps_b, a.kS, a.Bsplit, a.Bimg, a.d, r, j, a.seed, base, a.layer);
+        const float dlq = -a.dlw[r];
+        const float z = __fsub_rn(h / sc, mu / sc);
+        float G = 0.f;
+        for (int q = 0; q < a.nsrc; ++q) G += a.src[q][(size_t)r * a.ldsrc[q] + j];
+        if (a.std_normal) G += a.dlw[r] * (-h);
+        G += dlq * (-z / sc);
+        amu += G + dlq * (z / sc);
+        asc += G * ev + dlq * ((z * z - 1.f) / sc);
+      }
+    }
+    if (per_image) {
+      red[0][wave][lane] = amu;
+      red[1][wave][lane] = asc;
+      __syncthreads();
+      if (wave == 0) {
+        amu = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+        asc = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+      }
+      __syncthreads();
+    }
+    if (act && (!per_image || wave == 0)) {
+      if (a.kl_coef != 0.f) {
+        amu += a.kl_coef * mu / (float)a.kl_rows;
+        asc += a.kl_coef * (sc - 1.f / sc) / (float)a.kl_rows;
+      }
+      a.dP[(size_t)pr * a.lddP + j] = amu;
+      a.dP[(size_t)pr * a.lddP + a.d + j] = asc * e;
+    }
+  }
+}
+
+// Mode 1 (decoder prior head p(h_t | h_src)): dL/dlogp = dlw per row.
+__global__ __launch_bounds__(256) void gauss_bwd_prior_kernel(GaussBwdArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.M) return;
+  const float dlp = a.dlw[r];
+  for (int j = lane; j < a.d; j += 64) {
+    const float mu = a.P[(size_t)r * a.ldP + j];
+    const float zs = a.P[(size_t)r * a.ldP + a.d + j];
+    const float e = expf(zs);
+    const float sc = __fadd_rn(e, kScaleEps);
+    const float h = a.H[(size_t)r * a.ldH + j];
+    const float z = __fsub_rn(h / sc, mu / sc);
+    a.dh_out[(size_t)r * a.ldh_out + j] = dlp * (-z / sc);
+    a.dP[(size_t)r * a.lddP + j] = dlp * (z / sc);
+    a.dP[(size_t)r * a.lddP + a.d + j] = dlp * ((z * z - 1.f) / sc) * e;
+  }
+}
+
+hipError_t launch_gauss_bwd(hipStream_t st, int mode, const GaussBwdArgs& a) {
+  if (a.M <= 0) return hipSuccess;
+  if (mode == 0) {
+    const int nP = (a.M + a.prow_div - 1) / a.prow_div;
+    dim3 grid(a.prow_div > 1 ? nP : (nP + 3) / 4);
+    hipLaunchKernelGGL(gauss_bwd_enc_kernel, grid, dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(gauss_bwd_prior_kernel, dim3((a.M + 3) / 4), dim3(256), 0, st, a);
+  }
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------- bounds
+// One wave per image.  lw = (logp + logpx) - logq (F:345, F:349) with logpx
+// the sum of the Bernoulli epilogue's per-32-column partials.
+__device__ __forceinline__ float row_sum_parts(const float* part, int ldpart, int npart, int r) {
+  const float* p = part + (size_t)r * ldpart;
+  float s = 0.f;
+  for (int t = 0; t < npart; ++t) s += p[t];
+  return s;
+}
+__device__ __forceinline__ float lw_at(const BoundArgs& a, int r) {
+  return __fsub_rn(__fadd_rn(a.logp[r], row_sum_parts(a.part, a.ldpart, a.npart, r)), a.logq[r]);
+}
+
+struct ImgBound {
+  float val;
+  float mx, se;  // IWAE / POWER
+  int lo, hi;    // MEDIAN (row offsets)
+};
+
+// value of the per-image bound; LSE-type statistics kept for the gradient pass
+__device__ ImgBound image_bound(const BoundArgs& a, int mode, int row0, float* sh) {
+  const int lane = threadIdx.x & 63;
+  const int kS = a.kS;
+  ImgBound o{0.f, 0.f, 0.f, 0, 0};
+  if (mode == BM_NONE) return o;
+  if (mode == BM_VAE) {
+    float s = 0.f;
+    for (int q = lane; q < kS; q += 64) s += lw_at(a, row0 + q);
+    o.val = wave_sum(s) / (float)kS;          // reduce_mean (F:430)
+    return o;
+  }
+  if (mode == BM_IWAE || mode == BM_POWER) {
+    const float pp = mode == BM_POWER ? a.p : 1.f;
+    float mx = -INFINITY;
+    for (int q = lane; q < kS; q += 64) mx = fmaxf(mx, lw_at(a, row0 + q));
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int q = lane; q < kS; q += 64) se += expf((lw_at(a, row0 + q) - mx) * pp);
+    se = wave_sum(se);
+    o.mx = mx; o.se = se;
+    // F:369: log(reduce_mean(exp(lw - max))) + max ; F:408: .../p + max
+    o.val = (mode == BM_POWER) ? logf(se / (float)kS) / pp + mx : logf(se / (float)kS) + mx;
+    return o;
+  }
+  if (mode == BM_MEDIAN) {
+    // tfp.stats.percentile(50, 'midpoint') = mean of order statistics
+    // floor((k-1)/2) and ceil((k-1)/2) (F:377).  Rank by counting (kS <= 1024).
+    for (int q = lane; q < kS; q += 64) sh[q] = lw_at(a, row0 + q);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int klo = (kS - 1) / 2, khi = kS / 2;
+    float vlo = 0.f, vhi = 0.f;
+    int ilo = 0, ihi = 0;
+    for (int q = lane; q < kS; q += 64) {
+      const float v = sh[q];
+      int rank = 0;
+      for (int t = 0; t < kS; ++t) {
+        const float u = sh[t];
+        rank += (u < v) || (u == v && t < q);
+      }
+      if (rank == klo) { vlo = v; ilo = q + 1; }
+      if (rank == khi) { vhi = v; ihi = q + 1; }
+    }
+    // exactly one lane found each rank: combine by max over (index+1 > 0) lanes
+    vlo = wave_sum(ilo ? vlo : 0.f); vhi = wave_sum(ihi ? vhi : 0.f);
+    float flo = wave_max((float)ilo), fhi = wave_max((float)ihi);
+    o.lo = (int)flo - 1; o.hi = (int)fhi - 1;
+    o.val = (vlo + vhi) * 0.5f;
+    return o;
+  }
+  // BM_MIWAE: sample s = j*k1 + i; mean_j [log mean_i exp(lw - m_j) + m_j]
+  float tot = 0.f;
+  for (int j = 0; j < a.k2; ++j) {
+    const int g0 = row0 + j * a.k1;
+    float mx = -INFINITY;
+    for (int i = lane; i < a.k1; i += 64) mx = fmaxf(mx, lw_at(a, g0 + i));
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int i = lane; i < a.k1; i += 64) se += expf(lw_at(a, g0 + i) - mx);
+    se = wave_sum(se);
+    tot += logf(se / (float)a.k1) + mx;
+  }
+  o.val = tot / (float)a.k2;
+  return o;
+}
+
+// dBound/dlw at row r (q = sample index) times coef
+__device__ __forceinline__ void image_grad(const BoundArgs& a, int mode, int row0, const ImgBound& ib,
+                                           float coef, float* out) {
+  const int lane = threadIdx.x & 63;
+  const int kS = a.kS;
+  if (mode == BM_NONE) {
+    for (int q = lane; q < kS; q += 64) out[row0 + q] = 0.f;
+  } else if (mode == BM_VAE) {
+    for (int q = lane; q < kS; q += 64) out[row0 + q] = coef / (float)kS;
+  } else if (mode == BM_IWAE || mode == BM_POWER) {
+    const float pp = mode == BM_POWER ? a.p : 1.f;
+    for (int q = lane; q < kS; q += 64)
+      out[row0 + q] = coef * (expf((lw_at(a, row0 + q) - ib.mx) * pp) / ib.se);
+  } else if (mode == BM_MEDIAN) {
+    for (int q = lane; q < kS; q += 64)
+      out[row0 + q] = coef * (0.5f * (q == ib.lo) + 0.5f * (q == ib.hi));
+  } else {  // MIWAE
+    for (int j = 0; j < a.k2; ++j) {
+      const int g0 = row0 + j * a.k1;
+      float mx = -INFINITY;
+      for (int i = lane; i < a.k1; i += 64) mx = fmaxf(mx, lw_at(a, g0 + i));
+      mx = wave_max(mx);
+      float se = 0.f;
+      for (int i = lane; i < a.k1; i += 64) se += expf(lw_at(a, g0 + i) - mx);
+      se = wave_sum(se);
+      for (int i = lane; i < a.k1; i += 64)
+        out[g0 + i] = coef * (expf(lw_at(a, g0 + i) - mx) / se) / (float)a.k2;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void bound_kernel(BoundArgs a) {
+  __shared__ float sh_all[4][1024];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int b = blockIdx.x * 4 + wave;
+  if (b < a.Bimg) {
+    const bool ga = b < a.Bsplit;
+    const int mode = ga ? a.mode_a : a.mode_b;
+    const float w = ga ? a.w_a : a.w_b;
+    const int Bg = ga ? a.Bsplit : a.Bimg - a.Bsplit;
+    const int row0 = b * a.kS;
+    // log weights (for get_log_weights) and the optional Keras-BCE mean
+    float bsum = 0.f;
+    for (int q = lane; q < a.kS; q += 64) {
+      const int r = row0 + q;
+      a.lw[r] = lw_at(a, r);
+      if (a.part2) bsum += row_sum_parts(a.part2, a.ldpart, a.npart, r);
+    }
+    bsum = wave_sum(bsum);
+    const ImgBound ib = image_bound(a, mode, row0, sh_all[wave]);
+    if (lane == 0) {
+      float c = w * ib.val / (float)Bg;
+      if (a.part2) c += a.bce_w * (bsum / (float)a.kS) / (float)Bg;
+      a.contrib[b] = c;
+    }
+    if (a.dlw) {
+      // loss = -objective: dL/dlw = -(w/Bg) * dBound/dlw
+      image_grad(a, mode, row0, ib, -w / (float)Bg, a.dlw);
+      if (a.dpx) {
+        for (int q = lane; q < a.kS; q += 64) {
+          const int r = row0 + q;
+          a.dpx[r] = a.dpx_is_const ? a.dpx_const : a.dlw[r];
+        }
+      }
+    }
+    if (a.dlw2) {
+      const ImgBound ib2 = image_bound(a, a.mode2, row0, sh_all[wave]);
+      image_grad(a, a.mode2, row0, ib2, -w / (float)Bg, a.dlw2);
+      if (a.dpx2)
+        for (int q = lane; q < a.kS; q += 64) a.dpx2[row0 + q] = a.dlw2[row0 + q];
+    }
+  }
+  if (a.ticket && last_block_arrive(a.ticket)) {
+    if (threadIdx.x < 64) {
+      float s = 0.f;
+      for (int i = lane; i < a.Bimg; i += 64) s += a.contrib[i];
+      s = wave_sum(s);
+      if (lane == 0) {
+        if (a.loss) *a.loss = a.loss_sign * s + (a.loss_add ? a.loss_add_coef * *a.loss_add : 0.f);
+        if (a.rng_base) *a.rng_base += 1;
+        *a.ticket = 0u;
+      }
+    }
+  }
+}
+
+hipError_t launch_bound(hipStream_t st, const BoundArgs& a) {
+  if (a.Bimg <= 0) return hipSuccess;
+  if ((a.mode_a == BM_MEDIAN || a.mode_b == BM_MEDIAN) && a.kS > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bound_kernel, dim3((a.Bimg + 3) / 4), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------- NLL: LSE merge
+__global__ __launch_bounds__(256) void lse_kernel(LseArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b < a.Bimg) {
+    const int row0 = b * a.kS;
+    float m = -INFINITY, s = 0.f;
+    for (int q = lane; q < a.kS; q += 64) {
+      const int r = row0 + q;
+      const float v = __fsub_rn(__fadd_rn(a.logp[r], row_sum_parts(a.part, a.ldpart, a.npart, r)), a.logq[r]);
+      if (v > m) { s = s * expf(m - v) + 1.f; m = v; }
+      else s += expf(v - m);
+    }
+    const float M = wave_max(m);
+    s = wave_sum(m == -INFINITY ? 0.f : s * expf(m - M));
+    if (lane == 0) {
+      if (a.init) { a.run_m[b] = M; a.run_s[b] = s; }
+      else {
+        const float m0 = a.run_m[b], s0 = a.run_s[b];
+        const float MM = fmaxf(m0, M);
+        a.run_s[b] = s0 * expf(m0 - MM) + s * expf(M - MM);
+        a.run_m[b] = MM;
+      }
+    }
+  }
+  if (a.ticket && last_block_arrive(a.ticket)) {
+    if (threadIdx.x == 0) {
+      if (a.rng_base) *a.rng_base += 1;
+      *a.ticket = 0u;
+    }
+  }
+}
+
+hipError_t launch_lse(hipStream_t st, const LseArgs& a) {
+  if (a.Bimg <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lse_kernel, dim3((a.Bimg + 3) / 4), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+__global__ void lse_final_kernel(const float* m, const float* s, int n, float logk, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = m[i] + logf(s[i]) - logk;
+}
+hipError_t launch_lse_final(hipStream_t st, const float* m, const float* s, int n, float logk,
+                            float* out) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lse_final_kernel, dim3((n + 255) / 256), dim3(256), 0, st, m, s, n, logk, out);
+  return hipGetLastError();
+}
+
+// --------------------------------------------------------------- VAE_V1 KL
+// F:457-F:458: mean over rows of sum_d -0.5(1 + 2 log s - mu^2 - s^2)
+__global__ __launch_bounds__(256) void kl_v1_kernel(const float* P, int ldP, int d, int rows, float* out) {
+  __shared__ float red[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float acc = 0.f;
+  for (int r = wave; r < rows; r += 4) {
+    for (int j = lane; j < d; j += 64) {
+      const float mu = P[(size_t)r * ldP + j];
+      const float sc = __fadd_rn(expf(P[(size_t)r * ldP + d + j]), kScaleEps);
+      acc += -0.5f * (1.f + 2.f * logf(sc) - mu * mu - sc * sc);
+    }
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) red[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = (red[0] + red[1] + red[2] + red[3]) / (float)rows;
+}
+hipError_t launch_kl_v1(hipStream_t st, const float* P, int ldP, int d, int rows, float* out) {
+  hipLaunchKernelGGL(kl_v1_kernel, dim3(1), dim3(256), 0, st, P, ldP, d, rows, out);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------- Adam
+// Sums a layer's split-K weight-gradient slabs in fixed order (deterministic),
+// then TF ResourceApplyAdam: m += (g-m)(1-b1); v += (g^2-v)(1-b2);
+// p -= m * lr*sqrt(1-b2^t)/(1-b1^t) / (sqrt(v)+eps).
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+  const AdamSeg sg = a.seg[blockIdx.y];
+  const AdamState st = *a.state;
+  const float scale = a.grad_scale_override > 0.f ? a.grad_scale_override : st.grad_scale;
+  const float t = (float)(st.t + 1);
+  const float b1p = powf(st.b1, t), b2p = powf(st.b2, t);
+  const float alpha = st.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  const float omb1 = 1.f - st.b1, omb2 = 1.f - st.b2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < sg.n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long pidx = sg.off + i;
+    float g;
+    if (a.read_slabs && sg.splits > 0) {
+      g = 0.f;
+      for (int s = 0; s < sg.splits; ++s) g += a.slabs[sg.slab_off + (long long)s * sg.n + i];
+    } else {
+      g = a.grad[pidx];
+    }
+    if (a.write_grad) a.grad[pidx] = g;
+    if (a.do_adam) {
+      g = g * scale;
+      float m = a.m[pidx], v = a.v[pidx];
+      m = m + (g - m) * omb1;
+      v = v + (g * g - v) * omb2;
+      a.m[pidx] = m;
+      a.v[pidx] = v;
+      a.param[pidx] = a.param[pidx] - (m * alpha) / (sqrtf(v) + st.eps);
+    }
+  }
+  if (a.do_adam && last_block_arrive(a.ticket)) {
+    if (threadIdx.x == 0) {
+      a.state->t = st.t + 1;
+      *a.ticket = 0u;
+    }
+  }
+}
+
+hipError_t launch_adam(hipStream_t st, const AdamArgs& a, long long max_seg_n) {
+  if (a.nseg <= 0) return hipSuccess;
+  long long bx = (max_seg_n + 255) / 256;
+  if (bx > 64) bx = 64;
+  if (bx < 1) bx = 1;
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)bx, a.nseg), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- utility
+__global__ void fill_col_kernel(float* buf, int rows, int ld, int col, float v) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < rows) buf[(size_t)r * ld + col] = v;
+}
+hipError_t launch_fill_col(hipStream_t st, float* buf, int rows, int ld, int col, float v) {
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fill_col_kernel, dim3((rows + 255) / 256), dim3(256), 0, st, buf, rows, ld, col, v);
+  return hipGetLastError();
+}
+
+__global__ void transpose_lw_kernel(const float* lw, int Bimg, int kS, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < Bimg * kS) {
+    const int b = i / kS, s = i - b * kS;
+    out[(size_t)s * Bimg + b] = lw[i];
+  }
+}
+hipError_t launch_transpose_lw(hipStream_t st, const float* lw, int Bimg, int kS, float* out) {
+  const int n = Bimg * kS;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(transpose_lw_kernel, dim3((n + 255) / 256), dim3(256), 0, st, lw, Bimg, kS, out);
+  return hipGetLastError();
+}
+
+}  // namespace iwae

@@ -1,0 +1,310 @@
+// f32 MFMA GEMM with fused IWAE epilogues (gfx950 / CDNA4).
+//
+// Every Dense layer of the reference (Keras Dense, F:26-F:29, F:92-F:94) and
+// every backward GEMM of its GradientTape (F:243) runs through this kernel:
+//
+//   GEMM_FWD        C[M][N] = X[M][K] . W[K][N]           (X_aug . W_aug: bias folded)
+//   GEMM_BWD_DATA   C[M][N] = dZ[M][K] . W[N][K]^T         (dX = dZ W^T)
+//   GEMM_BWD_WEIGHT C[M][N] = X[K][M]^T . dZ[K][N]         (dW_aug = X_aug^T dZ), split over K
+//
+// Matrix cores: v_mfma_f32_32x32x2_f32 (f32 in, f32 accumulate, exact
+// k-ordered fmaf chain, 64 FLOP/clk/SIMD -- the gfx950 f32 peak; there is no
+// xf32 on CDNA4).  A workgroup of 4 wave64s owns a BM x BN tile (64x64 or
+// 128x128), each wave a (TM*32) x (TN*32) sub-tile; K is staged through LDS in
+// 16-deep slices, double-buffered with register prefetch (one barrier per
+// slice).  Both operands live k-major in LDS ([k][m], [k][n]) so each MFMA
+// operand fetch is one conflict-free ds_read_b32 of 32 consecutive floats per
+// half-wave; the row-major operand is transposed while being written to LDS,
+// with a row pad chosen so that those scalar writes are conflict-free too.
+//
+// Epilogues are fused so activations never make an extra HBM round trip:
+//   EPI_TANH       tanh(acc)                                       (Dense(tanh))
+//   EPI_TANH_GRAD  acc * rowscale[m] * (1 - Y^2)                   (TanhGrad)
+//   EPI_BERN       sigmoid -> p*(1-1e-6)+1e-7 (F:126) -> Bernoulli log_prob
+//                  (F:127-F:128) [+ Keras BCE, F:323] row partials per 32
+//                  columns, and the per-element dLoss/dlogit factor g for the
+//                  backward pass; the [rows][784] probabilities never hit HBM.
+#include "iwae_kernels.h"
+
+namespace iwae {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KSCALE>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs a) {
+  constexpr int NTH = WM * WN * 64;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 16;
+  // k-major LDS images.  Transposed (scalar) writes want a row stride = 2 mod 32
+  // floats (conflict-free, see header); float4 writes want a multiple of 4.
+  constexpr int LDSA = BM + (TA ? 4 : 2);
+  constexpr int LDSB = BN + (TB ? 2 : 4);
+  constexpr int A_F4 = (BM * BK / 4) / NTH;
+  constexpr int B_F4 = (BN * BK / 4) / NTH;
+  static_assert(A_F4 * NTH * 4 == BM * BK, "A tile must split evenly");
+  static_assert(B_F4 * NTH * 4 == BN * BK, "B tile must split evenly");
+  constexpr int SMEM = 2 * BK * LDSA + 2 * BK * LDSB;
+  static_assert(SMEM >= WM * WN * 32 * 33, "epilogue scratch must fit");
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
+  float* As = smem;
+  float* Bs = smem + 2 * BK * LDSA;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int kbeg = blockIdx.z * a.kchunk;
+  const int kend = min(a.K, kbeg + a.kchunk);
+  const int M = a.M, N = a.N;
+
+  float4 ra[A_F4], rb[B_F4];
+
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < A_F4; ++i) {
+      const int f = tid + i * NTH;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!TA) {
+        const int mr = f >> 2, kq = f & 3;
+        const int gm = m0 + mr, gk = k0 + 4 * kq;
+        if (gm < M && gk < kend) v = *reinterpret_cast<const float4*>(a.A + (size_t)gm * a.lda + gk);
+      } else {
+        const int kr = f / (BM / 4), mq = f % (BM / 4);
+        const int gk = k0 + kr, gm = m0 + 4 * mq;
+        if (gk < kend && gm < M) v = *reinterpret_cast<const float4*>(a.A + (size_t)gk * a.lda + gm);
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_F4; ++i) {
+      const int f = tid + i * NTH;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!TB) {
+        const int kr = f / (BN / 4), nq = f % (BN / 4);
+        const int gk = k0 + kr, gn = n0 + 4 * nq;
+        if (gk < kend && gn < N) {
+          v = *reinterpret_cast<const float4*>(a.B + (size_t)gk * a.ldb + gn);
+          if (KSCALE) {
+            const float s = a.kscale[gk];
+            v.x *= s; v.y *= s; v.z *= s; v.w *= s;
+          }
+        }
+      } else {
+        const int nr = f >> 2, kq = f & 3;
+        const int gn = n0 + nr, gk = k0 + 4 * kq;
+        if (gn < N && gk < kend) v = *reinterpret_cast<const float4*>(a.B + (size_t)gn * a.ldb + gk);
+      }
+      rb[i] = v;
+    }
+  };
+
+  auto sstore = [&](int buf) {
+    float* Ab = As + buf * BK * LDSA;
+    float* Bb = Bs + buf * BK * LDSB;
+#pragma unroll
+    for (int i = 0; i < A_F4; ++i) {
+      const int f = tid + i * NTH;
+      if (!TA) {
+        const int mr = f >> 2, kq = f & 3;
+        Ab[(4 * kq + 0) * LDSA + mr] = ra[i].x;
+        Ab[(4 * kq + 1) * LDSA + mr] = ra[i].y;
+        Ab[(4 * kq + 2) * LDSA + mr] = ra[i].z;
+        Ab[(4 * kq + 3) * LDSA + mr] = ra[i].w;
+      } else {
+        const int kr = f / (BM / 4), mq = f % (BM / 4);
+        *reinterpret_cast<float4*>(Ab + kr * LDSA + 4 * mq) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_F4; ++i) {
+      const int f = tid + i * NTH;
+      if (!TB) {
+        const int kr = f / (BN / 4), nq = f % (BN / 4);
+        *reinterpret_cast<float4*>(Bb + kr * LDSB + 4 * nq) = rb[i];
+      } else {
+        const int nr = f >> 2, kq = f & 3;
+        Bb[(4 * kq + 0) * LDSB + nr] = rb[i].x;
+        Bb[(4 * kq + 1) * LDSB + nr] = rb[i].y;
+        Bb[(4 * kq + 2) * LDSB + nr] = rb[i].z;
+        Bb[(4 * kq + 3) * LDSB + nr] = rb[i].w;
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nk > 0) {
+    gload(kbeg);
+    sstore(0);
+  }
+  __syncthreads();
+  const int arow = wm * TM * 32 + (lane & 31);
+  const int brow = wn * TN * 32 + (lane & 31);
+  const int khalf = lane >> 5;
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nk) gload(kbeg + (t + 1) * BK);
+    const float* Ab = As + cur * BK * LDSA;
+    const float* Bb = Bs + cur * BK * LDSB;
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      const int kr = 2 * kk + khalf;
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i] = Ab[kr * LDSA + arow + i * 32];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bv[j] = Bb[kr * LDSB + brow + j * 32];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  float* C = a.C + (size_t)blockIdx.z * a.c_split_stride;
+  const int rowq = 4 * (lane >> 5);
+  if (EPI != EPI_BERN) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + rowq;
+          if (m < M && n < N) {
+            float v = acc[i][j][r];
+            if (EPI == EPI_TANH) {
+              v = tanhf(v);
+            } else if (EPI == EPI_TANH_GRAD) {
+              if (a.rowscale) v = v * a.rowscale[m];
+              const float y = a.aux[(size_t)m * a.ldaux + n];
+              v = v * (1.f - y * y);
+            } else {  // EPI_STORE
+              if (a.rowscale) v = v * a.rowscale[m];
+            }
+            C[(size_t)m * a.ldc + n] = v;
+          }
+        }
+      }
+  } else {
+    // Bernoulli epilogue.  Per element: TFP Bernoulli(probs=p).log_prob(x)
+    // = log1p(-p)*(1-x) + log(p)*x with p = sigmoid(l)*(1-1e-6) + 1e-7.
+    float* S = smem + wave * 32 * 33;  // per-wave 32x33 scratch (main loop done)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int ncol0 = n0 + wn * TN * 32 + j * 32;
+        const int n = ncol0 + (lane & 31);
+        float vb[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ml = (r & 3) + 8 * (r >> 2) + rowq;
+          const int m = m0 + wm * TM * 32 + i * 32 + ml;
+          float val = 0.f, bce = 0.f;
+          if (m < M && n < N) {
+            const float l = acc[i][j][r];
+            const float xv = a.aux[(size_t)(m / a.x_row_div) * a.ldaux + n];
+            const float s = 1.f / (1.f + expf(-l));
+            const float p = __fadd_rn(__fmul_rn(s, kProbScale), kProbShift);
+            const float lp1 = logf(p), lp0 = log1pf(-p);
+            val = __fadd_rn(__fmul_rn(lp0, 1.f - xv), __fmul_rn(lp1, xv));
+            float gt = xv / p - (1.f - xv) / (1.f - p);
+            float gb = 0.f;
+            if (a.need_bce || a.wb != 0.f) {
+              const float pc = fminf(fmaxf(p, kKerasEps), 1.f - kKerasEps);
+              if (a.need_bce)
+                bce = xv * logf(pc + kKerasEps) + (1.f - xv) * logf(1.f - pc + kKerasEps);
+              const bool inr = (p >= kKerasEps) && (p <= 1.f - kKerasEps);
+              gb = inr ? (xv / (pc + kKerasEps) - (1.f - xv) / (1.f - pc + kKerasEps)) : 0.f;
+            }
+            if (a.store_g) {
+              const float g = (a.wa * gt + a.wb * gb) * kProbScale * (s * (1.f - s));
+              C[(size_t)m * a.ldc + n] = g;
+            }
+          }
+          S[ml * 33 + (lane & 31)] = val;
+          vb[r] = bce;
+        }
+        __syncthreads();
+        {
+          const int row = lane & 31, half = lane >> 5;
+          float sum = 0.f;
+#pragma unroll
+          for (int c = 0; c < 16; ++c) sum += S[row * 33 + 16 * half + c];
+          sum += __shfl_xor(sum, 32);
+          const int m = m0 + wm * TM * 32 + i * 32 + row;
+          if (half == 0 && m < M && ncol0 < N) a.part[(size_t)m * a.ldpart + ncol0 / 32] = sum;
+        }
+        __syncthreads();
+        if (a.need_bce) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int ml = (r & 3) + 8 * (r >> 2) + rowq;
+            S[ml * 33 + (lane & 31)] = vb[r];
+          }
+          __syncthreads();
+          const int row = lane & 31, half = lane >> 5;
+          float sum = 0.f;
+#pragma unroll
+          for (int c = 0; c < 16; ++c) sum += S[row * 33 + 16 * half + c];
+          sum += __shfl_xor(sum, 32);
+          const int m = m0 + wm * TM * 32 + i * 32 + row;
+          if (half == 0 && m < M && ncol0 < N) a.part2[(size_t)m * a.ldpart + ncol0 / 32] = sum;
+          __syncthreads();
+        }
+      }
+  }
+}
+
+template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KS>
+static hipError_t launch_t(hipStream_t st, int splits, const GemmArgs& a) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, splits);
+  hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, TA, TB, EPI, KS>), grid, dim3(WM * WN * 64), 0,
+                     st, a);
+  return hipGetLastError();
+}
+
+template <int WM, int WN, int TM, int TN>
+static hipError_t dispatch_tile(hipStream_t st, GemmKind kind, GemmEpi epi, int splits, bool ks,
+                                const GemmArgs& a) {
+  switch (kind) {
+    case GEMM_FWD:
+      if (epi == EPI_TANH) return launch_t<WM, WN, TM, TN, false, false, EPI_TANH, false>(st, splits, a);
+      if (epi == EPI_BERN) return launch_t<WM, WN, TM, TN, false, false, EPI_BERN, false>(st, splits, a);
+      if (epi == EPI_STORE) return launch_t<WM, WN, TM, TN, false, false, EPI_STORE, false>(st, splits, a);
+      break;
+    case GEMM_BWD_DATA:
+      if (epi == EPI_TANH_GRAD)
+        return launch_t<WM, WN, TM, TN, false, true, EPI_TANH_GRAD, false>(st, splits, a);
+      if (epi == EPI_STORE) return launch_t<WM, WN, TM, TN, false, true, EPI_STORE, false>(st, splits, a);
+      break;
+    case GEMM_BWD_WEIGHT:
+      if (epi == EPI_STORE) {
+        if (ks) return launch_t<WM, WN, TM, TN, true, false, EPI_STORE, true>(st, splits, a);
+        return launch_t<WM, WN, TM, TN, true, false, EPI_STORE, false>(st, splits, a);
+      }
+      break;
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_gemm(hipStream_t st, GemmKind kind, GemmEpi epi, int tile, int splits, bool ks,
+                       const GemmArgs& a) {
+  if (a.M <= 0 || a.N <= 0) return hipSuccess;
+  if (tile == 1) return dispatch_tile<2, 2, 2, 2>(st, kind, epi, splits, ks, a);
+  return dispatch_tile<2, 2, 1, 1>(st, kind, epi, splits, ks, a);
+}
+
+}  // namespace iwae

@@ -1,0 +1,142 @@
+// Internal kernel interfaces of libiwae_hip.so (gfx950 only).
+//
+// Storage conventions shared by every kernel:
+//  * all matrices are row-major float32 with a leading dimension that is a
+//    multiple of 4 floats (16 B), so every row starts 16-byte aligned;
+//  * columns between the logical width and the leading dimension are ZERO and
+//    stay zero (buffers are memset at allocation and no kernel writes there),
+//    except the "ones column" of GEMM inputs: an activation X[rows][fin] used as
+//    a Dense input keeps X[:, fin] == 1.0 so that X_aug @ W_aug = X W + b with
+//    W_aug = [W; b] ([fin+1][ld] -- exactly Keras' kernel-then-bias order), and
+//    X_aug^T dZ yields dW and db in one GEMM;
+//  * rows are image-major: row = b*k + s.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace iwae {
+
+constexpr float kProbScale = 0.999999f;      // F:126  (1-10**(-6)) as float32
+constexpr float kProbShift = 1e-7f;          // F:126  10**(-7)
+constexpr float kScaleEps = 1e-6f;           // F:37
+constexpr float kKerasEps = 1e-7f;           // keras.backend.epsilon()
+constexpr float kHalfLog2Pi = 0.918938533204672742f;
+
+// ---------------------------------------------------------------- GEMM ----
+enum GemmKind { GEMM_FWD = 0, GEMM_BWD_DATA = 1, GEMM_BWD_WEIGHT = 2 };
+enum GemmEpi { EPI_STORE = 0, EPI_TANH = 1, EPI_BERN = 2, EPI_TANH_GRAD = 3 };
+
+struct GemmArgs {
+  const float* A; const float* B; float* C;
+  int lda, ldb, ldc;
+  int M, N, K;
+  int kchunk;                 // K range per blockIdx.z (multiple of 16)
+  long long c_split_stride;   // C offset per blockIdx.z (split-K slabs)
+  const float* aux; int ldaux;  // TANH_GRAD: Y (tanh output); BERN: x_in
+  const float* rowscale;      // STORE/TANH_GRAD: C[m][:] *= rowscale[m]
+  const float* kscale;        // BWD_WEIGHT: B[k][:] *= kscale[k]
+  float* part; float* part2; int ldpart;  // BERN: per-32-column row partials
+  int x_row_div;              // BERN: x row = m / x_row_div
+  float wa, wb;               // BERN: g = (wa*dTFP + wb*dBCE) * dp/dlogit
+  int store_g;                // BERN: write g into C
+  int need_bce;               // BERN: write Keras-BCE partials into part2
+};
+
+// tile: 0 = 64x64 (4 waves), 1 = 128x128 (4 waves, 2x2 MFMA tiles each)
+hipError_t launch_gemm(hipStream_t st, GemmKind kind, GemmEpi epi, int tile, int splits,
+                       bool kscale, const GemmArgs& a);
+
+// ------------------------------------------------------------ Gaussians ----
+struct GaussArgs {
+  const float* P; int ldP; int prow_div;   // head output rows (mu | zs), row = r / prow_div
+  int d;
+  float* H; int ldH;                        // sampled / evaluated h
+  const float* eps_a; const float* eps_b;   // injected noise (sample-major [k][Bg][d]) or null
+  int kS, Bsplit, Bimg;                     // samples per image, images in group a, total images
+  uint64_t seed; const uint64_t* rng_base; int layer;
+  float* out; int accumulate;               // per-row log density (set or +=)
+  int M;
+};
+// mode 0: sample h = eps*scale+mu and log N(h; mu, scale)   (Encoder.call F:58-F:70)
+// mode 1: log N(h; mu, scale) of a given h                   (Decoder.get_log_ph F:139-F:140)
+// mode 2: log N(h; 0, 1)                                      (F:135-F:136)
+hipError_t launch_gauss_fwd(hipStream_t st, int mode, const GaussArgs& a);
+
+struct GaussBwdArgs {
+  const float* P; int ldP; int prow_div; int d;
+  const float* H; int ldH;
+  const float* eps_a; const float* eps_b; int kS, Bsplit, Bimg;
+  uint64_t seed; const uint64_t* rng_base; int layer;
+  const float* src[4]; int ldsrc[4]; int nsrc;   // dL/dh contributions (dX outputs)
+  int std_normal;            // this h is h_L: add dL/dlogp * (-h)
+  const float* dlw;          // dL/dlw per row (dL/dlogp = dlw, dL/dlogq = -dlw)
+  float kl_coef; int kl_rows;  // VAE_V1: dL/dKLmean on this head (0 = none)
+  float* dP; int lddP;       // (dmu | dzs) per P row
+  float* dh_out; int ldh_out;  // prior mode: dL/dh of the target
+  int M;                     // rows of H
+};
+// mode 0: backward of an encoder sampling layer -> dP (reduced over prow_div rows)
+// mode 1: backward of a decoder prior head      -> dP (per row) and dh_out
+hipError_t launch_gauss_bwd(hipStream_t st, int mode, const GaussBwdArgs& a);
+
+// --------------------------------------------------------------- bounds ----
+enum BoundMode { BM_VAE = 0, BM_IWAE = 1, BM_POWER = 2, BM_MEDIAN = 3, BM_MIWAE = 4, BM_NONE = 5 };
+
+struct BoundArgs {
+  const float* part; const float* part2; int ldpart, npart;
+  const float* logp; const float* logq;
+  float* lw; float* contrib;
+  float* dlw; float* dpx;               // may be null (no backward)
+  float* dlw2; float* dpx2;             // PIWAE second weighting (encoder), may be null
+  int kS, Bimg, Bsplit;
+  int mode_a; float w_a; int mode_b; float w_b;
+  int mode2;                            // weighting of dlw2 (PIWAE: MIWAE)
+  float p; int k1, k2;
+  float bce_w;                          // objective += bce_w * mean_s(bce row) / Bg
+  float dpx_const; int dpx_is_const;    // dpx = dpx_const instead of dlw
+  float* loss; float loss_sign;         // last block: *loss = loss_sign * sum(contrib) + loss_add
+  const float* loss_add;                // optional device scalar (VAE_V1 KL) ...
+  float loss_add_coef;                  // ... added as loss_add_coef * (*loss_add)
+  unsigned* ticket; uint64_t* rng_base; // last-block bookkeeping
+};
+hipError_t launch_bound(hipStream_t st, const BoundArgs& a);
+
+// per-image LSE over this chunk's rows merged into running (m, s)
+struct LseArgs {
+  const float* part; int ldpart, npart; const float* logp; const float* logq;
+  int kS, Bimg;
+  float* run_m; float* run_s; int init;
+  unsigned* ticket; uint64_t* rng_base;
+};
+hipError_t launch_lse(hipStream_t st, const LseArgs& a);
+hipError_t launch_lse_final(hipStream_t st, const float* m, const float* s, int n, float logk,
+                            float* out);
+
+// VAE_V1 analytic KL: value (mean over rows of sum_d KL) into *out
+hipError_t launch_kl_v1(hipStream_t st, const float* P, int ldP, int d, int rows, float* out);
+
+// ----------------------------------------------------------------- Adam ----
+struct AdamSeg {
+  long long off, n;        // parameter range in the flat internal buffer
+  long long slab_off;      // offset of this segment's slabs in the slab arena
+  int splits;              // number of slabs (0 = read grad buffer)
+};
+struct AdamState {         // device resident (graph-replay safe)
+  float lr, b1, b2, eps;
+  float grad_scale; int pad0;
+  long long t;             // Adam iterations applied so far
+};
+constexpr int kMaxSegs = 64;
+struct AdamArgs {
+  float* param; float* m; float* v; float* grad; const float* slabs;
+  AdamSeg seg[kMaxSegs]; int nseg;
+  int write_grad, do_adam, read_slabs;
+  AdamState* state; unsigned* ticket;
+  float grad_scale_override;   // >0: use this instead of state->grad_scale
+};
+hipError_t launch_adam(hipStream_t st, const AdamArgs& a, long long max_seg_n);
+
+hipError_t launch_fill_col(hipStream_t st, float* buf, int rows, int ld, int col, float v);
+hipError_t launch_transpose_lw(hipStream_t st, const float* lw_img, int Bimg, int kS, float* out);
+
+}  // namespace iwae

@@ -1,0 +1,1099 @@
+// Host side of libiwae_hip.so: model plan, HBM workspace, forward / backward
+// orchestration of the IWAE hot path, Adam, NLL chunking, hipGraph replay and
+// the extern "C" ABI declared in include/iwae.h.
+//
+// Reference call stacks mirrored here (F: = /root/reference/flexible_IWAE.py):
+//   train_step        F:221-F:247 -> get_log_weights F:327-F:351 -> bound -> tape.gradient -> Adam
+//   get_NLL           F:463-F:464 -> get_L_k with k = 5000
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/iwae.h"
+#include "iwae_kernels.h"
+
+using namespace iwae;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+inline int r4(int x) { return (x + 3) & ~3; }
+inline long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
+
+struct DenseL {
+  int fin = 0, fout = 0, ldw = 0;
+  long long off = 0;           // into the internal parameter buffer
+  long long size() const { return (long long)(fin + 1) * ldw; }
+  int max_splits = 1, splits = 1;
+  long long slab_off = 0;
+  int rows_kind = 1;           // 0: image rows (encoder layer 0), 1: sample rows
+};
+
+struct StochL {
+  int fin, H, d;
+  int l1, l2, head;            // dense indices
+};
+
+struct Mat {
+  float* p = nullptr;
+  int ld = 0;
+};
+
+struct LayerBufs {
+  Mat y1, y2, P, dP, dY2, dY1;
+};
+
+struct KerasDense {
+  int di, col0, width;
+};
+
+struct DevState {
+  AdamState adam;
+  uint64_t rng[2];             // [0] next forward's Philox counter, [1] last forward's
+  unsigned tickets[4];         // 0: bound, 1: lse, 2: adam
+  float scalars[8];            // 0: loss, 1: bound value, 2: KL (V1)
+};
+
+// Resolved loss plan (train_step dispatch, F:228-F:241)
+struct Plan {
+  int loss = IWAE_LOSS_IWAE;
+  int B = 0, Bimg = 0, Bsplit = 0, kS = 0;
+  int mode_a = BM_IWAE, mode_b = BM_NONE, mode2 = BM_NONE;
+  float w_a = 1.f, w_b = 0.f;
+  float p = 1.f;
+  int k1 = 0, k2 = 0;
+  int need_bce = 0;
+  float bce_w = 0.f, wa = 1.f, wb = 0.f;
+  int dpx_const = 0;
+  float dpx_val = 0.f;
+  int kl = 0;                  // VAE_V1 analytic KL on the last encoder layer
+  int piwae = 0;
+};
+
+}  // namespace
+
+struct iwae_handle {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  iwae_config cfg{};
+  int L = 0, xdim = 0;
+  std::vector<DenseL> dense;
+  std::vector<StochL> enc, dec;
+  int o1 = -1, o2 = -1, o3 = -1;
+  std::vector<KerasDense> keras;
+  long long nparam_int = 0, nparam_keras = 0;
+  // persistent device state
+  float* params = nullptr;
+  float* adam_m = nullptr;
+  float* adam_v = nullptr;
+  float* grad_own = nullptr;
+  float* grad = nullptr;
+  DevState* ds = nullptr;
+  uint64_t seed = 0x5eed5eedULL;
+  // workspace
+  char* arena = nullptr;
+  size_t arena_bytes = 0;
+  int cap_img = 0, cap_rows = 0;
+  bool cap_train = false;
+  Mat x_in;
+  std::vector<LayerBufs> eb, db;
+  LayerBufs ob;                      // output MLP: y1 = o1, y2 = o2, P = g
+  std::vector<Mat> h, dh_out, dh_prior, dh_dec, dh_enc;
+  float *logq = nullptr, *logp = nullptr, *lw = nullptr, *dlw = nullptr, *dpx = nullptr;
+  float *dlw2 = nullptr, *dpx2 = nullptr, *contrib = nullptr, *part = nullptr, *part2 = nullptr;
+  float *run_m = nullptr, *run_s = nullptr;
+  int ldpart = 0, npart = 0;
+  float* slabs = nullptr;
+  // graphs
+  bool use_graphs = false;
+  std::map<std::vector<long long>, hipGraphExec_t> graphs;
+  // live kernel timing (HIP events around every launch of one GEMM class)
+  int prof_kind = -1, prof_epi = -1;
+  std::vector<hipEvent_t> prof_ev;
+  size_t prof_used = 0;
+  double prof_flop = 0.0;
+};
+
+#define HIPCHK(expr)                                                           \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess) {                                                    \
+      h->err = std::string(#expr) + " -> " + hipGetErrorString(_e);            \
+      return IWAE_EHIP;                                                        \
+    }                                                                          \
+  } while (0)
+
+#define CHK(expr)                                                              \
+  do {                                                                         \
+    int _r = (expr);                                                           \
+    if (_r != IWAE_OK) return _r;                                              \
+  } while (0)
+
+static int fail(iwae_handle* h, int code, const std::string& msg) {
+  h->err = msg;
+  return code;
+}
+
+// ------------------------------------------------------------------ plan
+static int add_dense(iwae_handle* h, int fin, int fout, int rows_kind) {
+  DenseL d;
+  d.fin = fin; d.fout = fout; d.ldw = r4(fout); d.off = h->nparam_int; d.rows_kind = rows_kind;
+  h->nparam_int += d.size();
+  h->dense.push_back(d);
+  return (int)h->dense.size() - 1;
+}
+
+static StochL add_stoch(iwae_handle* h, int fin, int H, int d, int rows_kind) {
+  StochL s{fin, H, d, 0, 0, 0};
+  s.l1 = add_dense(h, fin, H, rows_kind);
+  s.l2 = add_dense(h, H, H, rows_kind);
+  s.head = add_dense(h, H, 2 * d, rows_kind);   // [lmu | lstd] concatenated along N
+  h->keras.push_back({s.l1, 0, H});
+  h->keras.push_back({s.l2, 0, H});
+  h->keras.push_back({s.head, 0, d});
+  h->keras.push_back({s.head, d, d});
+  return s;
+}
+
+static void free_workspace(iwae_handle* h) {
+  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+  h->graphs.clear();
+  if (h->arena) (void)hipFree(h->arena);
+  h->arena = nullptr;
+  h->arena_bytes = 0;
+  h->cap_img = h->cap_rows = 0;
+  h->cap_train = false;
+}
+
+static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
+  if (h->arena && Bimg <= h->cap_img && rows <= h->cap_rows && (!train || h->cap_train)) return IWAE_OK;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  Bimg = std::max(Bimg, h->cap_img);
+  rows = std::max(rows, h->cap_rows);
+  train = train || h->cap_train;
+  free_workspace(h);
+  // ---- layout pass (offsets in floats, 64-float aligned)
+  size_t off = 0;
+  auto take = [&](size_t n) {
+    size_t o = off;
+    off += (n + 63) & ~size_t(63);
+    return o;
+  };
+  struct Pending { Mat* m; size_t o; };
+  std::vector<std::pair<float**, size_t>> vecs;
+  std::vector<Pending> mats;
+  auto mat = [&](Mat& m, int nrows, int width) {
+    m.ld = r4(width);
+    mats.push_back({&m, take((size_t)nrows * m.ld)});
+  };
+  auto vec = [&](float*& p, size_t n) { vecs.push_back({&p, take(n)}); };
+  const int L = h->L;
+  h->eb.assign(L, LayerBufs());
+  h->db.assign(std::max(L - 1, 0), LayerBufs());
+  h->h.assign(L, Mat());
+  h->dh_out.assign(1, Mat());
+  h->dh_prior.assign(L, Mat());
+  h->dh_dec.assign(L, Mat());
+  h->dh_enc.assign(L, Mat());
+  mat(h->x_in, Bimg, h->xdim + 1);
+  for (int i = 0; i < L; ++i) {
+    const StochL& s = h->enc[i];
+    const int R = i == 0 ? Bimg : rows;
+    mat(h->eb[i].y1, R, s.H + 1);
+    mat(h->eb[i].y2, R, s.H + 1);
+    mat(h->eb[i].P, R, 2 * s.d + 1);
+    if (train) {
+      mat(h->eb[i].dP, R, 2 * s.d);
+      mat(h->eb[i].dY2, R, s.H);
+      mat(h->eb[i].dY1, R, s.H);
+    }
+    mat(h->h[i], rows, s.d + 1);
+  }
+  for (int i = 0; i < L - 1; ++i) {
+    const StochL& s = h->dec[i];
+    mat(h->db[i].y1, rows, s.H + 1);
+    mat(h->db[i].y2, rows, s.H + 1);
+    mat(h->db[i].P, rows, 2 * s.d + 1);
+    if (train) {
+      mat(h->db[i].dP, rows, 2 * s.d);
+      mat(h->db[i].dY2, rows, s.H);
+      mat(h->db[i].dY1, rows, s.H);
+    }
+  }
+  const int Hd = h->dense[h->o1].fout;
+  mat(h->ob.y1, rows, Hd + 1);
+  mat(h->ob.y2, rows, Hd + 1);
+  if (train) {
+    mat(h->ob.P, rows, h->xdim);   // g = dLoss/dlogit factor
+    mat(h->ob.dY2, rows, Hd);
+    mat(h->ob.dY1, rows, Hd);
+    const int d0 = h->enc[0].d;
+    mat(h->dh_out[0], rows, d0);
+    for (int i = 0; i < L; ++i) {
+      const int di = h->enc[i].d;
+      if (i <= L - 2) { mat(h->dh_prior[i], rows, di); mat(h->dh_enc[i], rows, di); }
+      if (i >= 1) mat(h->dh_dec[i], rows, di);
+    }
+  }
+  h->npart = (int)cdiv(h->xdim, 32);
+  h->ldpart = r4(h->npart);
+  vec(h->part, (size_t)rows * h->ldpart);
+  vec(h->part2, (size_t)rows * h->ldpart);
+  vec(h->logq, rows); vec(h->logp, rows); vec(h->lw, rows);
+  vec(h->dlw, rows); vec(h->dpx, rows); vec(h->dlw2, rows); vec(h->dpx2, rows);
+  vec(h->contrib, Bimg); vec(h->run_m, Bimg); vec(h->run_s, Bimg);
+  size_t slab_total = 0;
+  if (train) {
+    for (auto& d : h->dense) {
+      const long long R = d.rows_kind == 0 ? Bimg : rows;
+      const long long tiles = cdiv(d.fin + 1, 64) * cdiv(d.fout, 64);
+      long long S = std::max(1LL, cdiv(768, tiles));
+      S = std::min(S, std::max(1LL, cdiv(R, 64)));
+      d.max_splits = (int)S;
+      d.slab_off = (long long)slab_total;
+      slab_total += (size_t)((d.size() * S + 63) & ~63LL);
+    }
+  }
+  size_t slab_base = take(slab_total);
+  const size_t bytes = off * sizeof(float);
+  HIPCHK(hipMalloc(&h->arena, bytes));
+  h->arena_bytes = bytes;
+  HIPCHK(hipMemsetAsync(h->arena, 0, bytes, h->stream));
+  float* base = reinterpret_cast<float*>(h->arena);
+  for (auto& pm : mats) pm.m->p = base + pm.o;
+  for (auto& pv : vecs) *pv.first = base + pv.second;
+  h->slabs = train ? base + slab_base : nullptr;
+  // ones columns of every Dense input (bias folded into W_aug's last row)
+  HIPCHK(launch_fill_col(h->stream, h->x_in.p, Bimg, h->x_in.ld, h->xdim, 1.f));
+  for (int i = 0; i < L; ++i) {
+    const int R = i == 0 ? Bimg : rows;
+    HIPCHK(launch_fill_col(h->stream, h->eb[i].y1.p, R, h->eb[i].y1.ld, h->enc[i].H, 1.f));
+    HIPCHK(launch_fill_col(h->stream, h->eb[i].y2.p, R, h->eb[i].y2.ld, h->enc[i].H, 1.f));
+    HIPCHK(launch_fill_col(h->stream, h->h[i].p, rows, h->h[i].ld, h->enc[i].d, 1.f));
+  }
+  for (int i = 0; i < L - 1; ++i) {
+    HIPCHK(launch_fill_col(h->stream, h->db[i].y1.p, rows, h->db[i].y1.ld, h->dec[i].H, 1.f));
+    HIPCHK(launch_fill_col(h->stream, h->db[i].y2.p, rows, h->db[i].y2.ld, h->dec[i].H, 1.f));
+  }
+  HIPCHK(launch_fill_col(h->stream, h->ob.y1.p, rows, h->ob.y1.ld, Hd, 1.f));
+  HIPCHK(launch_fill_col(h->stream, h->ob.y2.p, rows, h->ob.y2.ld, Hd, 1.f));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->cap_img = Bimg;
+  h->cap_rows = rows;
+  h->cap_train = train;
+  return IWAE_OK;
+}
+
+// --------------------------------------------------------------- GEMMs
+static int choose_tile(long long M, long long N, int splits) {
+  return (cdiv(M, 128) * cdiv(N, 128) * splits >= 512) ? 1 : 0;
+}
+
+static bool prof_match(iwae_handle* h, GemmKind kind, GemmEpi epi) {
+  return h->prof_kind == (int)kind && h->prof_epi == (int)epi;
+}
+
+static int prof_begin(iwae_handle* h, GemmKind kind, GemmEpi epi, double flop) {
+  if (!prof_match(h, kind, epi)) return IWAE_OK;
+  if (h->prof_used + 2 > h->prof_ev.size()) {
+    for (int i = 0; i < 256; ++i) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      h->prof_ev.push_back(e);
+    }
+  }
+  HIPCHK(hipEventRecord(h->prof_ev[h->prof_used], h->stream));
+  h->prof_flop += flop;
+  return IWAE_OK;
+}
+
+static int prof_end(iwae_handle* h, GemmKind kind, GemmEpi epi) {
+  if (!prof_match(h, kind, epi)) return IWAE_OK;
+  HIPCHK(hipEventRecord(h->prof_ev[h->prof_used + 1], h->stream));
+  h->prof_used += 2;
+  return IWAE_OK;
+}
+
+static int gemm_fwd(iwae_handle* h, GemmEpi epi, const Mat& X, int rows, const DenseL& d, Mat& Y,
+                    GemmArgs extra = GemmArgs{}) {
+  GemmArgs a = extra;
+  a.A = X.p; a.lda = X.ld;
+  a.B = h->params + d.off; a.ldb = d.ldw;
+  a.C = Y.p; a.ldc = Y.ld;
+  a.M = rows; a.N = d.fout; a.K = d.fin + 1;
+  a.kchunk = a.K;
+  a.c_split_stride = 0;
+  CHK(prof_begin(h, GEMM_FWD, epi, 2.0 * rows * d.fout * d.fin));
+  HIPCHK(launch_gemm(h->stream, GEMM_FWD, epi, choose_tile(a.M, a.N, 1), 1, false, a));
+  CHK(prof_end(h, GEMM_FWD, epi));
+  return IWAE_OK;
+}
+
+// dX[rows][fin] = dZ[rows][fout] . W[:fin]^T  (optionally * rowscale, * (1-Y^2))
+static int gemm_bwd_data(iwae_handle* h, const Mat& dZ, int rows, const DenseL& d, Mat& dX,
+                         const Mat* Y, const float* rowscale) {
+  GemmArgs a{};
+  a.A = dZ.p; a.lda = dZ.ld;
+  a.B = h->params + d.off; a.ldb = d.ldw;
+  a.C = dX.p; a.ldc = dX.ld;
+  a.M = rows; a.N = d.fin; a.K = d.fout;
+  a.kchunk = a.K;
+  a.rowscale = rowscale;
+  GemmEpi epi = EPI_STORE;
+  if (Y) { a.aux = Y->p; a.ldaux = Y->ld; epi = EPI_TANH_GRAD; }
+  CHK(prof_begin(h, GEMM_BWD_DATA, epi, 2.0 * rows * d.fout * d.fin));
+  HIPCHK(launch_gemm(h->stream, GEMM_BWD_DATA, epi, choose_tile(a.M, a.N, 1), 1, false, a));
+  CHK(prof_end(h, GEMM_BWD_DATA, epi));
+  return IWAE_OK;
+}
+
+// slabs of dW_aug[fin+1][fout] = X_aug[rows][fin+1]^T . dZ[rows][fout], split over rows
+static int gemm_bwd_weight(iwae_handle* h, const Mat& X, const Mat& dZ, int rows, DenseL& d,
+                           const float* kscale) {
+  GemmArgs a{};
+  a.A = X.p; a.lda = X.ld;
+  a.B = dZ.p; a.ldb = dZ.ld;
+  a.C = h->slabs + d.slab_off; a.ldc = d.ldw;
+  a.M = d.fin + 1; a.N = d.fout; a.K = rows;
+  long long S = std::min<long long>(d.max_splits, std::max(1LL, cdiv(rows, 64)));
+  int kchunk = (int)(cdiv(cdiv(rows, S), 16) * 16);
+  S = cdiv(rows, kchunk);
+  d.splits = (int)S;
+  a.kchunk = kchunk;
+  a.c_split_stride = d.size();
+  a.kscale = kscale;
+  CHK(prof_begin(h, GEMM_BWD_WEIGHT, EPI_STORE, 2.0 * rows * d.fout * (d.fin + 1)));
+  HIPCHK(launch_gemm(h->stream, GEMM_BWD_WEIGHT, EPI_STORE, 0, (int)S, kscale != nullptr, a));
+  CHK(prof_end(h, GEMM_BWD_WEIGHT, EPI_STORE));
+  return IWAE_OK;
+}
+
+static int stoch_fwd(iwae_handle* h, const StochL& s, const Mat& in, int rows, LayerBufs& b) {
+  CHK(gemm_fwd(h, EPI_TANH, in, rows, h->dense[s.l1], b.y1));
+  CHK(gemm_fwd(h, EPI_TANH, b.y1, rows, h->dense[s.l2], b.y2));
+  CHK(gemm_fwd(h, EPI_STORE, b.y2, rows, h->dense[s.head], b.P));
+  return IWAE_OK;
+}
+
+static int stoch_bwd(iwae_handle* h, const StochL& s, const Mat& in, int rows, LayerBufs& b, bool do_dw,
+                     Mat* dx) {
+  CHK(gemm_bwd_data(h, b.dP, rows, h->dense[s.head], b.dY2, &b.y2, nullptr));
+  if (do_dw) CHK(gemm_bwd_weight(h, b.y2, b.dP, rows, h->dense[s.head], nullptr));
+  CHK(gemm_bwd_data(h, b.dY2, rows, h->dense[s.l2], b.dY1, &b.y1, nullptr));
+  if (do_dw) CHK(gemm_bwd_weight(h, b.y1, b.dY2, rows, h->dense[s.l2], nullptr));
+  if (dx) CHK(gemm_bwd_data(h, b.dY1, rows, h->dense[s.l1], *dx, nullptr, nullptr));
+  if (do_dw) CHK(gemm_bwd_weight(h, in, b.dY1, rows, h->dense[s.l1], nullptr));
+  return IWAE_OK;
+}
+
+// ------------------------------------------------------------ loss plan
+static int make_plan(iwae_handle* h, const iwae_loss_config* lc, int B, Plan& P) {
+  if (!lc) return fail(h, IWAE_EINVAL, "loss config is NULL");
+  if (B <= 0) return fail(h, IWAE_EINVAL, "batch must be positive");
+  if (lc->k <= 0) return fail(h, IWAE_EINVAL, "k must be positive");
+  P = Plan();
+  P.loss = lc->loss;
+  P.B = B; P.Bimg = B; P.Bsplit = B; P.kS = lc->k;
+  P.p = lc->p;
+  switch (lc->loss) {
+    case IWAE_LOSS_VAE: P.mode_a = BM_VAE; break;
+    case IWAE_LOSS_IWAE: P.mode_a = BM_IWAE; break;
+    case IWAE_LOSS_L_POWER_P:
+      if (!(lc->p > 0.f) && !(lc->p < 0.f)) return fail(h, IWAE_EINVAL, "L_power_p needs p != 0");
+      P.mode_a = BM_POWER; break;
+    case IWAE_LOSS_L_MEDIAN:
+      if (lc->k > 1024) return fail(h, IWAE_EINVAL, "L_median supports k <= 1024");
+      P.mode_a = BM_MEDIAN; break;
+    case IWAE_LOSS_MIWAE:
+    case IWAE_LOSS_PIWAE:
+      if (lc->k1 <= 0 || lc->k2 <= 0 || lc->k1 * lc->k2 != lc->k)
+        return fail(h, IWAE_EINVAL, "MIWAE/PIWAE need k1*k2 == k");
+      P.k1 = lc->k1; P.k2 = lc->k2;
+      if (lc->loss == IWAE_LOSS_MIWAE) {
+        P.mode_a = BM_MIWAE;
+      } else {
+        P.mode_a = BM_IWAE; P.mode2 = BM_MIWAE; P.piwae = 1;
+      }
+      break;
+    case IWAE_LOSS_CIWAE:
+      P.Bimg = 2 * B; P.Bsplit = B;
+      P.mode_a = BM_VAE; P.w_a = lc->beta;            // beta * get_L      (F:383)
+      P.mode_b = BM_IWAE; P.w_b = 1.f - lc->beta;     // (1-beta) * get_L_k
+      break;
+    case IWAE_LOSS_L_ALPHA:
+      P.mode_a = BM_VAE; P.w_a = lc->alpha;            // alpha * L          (F:401)
+      P.need_bce = 1; P.bce_w = 1.f - lc->alpha;       // (1-alpha) * E_q log p(x|h)
+      P.wa = lc->alpha; P.wb = 1.f - lc->alpha;
+      P.dpx_const = 1; P.dpx_val = -1.f / ((float)lc->k * (float)B);
+      break;
+    case IWAE_LOSS_VAE_V1:
+      P.mode_a = BM_NONE; P.w_a = 0.f;
+      P.need_bce = 1; P.bce_w = 1.f;                   // E_q log p(x|h) (F:456) - KL (F:458)
+      P.wa = 0.f; P.wb = 1.f;
+      P.dpx_const = 1; P.dpx_val = -1.f / ((float)lc->k * (float)B);
+      P.kl = 1;
+      break;
+    default:
+      return fail(h, IWAE_EINVAL, "unknown loss_function id " + std::to_string(lc->loss));
+  }
+  return IWAE_OK;
+}
+
+// ------------------------------------------------------------- forward
+struct EpsSet {
+  const float* a[IWAE_MAX_LAYERS];
+  const float* b[IWAE_MAX_LAYERS];
+};
+
+static int parse_eps(iwae_handle* h, const Plan& P, const float* const* eps, int n_eps, EpsSet& E) {
+  std::memset(&E, 0, sizeof(E));
+  if (!eps || n_eps == 0) return IWAE_OK;
+  const int need = (P.Bimg != P.Bsplit) ? 2 * h->L : h->L;
+  if (n_eps != need)
+    return fail(h, IWAE_EINVAL, "expected " + std::to_string(need) + " eps buffers, got " +
+                                   std::to_string(n_eps));
+  for (int i = 0; i < h->L; ++i) {
+    E.a[i] = eps[i];
+    if (P.Bimg != P.Bsplit) E.b[i] = eps[h->L + i];
+    if (!E.a[i] || (P.Bimg != P.Bsplit && !E.b[i])) return fail(h, IWAE_EINVAL, "NULL eps buffer");
+  }
+  return IWAE_OK;
+}
+
+// Encoder + prior + output layer.  Leaves part/logp/logq (and g when train).
+static int forward_core(iwae_handle* h, const Plan& P, const EpsSet& E, bool train) {
+  const int L = h->L, kS = P.kS, M = P.Bimg * kS;
+  // encoder (F:56-F:75)
+  CHK(stoch_fwd(h, h->enc[0], h->x_in, P.Bimg, h->eb[0]));
+  for (int i = 0; i < L; ++i) {
+    if (i > 0) CHK(stoch_fwd(h, h->enc[i], h->h[i - 1], M, h->eb[i]));
+    GaussArgs g{};
+    g.P = h->eb[i].P.p; g.ldP = h->eb[i].P.ld; g.prow_div = i == 0 ? kS : 1; g.d = h->enc[i].d;
+    g.H = h->h[i].p; g.ldH = h->h[i].ld;
+    g.eps_a = E.a[i]; g.eps_b = E.b[i];
+    g.kS = kS; g.Bsplit = P.Bsplit; g.Bimg = P.Bimg;
+    g.seed = h->seed; g.rng_base = &h->ds->rng[0]; g.layer = i;
+    g.out = h->logq; g.accumulate = i > 0; g.M = M;
+    HIPCHK(launch_gauss_fwd(h->stream, 0, g));
+  }
+  // prior log p(h) (F:134-F:142)
+  {
+    GaussArgs g{};
+    g.d = h->enc[L - 1].d; g.H = h->h[L - 1].p; g.ldH = h->h[L - 1].ld;
+    g.out = h->logp; g.accumulate = 0; g.M = M;
+    HIPCHK(launch_gauss_fwd(h->stream, 2, g));
+  }
+  for (int i = 0; i < L - 1; ++i) {
+    CHK(stoch_fwd(h, h->dec[i], h->h[L - 1 - i], M, h->db[i]));
+    GaussArgs g{};
+    g.P = h->db[i].P.p; g.ldP = h->db[i].P.ld; g.prow_div = 1; g.d = h->dec[i].d;
+    g.H = h->h[L - 2 - i].p; g.ldH = h->h[L - 2 - i].ld;
+    g.out = h->logp; g.accumulate = 1; g.M = M;
+    HIPCHK(launch_gauss_fwd(h->stream, 1, g));
+  }
+  // output MLP + Bernoulli (F:89-F:96, F:123-F:129)
+  CHK(gemm_fwd(h, EPI_TANH, h->h[0], M, h->dense[h->o1], h->ob.y1));
+  CHK(gemm_fwd(h, EPI_TANH, h->ob.y1, M, h->dense[h->o2], h->ob.y2));
+  {
+    GemmArgs ex{};
+    ex.aux = h->x_in.p; ex.ldaux = h->x_in.ld; ex.x_row_div = kS;
+    ex.part = h->part; ex.part2 = h->part2; ex.ldpart = h->ldpart;
+    ex.wa = P.wa; ex.wb = P.wb;
+    ex.store_g = train ? 1 : 0;
+    ex.need_bce = P.need_bce;
+    Mat gm = h->ob.P;
+    if (!train) { gm.p = nullptr; gm.ld = 0; }
+    CHK(gemm_fwd(h, EPI_BERN, h->ob.y2, M, h->dense[h->o3], gm, ex));
+  }
+  return IWAE_OK;
+}
+
+static int run_bound(iwae_handle* h, const Plan& P, bool train, float sign, float* value_out) {
+  if (P.kl) {
+    const int Lm1 = h->L - 1;
+    const int rows = Lm1 == 0 ? P.Bimg : P.Bimg * P.kS;
+    HIPCHK(launch_kl_v1(h->stream, h->eb[Lm1].P.p, h->eb[Lm1].P.ld, h->enc[Lm1].d, rows,
+                        &h->ds->scalars[2]));
+  }
+  BoundArgs b{};
+  b.part = h->part; b.part2 = P.need_bce ? h->part2 : nullptr; b.ldpart = h->ldpart; b.npart = h->npart;
+  b.logp = h->logp; b.logq = h->logq;
+  b.lw = h->lw; b.contrib = h->contrib;
+  b.dlw = train ? h->dlw : nullptr; b.dpx = train ? h->dpx : nullptr;
+  b.dlw2 = (train && P.piwae) ? h->dlw2 : nullptr; b.dpx2 = (train && P.piwae) ? h->dpx2 : nullptr;
+  b.kS = P.kS; b.Bimg = P.Bimg; b.Bsplit = P.Bsplit;
+  b.mode_a = P.mode_a; b.w_a = P.w_a; b.mode_b = P.mode_b; b.w_b = P.w_b; b.mode2 = P.mode2;
+  b.p = P.p; b.k1 = P.k1; b.k2 = P.k2;
+  b.bce_w = P.bce_w; b.dpx_const = P.dpx_val; b.dpx_is_const = P.dpx_const;
+  b.loss = value_out; b.loss_sign = sign;
+  b.loss_add = nullptr;
+  if (P.kl) {
+    // training loss = -(E - KL) = -E + KL ; bound value = E - KL  (F:459)
+    b.loss_add = &h->ds->scalars[2];
+    b.loss_add_coef = sign > 0 ? -1.f : 1.f;
+  }
+  b.ticket = &h->ds->tickets[0]; b.rng_base = &h->ds->rng[0];
+  HIPCHK(launch_bound(h->stream, b));
+  return IWAE_OK;
+}
+
+// --------------------------------------------------------------- backward
+static int decoder_bwd(iwae_handle* h, const Plan& P, const float* dlw, const float* dpx, bool do_dw,
+                       bool do_dx) {
+  const int L = h->L, M = P.Bimg * P.kS;
+  // output MLP: dlogit = dpx[row] * g
+  CHK(gemm_bwd_data(h, h->ob.P, M, h->dense[h->o3], h->ob.dY2, &h->ob.y2, dpx));
+  if (do_dw) CHK(gemm_bwd_weight(h, h->ob.y2, h->ob.P, M, h->dense[h->o3], dpx));
+  CHK(gemm_bwd_data(h, h->ob.dY2, M, h->dense[h->o2], h->ob.dY1, &h->ob.y1, nullptr));
+  if (do_dw) CHK(gemm_bwd_weight(h, h->ob.y1, h->ob.dY2, M, h->dense[h->o2], nullptr));
+  if (do_dx) CHK(gemm_bwd_data(h, h->ob.dY1, M, h->dense[h->o1], h->dh_out[0], nullptr, nullptr));
+  if (do_dw) CHK(gemm_bwd_weight(h, h->h[0], h->ob.dY1, M, h->dense[h->o1], nullptr));
+  // decoder prior layers p(h_t | h_src)
+  for (int i = 0; i < L - 1; ++i) {
+    const int t = L - 2 - i, src = L - 1 - i;
+    GaussBwdArgs g{};
+    g.P = h->db[i].P.p; g.ldP = h->db[i].P.ld; g.prow_div = 1; g.d = h->dec[i].d;
+    g.H = h->h[t].p; g.ldH = h->h[t].ld;
+    g.dlw = dlw;
+    g.dP = h->db[i].dP.p; g.lddP = h->db[i].dP.ld;
+    g.dh_out = h->dh_prior[t].p; g.ldh_out = h->dh_prior[t].ld;
+    g.M = M;
+    HIPCHK(launch_gauss_bwd(h->stream, 1, g));
+    CHK(stoch_bwd(h, h->dec[i], h->h[src], M, h->db[i], do_dw, do_dx ? &h->dh_dec[src] : nullptr));
+  }
+  return IWAE_OK;
+}
+
+static int encoder_bwd(iwae_handle* h, const Plan& P, const EpsSet& E, const float* dlw) {
+  const int L = h->L, kS = P.kS, M = P.Bimg * kS;
+  for (int i = L - 1; i >= 0; --i) {
+    GaussBwdArgs g{};
+    g.P = h->eb[i].P.p; g.ldP = h->eb[i].P.ld; g.prow_div = i == 0 ? kS : 1; g.d = h->enc[i].d;
+    g.H = h->h[i].p; g.ldH = h->h[i].ld;
+    g.eps_a = E.a[i]; g.eps_b = E.b[i]; g.kS = kS; g.Bsplit = P.Bsplit; g.Bimg = P.Bimg;
+    g.seed = h->seed; g.rng_base = &h->ds->rng[1]; g.layer = i;
+    int n = 0;
+    if (i == 0) { g.src[n] = h->dh_out[0].p; g.ldsrc[n++] = h->dh_out[0].ld; }
+    if (i <= L - 2) {
+      g.src[n] = h->dh_prior[i].p; g.ldsrc[n++] = h->dh_prior[i].ld;
+      g.src[n] = h->dh_enc[i].p; g.ldsrc[n++] = h->dh_enc[i].ld;
+    }
+    if (i >= 1) { g.src[n] = h->dh_dec[i].p; g.ldsrc[n++] = h->dh_dec[i].ld; }
+    g.nsrc = n;
+    g.std_normal = i == L - 1;
+    g.dlw = dlw;
+    if (P.kl && i == L - 1) {
+      g.kl_coef = 1.f;   // dLoss/dKL_mean for loss = -(E - KL)
+      g.kl_rows = (L == 1) ? P.Bimg : M;
+    }
+    g.dP = h->eb[i].dP.p; g.lddP = h->eb[i].dP.ld;
+    g.M = M;
+    HIPCHK(launch_gauss_bwd(h->stream, 0, g));
+    const Mat& in = i == 0 ? h->x_in : h->h[i - 1];
+    const int rows = i == 0 ? P.Bimg : M;
+    CHK(stoch_bwd(h, h->enc[i], in, rows, h->eb[i], true, i > 0 ? &h->dh_enc[i - 1] : nullptr));
+  }
+  return IWAE_OK;
+}
+
+static int run_adam(iwae_handle* h, bool read_slabs, bool write_grad, bool do_adam, float scale_override) {
+  AdamArgs a{};
+  a.param = h->params; a.m = h->adam_m; a.v = h->adam_v; a.grad = h->grad; a.slabs = h->slabs;
+  long long mx = 0;
+  for (size_t i = 0; i < h->dense.size(); ++i) {
+    const DenseL& d = h->dense[i];
+    a.seg[i].off = d.off; a.seg[i].n = d.size(); a.seg[i].slab_off = d.slab_off;
+    a.seg[i].splits = read_slabs ? d.splits : 0;
+    mx = std::max(mx, d.size());
+  }
+  a.nseg = (int)h->dense.size();
+  a.write_grad = write_grad; a.do_adam = do_adam; a.read_slabs = read_slabs;
+  a.state = &h->ds->adam; a.ticket = &h->ds->tickets[2];
+  a.grad_scale_override = scale_override;
+  HIPCHK(launch_adam(h->stream, a, mx));
+  return IWAE_OK;
+}
+
+static int copy_x(iwae_handle* h, const Plan& P, const float* x) {
+  const size_t wbytes = (size_t)h->xdim * sizeof(float);
+  HIPCHK(hipMemcpy2DAsync(h->x_in.p, (size_t)h->x_in.ld * sizeof(float), x, wbytes, wbytes, P.B,
+                          hipMemcpyDeviceToDevice, h->stream));
+  if (P.Bimg != P.B) {
+    HIPCHK(hipMemcpy2DAsync(h->x_in.p + (size_t)P.B * h->x_in.ld, (size_t)h->x_in.ld * sizeof(float), x,
+                            wbytes, wbytes, P.B, hipMemcpyDeviceToDevice, h->stream));
+  }
+  return IWAE_OK;
+}
+
+// forward + backward (+ Adam) after x is staged
+static int train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
+  CHK(forward_core(h, P, E, true));
+  CHK(run_bound(h, P, true, -1.f, &h->ds->scalars[0]));
+  if (P.piwae) {
+    CHK(decoder_bwd(h, P, h->dlw, h->dpx, true, false));      // decoder: IWAE_{k1 k2}
+    CHK(decoder_bwd(h, P, h->dlw2, h->dpx2, false, true));    // encoder path: MIWAE(k1,k2)
+    CHK(encoder_bwd(h, P, E, h->dlw2));
+  } else {
+    CHK(decoder_bwd(h, P, h->dlw, h->dpx, true, true));
+    CHK(encoder_bwd(h, P, E, h->dlw));
+  }
+  CHK(run_adam(h, true, true, adam, 1.f));
+  return IWAE_OK;
+}
+
+static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,
+                    const float* const* eps, int n_eps, float* loss_dev, bool adam) {
+  if (!x) return fail(h, IWAE_EINVAL, "x is NULL");
+  Plan P;
+  CHK(make_plan(h, lc, B, P));
+  EpsSet E;
+  CHK(parse_eps(h, P, eps, n_eps, E));
+  CHK(ensure_capacity(h, P.Bimg, P.Bimg * P.kS, true));
+  CHK(copy_x(h, P, x));
+  const bool philox = (E.a[0] == nullptr);
+  if (h->use_graphs && philox && h->prof_kind < 0) {
+    std::vector<long long> key = {adam ? 1 : 0, lc->loss, B, lc->k, lc->k1, lc->k2};
+    float fk[3] = {lc->p, lc->alpha, lc->beta};
+    for (float f : fk) {
+      int bits;
+      std::memcpy(&bits, &f, 4);
+      key.push_back(bits);
+    }
+    auto it = h->graphs.find(key);
+    if (it == h->graphs.end()) {
+      hipGraph_t graph;
+      HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
+      int rc = train_body(h, P, E, adam);
+      hipError_t ec = hipStreamEndCapture(h->stream, &graph);
+      if (rc != IWAE_OK) return rc;
+      HIPCHK(ec);
+      hipGraphExec_t exec;
+      HIPCHK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+      HIPCHK(hipGraphDestroy(graph));
+      it = h->graphs.emplace(key, exec).first;
+    }
+    HIPCHK(hipGraphLaunch(it->second, h->stream));
+  } else {
+    CHK(train_body(h, P, E, adam));
+  }
+  if (loss_dev)
+    HIPCHK(hipMemcpyAsync(loss_dev, &h->ds->scalars[0], sizeof(float), hipMemcpyDeviceToDevice, h->stream));
+  return IWAE_OK;
+}
+
+// ---------------------------------------------------------------- ABI
+extern "C" {
+
+iwae_handle* iwae_create(const iwae_config* cfg, int device) {
+  g_create_error.clear();
+  if (!cfg) { g_create_error = "config is NULL"; return nullptr; }
+  const int L = cfg->n_stochastic;
+  if (L < 1 || L > IWAE_MAX_LAYERS) { g_create_error = "n_stochastic must be in [1, 8]"; return nullptr; }
+  if (cfg->x_dim <= 0) { g_create_error = "x_dim must be positive"; return nullptr; }
+  for (int i = 0; i < L; ++i) {
+    if (cfg->n_hidden_encoder[i] <= 0 || cfg->n_latent_encoder[i] <= 0 || cfg->n_hidden_decoder[i] <= 0) {
+      g_create_error = "layer sizes must be positive";
+      return nullptr;
+    }
+  }
+  for (int i = 0; i < L - 1; ++i) {
+    if (cfg->n_latent_decoder[i] != cfg->n_latent_encoder[L - 2 - i]) {
+      g_create_error = "n_latent_decoder[" + std::to_string(i) + "] must equal n_latent_encoder[" +
+                       std::to_string(L - 2 - i) + "]";
+      return nullptr;
+    }
+  }
+  if (hipSetDevice(device) != hipSuccess) {
+    g_create_error = "hipSetDevice failed (no GPU?)";
+    return nullptr;
+  }
+  iwae_handle* h = new iwae_handle();
+  h->device = device;
+  h->cfg = *cfg;
+  h->L = L;
+  h->xdim = cfg->x_dim;
+  // encoder stochastic layers (F:48-F:49), decoder prior layers (F:86-F:87), output MLP (F:89-F:96)
+  for (int i = 0; i < L; ++i) {
+    const int fin = i == 0 ? cfg->x_dim : cfg->n_latent_encoder[i - 1];
+    h->enc.push_back(add_stoch(h, fin, cfg->n_hidden_encoder[i], cfg->n_latent_encoder[i], i == 0 ? 0 : 1));
+  }
+  for (int i = 0; i < L - 1; ++i) {
+    h->dec.push_back(add_stoch(h, cfg->n_latent_encoder[L - 1 - i], cfg->n_hidden_decoder[i],
+                               cfg->n_latent_decoder[i], 1));
+  }
+  const int Hd = cfg->n_hidden_decoder[L - 1];
+  h->o1 = add_dense(h, cfg->n_latent_encoder[0], Hd, 1);
+  h->o2 = add_dense(h, Hd, Hd, 1);
+  h->o3 = add_dense(h, Hd, cfg->x_dim, 1);
+  h->keras.push_back({h->o1, 0, Hd});
+  h->keras.push_back({h->o2, 0, Hd});
+  h->keras.push_back({h->o3, 0, cfg->x_dim});
+  for (auto& k : h->keras) h->nparam_keras += (long long)(h->dense[k.di].fin + 1) * k.width;
+  hipError_t e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
+  h->stream = h->own_stream;
+  const size_t pb = (size_t)h->nparam_int * sizeof(float);
+  if (e == hipSuccess) e = hipMalloc(&h->params, pb);
+  if (e == hipSuccess) e = hipMalloc(&h->adam_m, pb);
+  if (e == hipSuccess) e = hipMalloc(&h->adam_v, pb);
+  if (e == hipSuccess) e = hipMalloc(&h->grad_own, pb);
+  if (e == hipSuccess) e = hipMalloc(&h->ds, sizeof(DevState));
+  if (e == hipSuccess) e = hipMemset(h->params, 0, pb);
+  if (e == hipSuccess) e = hipMemset(h->adam_m, 0, pb);
+  if (e == hipSuccess) e = hipMemset(h->adam_v, 0, pb);
+  if (e == hipSuccess) e = hipMemset(h->grad_own, 0, pb);
+  if (e == hipSuccess) {
+    DevState s{};
+    s.adam.lr = 1e-3f; s.adam.b1 = 0.9f; s.adam.b2 = 0.999f; s.adam.eps = 1e-7f;  // Keras defaults
+    s.adam.grad_scale = 1.f; s.adam.t = 0;
+    e = hipMemcpy(h->ds, &s, sizeof(s), hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) {
+    g_create_error = std::string("device allocation failed: ") + hipGetErrorString(e);
+    iwae_destroy(h);
+    return nullptr;
+  }
+  h->grad = h->grad_own;
+  return h;
+}
+
+const char* iwae_create_error(void) { return g_create_error.c_str(); }
+
+void iwae_destroy(iwae_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  free_workspace(h);
+  for (auto e : h->prof_ev) (void)hipEventDestroy(e);
+  if (h->params) (void)hipFree(h->params);
+  if (h->adam_m) (void)hipFree(h->adam_m);
+  if (h->adam_v) (void)hipFree(h->adam_v);
+  if (h->grad_own) (void)hipFree(h->grad_own);
+  if (h->ds) (void)hipFree(h->ds);
+  if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+  delete h;
+}
+
+const char* iwae_last_error(const iwae_handle* h) { return h ? h->err.c_str() : "NULL handle"; }
+
+int iwae_set_stream(iwae_handle* h, void* s) {
+  if (!h) return IWAE_EINVAL;
+  h->stream = s ? (hipStream_t)s : h->own_stream;
+  return IWAE_OK;
+}
+
+int iwae_synchronize(iwae_handle* h) {
+  if (!h) return IWAE_EINVAL;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return IWAE_OK;
+}
+
+int iwae_set_seed(iwae_handle* h, unsigned long long seed) {
+  if (!h) return IWAE_EINVAL;
+  h->seed = seed;
+  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);   // seed is a captured kernel argument
+  h->graphs.clear();
+  uint64_t z[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(h->ds->rng, z, sizeof(z), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return IWAE_OK;
+}
+
+int iwae_set_graphs(iwae_handle* h, int enable) {
+  if (!h) return IWAE_EINVAL;
+  h->use_graphs = enable != 0;
+  return IWAE_OK;
+}
+
+long long iwae_num_params(const iwae_handle* h) { return h ? h->nparam_keras : -1; }
+
+static void keras_to_internal(const iwae_handle* h, const float* src, std::vector<float>& dst) {
+  dst.assign((size_t)h->nparam_int, 0.f);
+  long long o = 0;
+  for (const auto& k : h->keras) {
+    const DenseL& d = h->dense[k.di];
+    for (int r = 0; r < d.fin; ++r)
+      for (int j = 0; j < k.width; ++j) dst[d.off + (long long)r * d.ldw + k.col0 + j] = src[o++];
+    for (int j = 0; j < k.width; ++j) dst[d.off + (long long)d.fin * d.ldw + k.col0 + j] = src[o++];
+  }
+}
+
+static void internal_to_keras(const iwae_handle* h, const std::vector<float>& src, float* dst) {
+  long long o = 0;
+  for (const auto& k : h->keras) {
+    const DenseL& d = h->dense[k.di];
+    for (int r = 0; r < d.fin; ++r)
+      for (int j = 0; j < k.width; ++j) dst[o++] = src[d.off + (long long)r * d.ldw + k.col0 + j];
+    for (int j = 0; j < k.width; ++j) dst[o++] = src[d.off + (long long)d.fin * d.ldw + k.col0 + j];
+  }
+}
+
+static int check_n(iwae_handle* h, long long n, const void* p) {
+  if (!h) return IWAE_EINVAL;
+  if (!p) return fail(h, IWAE_EINVAL, "NULL host buffer");
+  if (n != h->nparam_keras)
+    return fail(h, IWAE_EINVAL, "expected " + std::to_string(h->nparam_keras) + " parameters, got " +
+                                   std::to_string(n));
+  return IWAE_OK;
+}
+
+static int upload(iwae_handle* h, float* dev, const float* host) {
+  std::vector<float> tmp;
+  keras_to_internal(h, host, tmp);
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(dev, tmp.data(), tmp.size() * sizeof(float), hipMemcpyHostToDevice));
+  return IWAE_OK;
+}
+
+static int download(iwae_handle* h, const float* dev, float* host) {
+  std::vector<float> tmp((size_t)h->nparam_int);
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(tmp.data(), dev, tmp.size() * sizeof(float), hipMemcpyDeviceToHost));
+  internal_to_keras(h, tmp, host);
+  return IWAE_OK;
+}
+
+int iwae_set_params(iwae_handle* h, const float* host, long long n) {
+  CHK(check_n(h, n, host));
+  return upload(h, h->params, host);
+}
+
+int iwae_get_params(iwae_handle* h, float* host, long long n) {
+  CHK(check_n(h, n, host));
+  return download(h, h->params, host);
+}
+
+int iwae_get_grads(iwae_handle* h, float* host, long long n) {
+  CHK(check_n(h, n, host));
+  return download(h, h->grad, host);
+}
+
+int iwae_set_adam(iwae_handle* h, float lr, float b1, float b2, float eps) {
+  if (!h) return IWAE_EINVAL;
+  float v[4] = {lr, b1, b2, eps};
+  HIPCHK(hipMemcpyAsync(&h->ds->adam, v, sizeof(v), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return IWAE_OK;
+}
+
+int iwae_get_adam_state(iwae_handle* h, float* m, float* v, long long n, long long* step) {
+  CHK(check_n(h, n, m));
+  CHK(check_n(h, n, v));
+  CHK(download(h, h->adam_m, m));
+  CHK(download(h, h->adam_v, v));
+  if (step) {
+    AdamState s;
+    HIPCHK(hipMemcpy(&s, &h->ds->adam, sizeof(s), hipMemcpyDeviceToHost));
+    *step = s.t;
+  }
+  return IWAE_OK;
+}
+
+int iwae_set_adam_state(iwae_handle* h, const float* m, const float* v, long long n, long long step) {
+  CHK(check_n(h, n, m));
+  CHK(check_n(h, n, v));
+  CHK(upload(h, h->adam_m, m));
+  CHK(upload(h, h->adam_v, v));
+  AdamState s;
+  HIPCHK(hipMemcpy(&s, &h->ds->adam, sizeof(s), hipMemcpyDeviceToHost));
+  s.t = step;
+  HIPCHK(hipMemcpy(&h->ds->adam, &s, sizeof(s), hipMemcpyHostToDevice));
+  return IWAE_OK;
+}
+
+int iwae_train_step(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,
+                    const float* const* eps, int n_eps, float* loss_dev) {
+  if (!h) return IWAE_EINVAL;
+  return do_train(h, lc, x, B, eps, n_eps, loss_dev, true);
+}
+
+int iwae_forward_backward(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,
+                          const float* const* eps, int n_eps, float* loss_dev) {
+  if (!h) return IWAE_EINVAL;
+  return do_train(h, lc, x, B, eps, n_eps, loss_dev, false);
+}
+
+int iwae_grad_buffer(iwae_handle* h, float** g, long long* n) {
+  if (!h || !g || !n) return IWAE_EINVAL;
+  *g = h->grad;
+  *n = h->nparam_int;
+  return IWAE_OK;
+}
+
+int iwae_bind_grad_buffer(iwae_handle* h, float* g, long long n) {
+  if (!h) return IWAE_EINVAL;
+  if (g && n != h->nparam_int)
+    return fail(h, IWAE_EINVAL, "grad buffer must hold " + std::to_string(h->nparam_int) + " floats");
+  h->grad = g ? g : h->grad_own;
+  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+  h->graphs.clear();
+  return IWAE_OK;
+}
+
+int iwae_apply_adam(iwae_handle* h, float grad_scale) {
+  if (!h) return IWAE_EINVAL;
+  if (!(grad_scale > 0.f)) return fail(h, IWAE_EINVAL, "grad_scale must be > 0");
+  return run_adam(h, false, false, true, grad_scale);
+}
+
+static int eval_forward(iwae_handle* h, const Plan& P, const float* x, const float* const* eps, int n_eps,
+                        EpsSet& E) {
+  if (!x) return fail(h, IWAE_EINVAL, "x is NULL");
+  CHK(parse_eps(h, P, eps, n_eps, E));
+  CHK(ensure_capacity(h, P.Bimg, P.Bimg * P.kS, false));
+  CHK(copy_x(h, P, x));
+  return forward_core(h, P, E, false);
+}
+
+int iwae_log_weights(iwae_handle* h, const float* x, int B, int k, const float* const* eps, int n_eps,
+                     float* lw) {
+  if (!h) return IWAE_EINVAL;
+  if (!lw) return fail(h, IWAE_EINVAL, "lw is NULL");
+  iwae_loss_config lc{IWAE_LOSS_VAE, k, 1.f, 1.f, 0.5f, 0, 0};
+  Plan P;
+  CHK(make_plan(h, &lc, B, P));
+  EpsSet E;
+  CHK(eval_forward(h, P, x, eps, n_eps, E));
+  CHK(run_bound(h, P, false, 1.f, &h->ds->scalars[1]));
+  HIPCHK(hipMemcpyAsync(lw, h->lw, (size_t)B * k * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
+  return IWAE_OK;
+}
+
+int iwae_bound(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B, const float* const* eps,
+               int n_eps, float* value_dev) {
+  if (!h) return IWAE_EINVAL;
+  if (!value_dev) return fail(h, IWAE_EINVAL, "value_dev is NULL");
+  Plan P;
+  CHK(make_plan(h, lc, B, P));
+  EpsSet E;
+  CHK(eval_forward(h, P, x, eps, n_eps, E));
+  CHK(run_bound(h, P, false, 1.f, value_dev));
+  return IWAE_OK;
+}
+
+int iwae_e_log_px(iwae_handle* h, const float* x, int B, int k, const float* const* eps, int n_eps,
+                  float* value_dev) {
+  if (!h) return IWAE_EINVAL;
+  if (!value_dev) return fail(h, IWAE_EINVAL, "value_dev is NULL");
+  iwae_loss_config lc{IWAE_LOSS_VAE, k, 1.f, 1.f, 0.5f, 0, 0};
+  Plan P;
+  CHK(make_plan(h, &lc, B, P));
+  P.mode_a = BM_NONE; P.w_a = 0.f; P.need_bce = 1; P.bce_w = 1.f;
+  EpsSet E;
+  CHK(eval_forward(h, P, x, eps, n_eps, E));
+  CHK(run_bound(h, P, false, 1.f, value_dev));
+  return IWAE_OK;
+}
+
+// chunked k-sample NLL over N images; accumulates per-image (m, s)
+static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, float* out_m, float* out_s,
+                    float* out_logpx) {
+  if (!h) return IWAE_EINVAL;
+  if (!x) return fail(h, IWAE_EINVAL, "x is NULL");
+  if (N <= 0 || k <= 0) return fail(h, IWAE_EINVAL, "N and k must be positive");
+  const long long target_rows = std::max<long long>(1 << 20, k);
+  int imgs = chunk > 0 ? chunk : (int)std::max<long long>(1, target_rows / k);
+  imgs = std::min(imgs, N);
+  const int kS = (int)std::min<long long>(k, std::max<long long>(1, target_rows / imgs));
+  CHK(ensure_capacity(h, imgs, imgs * kS, false));
+  const size_t wbytes = (size_t)h->xdim * sizeof(float);
+  for (int i0 = 0; i0 < N; i0 += imgs) {
+    const int n = std::min(imgs, N - i0);
+    HIPCHK(hipMemcpy2DAsync(h->x_in.p, (size_t)h->x_in.ld * sizeof(float), x + (size_t)i0 * h->xdim, wbytes,
+                            wbytes, n, hipMemcpyDeviceToDevice, h->stream));
+    for (int s0 = 0; s0 < k; s0 += kS) {
+      Plan P;
+      P.B = n; P.Bimg = n; P.Bsplit = n; P.kS = std::min(kS, k - s0);
+      EpsSet E;
+      std::memset(&E, 0, sizeof(E));
+      CHK(forward_core(h, P, E, false));
+      LseArgs a{};
+      a.part = h->part; a.ldpart = h->ldpart; a.npart = h->npart; a.logp = h->logp; a.logq = h->logq;
+      a.kS = P.kS; a.Bimg = n; a.run_m = h->run_m; a.run_s = h->run_s; a.init = s0 == 0;
+      a.ticket = &h->ds->tickets[1]; a.rng_base = &h->ds->rng[0];
+      HIPCHK(launch_lse(h->stream, a));
+    }
+    if (out_logpx) HIPCHK(launch_lse_final(h->stream, h->run_m, h->run_s, n, logf((float)k), out_logpx + i0));
+    if (out_m) HIPCHK(hipMemcpyAsync(out_m + i0, h->run_m, n * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
+    if (out_s) HIPCHK(hipMemcpyAsync(out_s + i0, h->run_s, n * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
+  }
+  return IWAE_OK;
+}
+
+int iwae_nll(iwae_handle* h, const float* x, int N, int k, int chunk, float* out_logpx) {
+  if (!h) return IWAE_EINVAL;
+  if (!out_logpx) return fail(h, IWAE_EINVAL, "out_logpx is NULL");
+  return nll_core(h, x, N, k, chunk, nullptr, nullptr, out_logpx);
+}
+
+int iwae_nll_partials(iwae_handle* h, const float* x, int N, int k_local, int chunk, float* out_m,
+                      float* out_s) {
+  if (!h) return IWAE_EINVAL;
+  if (!out_m || !out_s) return fail(h, IWAE_EINVAL, "NULL output");
+  return nll_core(h, x, N, k_local, chunk, out_m, out_s, nullptr);
+}
+
+int iwae_nll_eps(iwae_handle* h, const float* x, int N, int k, const float* const* eps, int n_eps,
+                 float* out_logpx) {
+  if (!h) return IWAE_EINVAL;
+  if (!out_logpx) return fail(h, IWAE_EINVAL, "out_logpx is NULL");
+  iwae_loss_config lc{IWAE_LOSS_IWAE, k, 1.f, 1.f, 0.5f, 0, 0};
+  Plan P;
+  CHK(make_plan(h, &lc, N, P));
+  EpsSet E;
+  CHK(eval_forward(h, P, x, eps, n_eps, E));
+  LseArgs a{};
+  a.part = h->part; a.ldpart = h->ldpart; a.npart = h->npart; a.logp = h->logp; a.logq = h->logq;
+  a.kS = k; a.Bimg = N; a.run_m = h->run_m; a.run_s = h->run_s; a.init = 1;
+  a.ticket = &h->ds->tickets[1]; a.rng_base = &h->ds->rng[0];
+  HIPCHK(launch_lse(h->stream, a));
+  HIPCHK(launch_lse_final(h->stream, h->run_m, h->run_s, N, logf((float)k), out_logpx));
+  return IWAE_OK;
+}
+
+int iwae_debug_gemm(iwae_handle* h, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
+                    int M, int N, int K) {
+  if (!h) return IWAE_EINVAL;
+  if ((lda | ldb | ldc) & 3) return fail(h, IWAE_EINVAL, "leading dims must be multiples of 4");
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return fail(h, IWAE_EINVAL, "pointers must be 16B aligned");
+  GemmArgs a{};
+  a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = C; a.ldc = ldc; a.M = M; a.N = N; a.K = K; a.kchunk = K;
+  HIPCHK(launch_gemm(h->stream, GEMM_FWD, EPI_STORE, choose_tile(M, N, 1), 1, false, a));
+  return IWAE_OK;
+}
+
+double iwae_workspace_bytes(const iwae_handle* h) { return h ? (double)h->arena_bytes : 0.0; }
+
+int iwae_profile_gemm(iwae_handle* h, int kind, int epi) {
+  if (!h) return IWAE_EINVAL;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->prof_kind = kind;
+  h->prof_epi = epi;
+  h->prof_used = 0;
+  h->prof_flop = 0.0;
+  return IWAE_OK;
+}
+
+int iwae_profile_read(iwae_handle* h, double* total_ms, double* total_flop, long long* launches) {
+  if (!h || !total_ms || !total_flop || !launches) return IWAE_EINVAL;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  double ms = 0.0;
+  for (size_t i = 0; i + 1 < h->prof_used; i += 2) {
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, h->prof_ev[i], h->prof_ev[i + 1]));
+    ms += t;
+  }
+  *total_ms = ms;
+  *total_flop = h->prof_flop;
+  *launches = (long long)(h->prof_used / 2);
+  return IWAE_OK;
+}
+
+}  // extern "C"

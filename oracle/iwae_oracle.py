@@ -1,0 +1,549 @@
+"""CPU oracle for the IWAE train-step / NLL hot path -- TEST INFRASTRUCTURE ONLY.
+
+This module is the checker, never the product.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import it.
+The product path (``iwae_replication_project_amd``) runs exclusively on the HIP
+library and fails loudly when that library is missing.
+
+What it is
+----------
+A numpy restatement (float64 by default, float32 on request) of the reference
+``flexible_IWAE.py`` (``F:`` below = /root/reference/flexible_IWAE.py,
+``E:`` = /root/reference/experiment_example.py), with the reference's own
+layout: every post-sampling tensor is sample-major ``[k, B, ...]`` exactly as
+``Normal.sample(n)`` produces it (F:59, F:68).  Noise ``eps`` is *injected*
+(one ``[k, B, d_i]`` array per stochastic layer), which is the only way the
+reference's unseeded sampling (no seed anywhere in F or E) can be compared.
+
+Gradients are a hand-written reverse pass (TF ``GradientTape`` semantics: the
+log-densities are differentiated through both the sample ``h`` and the
+distribution parameters, F:59-F:73, no stop_gradient anywhere).  They are
+checked against central finite differences and an independent torch-autograd
+restatement in ``tests/test_oracle.py``.
+
+PARITY UNPINNED
+---------------
+The reference needs TensorFlow 2.4.1 + TensorFlow-Probability (unpinned,
+TF 2.4 pairs with TFP 0.12) + tensorflow_datasets (F:2-F:7).  None is
+installed and there is no network, so the reference cannot run here, and it
+ships no tests, fixtures or golden vectors.  This restatement is therefore
+*parity unpinned*: it is pinned only by (a) finite differences, (b) an
+independent torch.distributions/autograd restatement, (c) the known-answer
+identities the reference's own definitions imply (L_1 == VAE, CIWAE(beta=1) ==
+VAE, power-p(p=1) == IWAE, L_alpha(alpha=1) == VAE, MIWAE(1,k) == VAE,
+MIWAE(k,1) == IWAE) and (d) closed-form Gaussian/Bernoulli densities.
+
+Third-party numerics restated here (not vendored in the reference):
+  * TFP ``Normal.log_prob`` (TFP 0.12): ``-0.5*squared_difference(x/s, loc/s)
+    - (0.5*log(2*pi) + log(s))``; ``Normal.sample``: ``eps*s + loc``.
+  * TFP ``Bernoulli(probs=p).log_prob(x)``: ``log1p(-p)*(1-x) + log(p)*x``.
+  * Keras backend ``binary_crossentropy`` (probabilities path, epsilon 1e-7):
+    ``-(x*log(clip(p)+1e-7) + (1-x)*log(1-clip(p)+1e-7))``.
+  * TF ``ResourceApplyAdam`` (Keras OptimizerV2 Adam, epsilon-hat form).
+  * ``tfp.stats.percentile(q=50, interpolation='midpoint')``.
+MIWAE / PIWAE are absent from the reference code; they follow
+IWAE_replication.pdf p7 section 2.4 (MIWAE: k1 samples averaged inside the
+log, Monte-Carlo over k2 outside) and Rainforth et al. 2018 (PIWAE: decoder
+gets grad of IWAE_{k1*k2}, encoder gets grad of MIWAE_{k1,k2}).  Sample index
+convention (build-defined): s = j*k1 + i, j in [0,k2) outer, i in [0,k1) inner.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+# ---- constants straight from the reference ---------------------------------
+PROB_SCALE = 1.0 - 1e-6      # F:102 / F:126  probs*(1-10**(-6)) + 10**(-7)
+PROB_SHIFT = 1e-7
+SCALE_EPS = 1e-6             # F:37  tfd.Normal(q_mu, q_std + 1e-6)
+KERAS_EPS = 1e-7             # keras.backend.epsilon(), used by F:323/F:400/F:456
+HALF_LOG_2PI = 0.5 * math.log(2.0 * math.pi)
+
+LOSSES = ("VAE", "IWAE", "VAE_V1", "L_alpha", "L_power_p", "L_median",
+          "CIWAE", "MIWAE", "PIWAE")
+
+
+# ---------------------------------------------------------------------------
+# Model structure (F:22-F:218)
+# ---------------------------------------------------------------------------
+@dataclass
+class ModelSpec:
+    """Layer structure of ``Flexible_Model`` (F:178-F:218).
+
+    ``dense`` lists every Keras Dense layer in ``trainable_weights`` order
+    (encoder first, then decoder; per Stochastic_layer l1, l2, lmu, lstd,
+    F:26-F:29; decoder prior layers then the output Sequential, F:86-F:96).
+    """
+    n_hidden_encoder: list
+    n_hidden_decoder: list
+    n_latent_encoder: list
+    n_latent_decoder: list
+    x_dim: int = 784
+    dense: list = field(default_factory=list)
+
+    def __post_init__(self):
+        he, hd = list(self.n_hidden_encoder), list(self.n_hidden_decoder)
+        le, ld = list(self.n_latent_encoder), list(self.n_latent_decoder)
+        L = len(he)
+        if L < 1 or len(le) != L:
+            raise ValueError("n_hidden_encoder / n_latent_encoder must be equal-length, non-empty")
+        if len(hd) != L or len(ld) != L:
+            raise ValueError("decoder lists must have one entry per stochastic layer "
+                             "(F:206-F:209 index the two stacks in lockstep)")
+        for i in range(L - 1):
+            # decoder.stochastic_layers[i] maps h[L-1-i] -> dist over h[L-2-i] (F:139-F:140)
+            if ld[i] != le[L - 2 - i]:
+                raise ValueError(f"n_latent_decoder[{i}]={ld[i]} must equal "
+                                 f"n_latent_encoder[{L-2-i}]={le[L-2-i]}")
+        self.L = L
+        dense = []
+        for i in range(L):
+            fin = self.x_dim if i == 0 else le[i - 1]
+            H, d = he[i], le[i]
+            dense += [(f"enc{i}.l1", fin, H), (f"enc{i}.l2", H, H),
+                      (f"enc{i}.lmu", H, d), (f"enc{i}.lstd", H, d)]
+        for i in range(L - 1):
+            fin, H, d = le[L - 1 - i], hd[i], ld[i]
+            dense += [(f"dec{i}.l1", fin, H), (f"dec{i}.l2", H, H),
+                      (f"dec{i}.lmu", H, d), (f"dec{i}.lstd", H, d)]
+        Hd = hd[-1]
+        # F:92-F:94: Dense(n_hidden[-1]) x2 then Dense(28*28); n_latent_decoder[-1] is ignored
+        dense += [("out.l1", le[0], Hd), ("out.l2", Hd, Hd), ("out.l3", Hd, self.x_dim)]
+        self.dense = dense
+
+    def param_shapes(self):
+        shapes = []
+        for _, fin, fout in self.dense:
+            shapes += [(fin, fout), (fout,)]
+        return shapes
+
+    def n_params(self):
+        return sum(int(np.prod(s)) for s in self.param_shapes())
+
+
+def output_bias_from_mean(train_mean):
+    """F:170-F:175: bias = -log(1/clip(mean, .001, .999) - 1)."""
+    m = np.clip(np.asarray(train_mean, dtype=np.float64), 0.001, 0.999)
+    return -np.log(1.0 / m - 1.0)
+
+
+def glorot_init(spec: ModelSpec, rng: np.random.Generator, out_bias=None, dtype=np.float64):
+    """Keras defaults: glorot_uniform kernels, zero biases; decoder output bias
+    from ``get_bias`` (F:94).  Returns dict name -> [W, b]."""
+    params = {}
+    for name, fin, fout in spec.dense:
+        lim = math.sqrt(6.0 / (fin + fout))
+        W = rng.uniform(-lim, lim, size=(fin, fout))
+        b = np.zeros(fout)
+        if name == "out.l3" and out_bias is not None:
+            b = np.asarray(out_bias, dtype=np.float64).copy()
+        params[name] = [W.astype(dtype), b.astype(dtype)]
+    return params
+
+
+def flatten_params(spec, params):
+    return np.concatenate([np.concatenate([params[n][0].ravel(), params[n][1].ravel()])
+                           for n, _, _ in spec.dense])
+
+
+def unflatten_params(spec, flat, dtype=np.float64):
+    out, o = {}, 0
+    for n, fin, fout in spec.dense:
+        W = flat[o:o + fin * fout].reshape(fin, fout).astype(dtype); o += fin * fout
+        b = flat[o:o + fout].astype(dtype); o += fout
+        out[n] = [W, b]
+    assert o == flat.size
+    return out
+
+
+def cast_params(params, dtype):
+    return {k: [v[0].astype(dtype), v[1].astype(dtype)] for k, v in params.items()}
+
+
+def draw_eps(spec, k, B, rng, dtype=np.float64):
+    """One standard-normal array per stochastic layer, [k, B, d_i] (F:59, F:68)."""
+    return [rng.standard_normal((k, B, d)).astype(dtype) for d in spec.n_latent_encoder]
+
+
+# ---------------------------------------------------------------------------
+# Forward (F:22-F:145, F:327-F:351)
+# ---------------------------------------------------------------------------
+def _stoch_forward(params, prefix, X):
+    """Stochastic_layer.call (F:32-F:38)."""
+    W1, b1 = params[prefix + ".l1"]; W2, b2 = params[prefix + ".l2"]
+    Wm, bm = params[prefix + ".lmu"]; Ws, bs = params[prefix + ".lstd"]
+    y1 = np.tanh(X @ W1 + b1)
+    y2 = np.tanh(y1 @ W2 + b2)
+    mu = y2 @ Wm + bm
+    e = np.exp(y2 @ Ws + bs)                 # lstd: activation=tf.exp (F:29)
+    scale = e + X.dtype.type(SCALE_EPS)      # F:37
+    return dict(X=X, y1=y1, y2=y2, mu=mu, e=e, scale=scale)
+
+
+def normal_log_prob(x, loc, scale):
+    """TFP Normal._log_prob: -0.5*(x/s - loc/s)^2 - (0.5 log 2pi + log s)."""
+    z = x / scale - loc / scale
+    return -0.5 * z * z - (x.dtype.type(HALF_LOG_2PI) + np.log(scale)), z
+
+
+def forward(params, spec: ModelSpec, x, eps, need_bce=False, dup_decoder=False):
+    """get_log_weights (F:327-F:351) with injected noise.
+
+    x: [B, 784] in {0,1}; eps: list of [k, B, d_i].  Returns a cache dict
+    whose 'lw' is the [k, B] log-weight matrix.  ``dup_decoder`` also runs the
+    decoder output MLP whose result F:340 discards (the reference computes it
+    twice per call; only the CPU-baseline timing uses this)."""
+    dt = x.dtype.type
+    L = spec.L
+    c = dict(x=x, eps=eps)
+    # ---- encoder (F:56-F:75)
+    enc = []
+    h = []
+    lq_layers = []
+    q0 = _stoch_forward(params, "enc0", x)            # F:58, M = B rows
+    h1 = eps[0] * q0["scale"] + q0["mu"]              # F:59 sample(n): eps*scale + loc
+    lp, z = normal_log_prob(h1, q0["mu"], q0["scale"])
+    q0["z"] = z
+    enc.append(q0); h.append(h1); lq_layers.append(lp.sum(-1))   # F:60
+    for i in range(1, L):
+        qi = _stoch_forward(params, f"enc{i}", h[-1])             # F:66
+        hi = eps[i] * qi["scale"] + qi["mu"]                     # F:68
+        lp, z = normal_log_prob(hi, qi["mu"], qi["scale"])
+        qi["z"] = z
+        enc.append(qi); h.append(hi); lq_layers.append(lp.sum(-1))   # F:70
+    logq = lq_layers[0]
+    for t in lq_layers[1:]:
+        logq = logq + t                                           # F:73
+    # ---- decoder output MLP (F:89-F:96, F:123-F:129)
+    W1, b1 = params["out.l1"]; W2, b2 = params["out.l2"]; W3, b3 = params["out.l3"]
+    if dup_decoder:                                               # F:340, result unused
+        _ = 1.0 / (1.0 + np.exp(-(np.tanh(np.tanh(h[0] @ W1 + b1) @ W2 + b2) @ W3 + b3)))
+    o1 = np.tanh(h[0] @ W1 + b1)
+    o2 = np.tanh(o1 @ W2 + b2)
+    logit = o2 @ W3 + b3
+    s = 1.0 / (1.0 + np.exp(-logit))                              # sigmoid
+    p = s * dt(PROB_SCALE) + dt(PROB_SHIFT)                       # F:126
+    xb = x[None]
+    logpx = (np.log1p(-p) * (1 - xb) + np.log(p) * xb).sum(-1)   # F:127-F:128
+    c.update(o1=o1, o2=o2, s=s, p=p)
+    if need_bce:
+        pc = np.clip(p, dt(KERAS_EPS), dt(1 - KERAS_EPS))
+        c["bce_row"] = (xb * np.log(pc + dt(KERAS_EPS))
+                        + (1 - xb) * np.log(1 - pc + dt(KERAS_EPS))).sum(-1)
+    # ---- prior (F:134-F:142)
+    lp_L, _ = normal_log_prob(h[-1], dt(0.0), dt(1.0))
+    logp = lp_L.sum(-1)
+    dec = []
+    for i in range(L - 1):
+        di = _stoch_forward(params, f"dec{i}", h[L - 1 - i])     # F:139
+        lp, z = normal_log_prob(h[L - 2 - i], di["mu"], di["scale"])  # F:140
+        di["z"] = z
+        dec.append(di)
+        logp = logp + lp.sum(-1)                                  # F:141
+    lw = (logp + logpx) - logq                                    # F:345, F:349
+    c.update(enc=enc, dec=dec, h=h, logq=logq, logp=logp, logpx=logpx, lw=lw)
+    return c
+
+
+# ---------------------------------------------------------------------------
+# Bounds: value and dJ/dlw (F:354-F:430 + PDF p7 / Rainforth for MIWAE/PIWAE)
+# ---------------------------------------------------------------------------
+def _softmax0(a):
+    m = a.max(axis=0)
+    e = np.exp(a - m)
+    return e / e.sum(axis=0), m, e
+
+
+def L_k_from_weights(lw):
+    """F:363-F:370: mean_B(log(mean_k exp(lw - max)) + max)."""
+    m = lw.max(axis=0)
+    return np.mean(np.log(np.mean(np.exp(lw - m), axis=0)) + m)
+
+
+def L_k_per_image(lw):
+    m = lw.max(axis=0)
+    return np.log(np.mean(np.exp(lw - m), axis=0)) + m
+
+
+def L_from_weights(lw):
+    """F:429-F:430."""
+    return np.mean(lw)
+
+
+def L_power_p_from_weights(lw, p):
+    """F:405-F:409."""
+    m = lw.max(axis=0)
+    return np.mean(np.log(np.mean(np.exp((lw - m) * p), axis=0)) / p + m)
+
+
+def median_indices(k):
+    """tfp.stats.percentile(q=50, 'midpoint') averages order statistics
+    floor((k-1)/2) and ceil((k-1)/2) (F:377)."""
+    return (k - 1) // 2, k // 2
+
+
+def L_median_from_weights(lw):
+    lo, hi = median_indices(lw.shape[0])
+    srt = np.sort(lw, axis=0)
+    return np.mean((srt[lo] + srt[hi]) / 2)
+
+
+def MIWAE_from_weights(lw, k1, k2):
+    k, B = lw.shape
+    assert k == k1 * k2
+    g = lw.reshape(k2, k1, B)
+    m = g.max(axis=1, keepdims=True)
+    inner = np.log(np.mean(np.exp(g - m), axis=1)) + m[:, 0]
+    return np.mean(inner)
+
+
+def bound_grad(lw, kind, p=1.0, k1=None, k2=None):
+    """dJ/dlw for the lw-only bounds."""
+    k, B = lw.shape
+    if kind == "VAE":
+        return np.full_like(lw, 1.0 / (k * B))
+    if kind == "IWAE":
+        sm, _, _ = _softmax0(lw)
+        return sm / B
+    if kind == "L_power_p":
+        sm, _, _ = _softmax0(lw * p)
+        return sm / B
+    if kind == "L_median":
+        lo, hi = median_indices(k)
+        order = np.argsort(lw, axis=0, kind="stable")
+        g = np.zeros_like(lw)
+        cols = np.arange(B)
+        g[order[lo], cols] += 0.5 / B
+        g[order[hi], cols] += 0.5 / B
+        return g
+    if kind == "MIWAE":
+        g = lw.reshape(k2, k1, B)
+        m = g.max(axis=1, keepdims=True)
+        e = np.exp(g - m)
+        sm = e / e.sum(axis=1, keepdims=True)
+        return (sm / (k2 * B)).reshape(k, B)
+    raise ValueError(kind)
+
+
+# ---------------------------------------------------------------------------
+# Backward (reverse of forward; TF GradientTape semantics, F:243)
+# ---------------------------------------------------------------------------
+def _dense_back(W, X, dZ):
+    """Z = X @ W + b over arbitrary leading dims -> (dW, db, dX)."""
+    Xf = X.reshape(-1, X.shape[-1]); dZf = dZ.reshape(-1, dZ.shape[-1])
+    return Xf.T @ dZf, dZf.sum(0), dZ @ W.T
+
+
+def _stoch_backward(params, prefix, cache, dmu, dscale, grads, need_dx):
+    W1, _ = params[prefix + ".l1"]; W2, _ = params[prefix + ".l2"]
+    Wm, _ = params[prefix + ".lmu"]; Ws, _ = params[prefix + ".lstd"]
+    y1, y2, X, e = cache["y1"], cache["y2"], cache["X"], cache["e"]
+    dzs = dscale * e                                   # d exp(zs) = exp(zs) dzs
+    gWm, gbm, dy2a = _dense_back(Wm, y2, dmu)
+    gWs, gbs, dy2b = _dense_back(Ws, y2, dzs)
+    da2 = (dy2a + dy2b) * (1 - y2 * y2)
+    gW2, gb2, dy1 = _dense_back(W2, y1, da2)
+    da1 = dy1 * (1 - y1 * y1)
+    gW1, gb1, dX = _dense_back(W1, X, da1)
+    for name, gw, gb in ((".l1", gW1, gb1), (".l2", gW2, gb2), (".lmu", gWm, gbm), (".lstd", gWs, gbs)):
+        grads[prefix + name][0] += gw
+        grads[prefix + name][1] += gb
+    return dX if need_dx else None
+
+
+def backward(params, spec: ModelSpec, c, a, bce_coef=None, kl_coef=0.0,
+             want=("enc", "dec")):
+    """Gradient of J = sum(a*lw) + sum(bce_coef*bce_row) + kl_coef*KL_mean.
+
+    a: [k,B] dJ/dlw; bce_coef: [k,B] or None; kl_coef: scalar multiplying the
+    V1 analytic-KL mean (F:457-F:458).  ``want`` selects which parameter
+    groups receive gradients ('enc' = encoder, 'dec' = decoder)."""
+    dt = c["x"].dtype.type
+    L = spec.L
+    grads = {n: [np.zeros_like(params[n][0]), np.zeros_like(params[n][1])] for n, _, _ in spec.dense}
+    x = c["x"][None]
+    h, eps = c["h"], c["eps"]
+    dh = [np.zeros_like(hi) for hi in h]
+    # ---- output layer: d/dlogit of Bernoulli log_prob (+ Keras BCE)
+    s, p = c["s"], c["p"]
+    dp = a[..., None] * (x / p - (1 - x) / (1 - p))
+    if bce_coef is not None:
+        lo, hi = dt(KERAS_EPS), dt(1 - KERAS_EPS)
+        pc = np.clip(p, lo, hi)
+        inr = ((p >= lo) & (p <= hi)).astype(p.dtype)
+        dp = dp + bce_coef[..., None] * (x / (pc + lo) - (1 - x) / (1 - pc + lo)) * inr
+    dlogit = dp * dt(PROB_SCALE) * (s * (1 - s))
+    W1, _ = params["out.l1"]; W2, _ = params["out.l2"]; W3, _ = params["out.l3"]
+    gW3, gb3, do2 = _dense_back(W3, c["o2"], dlogit)
+    da2 = do2 * (1 - c["o2"] ** 2)
+    gW2, gb2, do1 = _dense_back(W2, c["o1"], da2)
+    da1 = do1 * (1 - c["o1"] ** 2)
+    gW1, gb1, dh0 = _dense_back(W1, h[0], da1)
+    dh[0] += dh0
+    for name, gw, gb in (("out.l1", gW1, gb1), ("out.l2", gW2, gb2), ("out.l3", gW3, gb3)):
+        grads[name][0] += gw; grads[name][1] += gb
+    # ---- prior terms (dJ/dlogp = a)
+    dlp = a[..., None]
+    dh[L - 1] += dlp * (-h[L - 1])                      # N(0,1): d/dx = -x
+    for i in range(L - 1):
+        di = c["dec"][i]
+        t, src = L - 2 - i, L - 1 - i
+        z, sc = di["z"], di["scale"]
+        dh[t] += dlp * (-z / sc)
+        dmu = dlp * (z / sc)
+        dsc = dlp * ((z * z - 1) / sc)
+        dX = _stoch_backward(params, f"dec{i}", di, dmu, dsc, grads, True)
+        dh[src] += dX
+    # ---- encoder, top layer down (dJ/dlogq = -a)
+    dlq = -a[..., None]
+    for i in reversed(range(L)):
+        qi = c["enc"][i]
+        z, sc = qi["z"], qi["scale"]
+        dht = dh[i] + dlq * (-z / sc)
+        dmu = dht + dlq * (z / sc)
+        dsc = dht * eps[i] + dlq * ((z * z - 1) / sc)
+        if i == 0:
+            dmu = dmu.sum(0); dsc = dsc.sum(0)            # mu/scale broadcast over k
+        if i == L - 1 and kl_coef != 0.0:
+            mu, scl = qi["mu"], qi["scale"]
+            nrows = int(np.prod(mu.shape[:-1]))
+            dmu = dmu + kl_coef * mu / nrows
+            dsc = dsc + kl_coef * (-1.0 / scl + scl) / nrows
+        dX = _stoch_backward(params, f"enc{i}", qi, dmu, dsc, grads, i > 0)
+        if i > 0:
+            dh[i - 1] += dX
+    # zero out unwanted groups
+    for n, _, _ in spec.dense:
+        grp = "enc" if n.startswith("enc") else "dec"
+        if grp not in want:
+            grads[n][0][...] = 0; grads[n][1][...] = 0
+    return grads
+
+
+def kl_v1(c):
+    """F:457-F:458: mean over rows of sum_d -0.5(1 + 2log s - mu^2 - s^2) of
+    the LAST encoder layer's distribution."""
+    q = c["enc"][-1]
+    mu, s = q["mu"], q["scale"]
+    kl = -0.5 * (1 + 2 * np.log(s) - mu * mu - s * s)
+    return np.mean(kl.sum(-1))
+
+
+# ---------------------------------------------------------------------------
+# Objective dispatch = train_step's loss selection (F:228-F:241)
+# ---------------------------------------------------------------------------
+def objective_and_grads(params, spec, x, eps, loss, k, p=1.0, alpha=1.0, beta=0.5,
+                        k1=None, k2=None, eps2=None, with_grads=True, dup_decoder=False):
+    """Returns (J, grads_of_J or None).  ``loss = -J`` is what train_step
+    minimises (F:229-F:241).  CIWAE takes two independent draws (F:383):
+    ``eps`` feeds the VAE term, ``eps2`` the IWAE term."""
+    B = x.shape[0]
+    if loss in ("VAE", "IWAE", "L_power_p", "L_median", "MIWAE"):
+        c = forward(params, spec, x, eps, dup_decoder=dup_decoder)
+        lw = c["lw"]
+        if loss == "VAE":
+            J = L_from_weights(lw)
+        elif loss == "IWAE":
+            J = L_k_from_weights(lw)
+        elif loss == "L_power_p":
+            J = L_power_p_from_weights(lw, p)
+        elif loss == "L_median":
+            J = L_median_from_weights(lw)
+        else:
+            J = MIWAE_from_weights(lw, k1, k2)
+        if not with_grads:
+            return J, None
+        a = bound_grad(lw, loss, p=p, k1=k1, k2=k2)
+        return J, backward(params, spec, c, a)
+    if loss == "PIWAE":
+        c = forward(params, spec, x, eps)
+        lw = c["lw"]
+        J = L_k_from_weights(lw)            # reported objective: IWAE_{k1 k2}
+        if not with_grads:
+            return J, None
+        g_dec = backward(params, spec, c, bound_grad(lw, "IWAE"), want=("dec",))
+        g_enc = backward(params, spec, c, bound_grad(lw, "MIWAE", k1=k1, k2=k2), want=("enc",))
+        return J, {n: [g_dec[n][0] + g_enc[n][0], g_dec[n][1] + g_enc[n][1]] for n in g_dec}
+    if loss == "CIWAE":
+        c1 = forward(params, spec, x, eps)
+        c2 = forward(params, spec, x, eps2)
+        J = beta * L_from_weights(c1["lw"]) + (1 - beta) * L_k_from_weights(c2["lw"])
+        if not with_grads:
+            return J, None
+        g1 = backward(params, spec, c1, beta * bound_grad(c1["lw"], "VAE"))
+        g2 = backward(params, spec, c2, (1 - beta) * bound_grad(c2["lw"], "IWAE"))
+        return J, {n: [g1[n][0] + g2[n][0], g1[n][1] + g2[n][1]] for n in g1}
+    if loss == "L_alpha":
+        c = forward(params, spec, x, eps, need_bce=True)
+        lw = c["lw"]
+        Eq = np.mean(c["bce_row"])                             # F:400
+        J = (1 - alpha) * Eq + alpha * L_from_weights(lw)       # F:401
+        if not with_grads:
+            return J, None
+        kB = lw.size
+        a = np.full_like(lw, alpha / kB)
+        bc = np.full_like(lw, (1 - alpha) / kB)
+        return J, backward(params, spec, c, a, bce_coef=bc)
+    if loss == "VAE_V1":
+        c = forward(params, spec, x, eps, need_bce=True)
+        Eq = np.mean(c["bce_row"])                              # F:456
+        J = Eq - kl_v1(c)                                       # F:459
+        if not with_grads:
+            return J, None
+        lw = c["lw"]
+        a = np.zeros_like(lw)
+        bc = np.full_like(lw, 1.0 / lw.size)
+        return J, backward(params, spec, c, a, bce_coef=bc, kl_coef=-1.0)
+    raise ValueError(f"unknown loss_function {loss!r}")
+
+
+# ---------------------------------------------------------------------------
+# Adam (E:36-E:40; TF ResourceApplyAdam kernel form)
+# ---------------------------------------------------------------------------
+class Adam:
+    def __init__(self, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7):
+        self.lr, self.b1, self.b2, self.eps = lr, beta_1, beta_2, epsilon
+        self.m = None; self.v = None; self.t = 0
+
+    def apply(self, flat_params, flat_grads):
+        dt = flat_params.dtype.type
+        if self.m is None:
+            self.m = np.zeros_like(flat_params); self.v = np.zeros_like(flat_params)
+        self.t += 1
+        b1p = dt(self.b1) ** dt(self.t); b2p = dt(self.b2) ** dt(self.t)
+        alpha = dt(self.lr) * np.sqrt(dt(1) - b2p) / (dt(1) - b1p)
+        g = flat_grads
+        self.m += (g - self.m) * (dt(1) - dt(self.b1))
+        self.v += (g * g - self.v) * (dt(1) - dt(self.b2))
+        return flat_params - (self.m * alpha) / (np.sqrt(self.v) + dt(self.eps))
+
+
+def train_step(params, spec, x, eps, loss, k, opt: Adam, **kw):
+    """F:221-F:247: loss = -J, grads of loss, Adam update.  Returns
+    (loss, new_params, flat_grads_of_loss)."""
+    J, gJ = objective_and_grads(params, spec, x, eps, loss, k, **kw)
+    dt = x.dtype
+    flat_g = -flatten_params(spec, gJ).astype(dt)
+    new_flat = opt.apply(flatten_params(spec, params).astype(dt), flat_g)
+    return -J, unflatten_params(spec, new_flat, dtype=dt), flat_g
+
+
+# ---------------------------------------------------------------------------
+# k-sample NLL (F:463-F:464), chunked over samples with an LSE merge
+# ---------------------------------------------------------------------------
+def log_px_per_image(params, spec, x, k, rng=None, eps=None, chunk=500):
+    """log p_hat(x) = logmeanexp_k lw per image.  Either ``eps`` (list of
+    [k,B,d]) or an rng drawing it chunk by chunk."""
+    B = x.shape[0]
+    m_run = np.full(B, -np.inf); s_run = np.zeros(B)
+    for s0 in range(0, k, chunk):
+        kc = min(chunk, k - s0)
+        e = [ee[s0:s0 + kc] for ee in eps] if eps is not None else draw_eps(spec, kc, B, rng, x.dtype)
+        lw = forward(params, spec, x, e)["lw"].astype(np.float64)
+        m = lw.max(0)
+        M = np.maximum(m_run, m)
+        s_run = s_run * np.exp(m_run - M) + np.exp(lw - M).sum(0)
+        m_run = M
+    return m_run + np.log(s_run) - math.log(k)
