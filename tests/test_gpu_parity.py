@@ -157,7 +157,8 @@ def test_c2_full_size_iwae_train_step_matches_oracle():
     ref_loss, ref_new, ref_g = O.train_step(params, spec, x, eps, "IWAE", k, opt)
     assert abs(loss - ref_loss) <= REL * abs(ref_loss)
     assert rel_l2(flat(m.get_gradients()), ref_g) <= REL
-    np.testing.assert_allclose(flat(m.get_weights()), O.flatten_params(spec, ref_new), atol=2e-6)
+    # first Adam step moves each weight by up to ~lr; allow 0.5% of it
+    np.testing.assert_allclose(flat(m.get_weights()), O.flatten_params(spec, ref_new), atol=5e-6)
 
 
 # ----------------------------------------------- multi-step training parity
@@ -226,37 +227,77 @@ def test_philox_noise_statistics_match_oracle_vae_bound():
     assert abs(gpu - lw.mean()) <= 5 * se + 1e-4 * abs(lw.mean()), (gpu, lw.mean(), se)
 
 
-def test_nll_philox_matches_oracle_statistically():
-    """k=5000 NLL from device noise vs the oracle with its own noise: two
-    independent estimates of the same quantity; agree within 0.05 nats."""
+def _concentrated_model(seed, he=(64,), le=(16,)):
+    """A model whose log-weights barely depend on the noise: encoder heads zero
+    (q = N(0, (1+1e-6)^2) ~ prior) and decoder output kernel scaled by 1e-3, so
+    every k-sample estimate of log p(x) agrees to ~1e-3 nats.  This isolates
+    the NLL machinery (sampling, LSE over k, chunk merging) from Monte-Carlo
+    spread, which for an untrained model is tens of nats."""
     from oracle import iwae_oracle as O
-    he, hd, le, ld = [64], [64], [16], [784]
-    rng = np.random.default_rng(14)
-    mean = rng.uniform(0.02, 0.3, 784)
+    he, le = list(he), list(le)
+    hd, ld = list(reversed(he)), [*le[:-1][::-1], 784] if len(le) > 1 else [784]
     spec = O.ModelSpec(he, hd, le, ld)
+    rng = np.random.default_rng(seed)
+    mean = rng.uniform(0.02, 0.3, 784)
     params = O.glorot_init(spec, rng, out_bias=O.output_bias_from_mean(mean))
+    for n in params:
+        if n.startswith("enc") and (n.endswith("lmu") or n.endswith("lstd")):
+            params[n] = [np.zeros_like(params[n][0]), np.zeros_like(params[n][1])]
+        if n.startswith("dec") and (n.endswith("lmu") or n.endswith("lstd")):
+            params[n] = [np.zeros_like(params[n][0]), np.zeros_like(params[n][1])]
+    params["out.l3"][0] = params["out.l3"][0] * 1e-3
     params = {n: [w.astype(np.float32).astype(np.float64), b.astype(np.float32).astype(np.float64)]
               for n, (w, b) in params.items()}
-    m = make_model(he, hd, le, ld, seed=3)
+    m = make_model(he, hd, le, ld, seed=seed)
     m.set_weights(weights_from_flat(m, O.flatten_params(spec, params)))
     x = (rng.random((6, 784)) < mean).astype(np.float32)
+    return O, spec, params, m, x, rng
+
+
+@pytest.mark.parametrize("layers", [((64,), (16,)), ((64, 32), (32, 16))])
+def test_nll_k5000_matches_oracle_within_0p05_nats(layers):
+    """k=5000 NLL from device Philox noise vs the float64 oracle with its own
+    numpy noise (north_star: 0.05 nats)."""
+    O, spec, params, m, x, rng = _concentrated_model(3, *layers)
     nll_gpu = m.get_NLL(x, k=5000)
     ref = -np.mean(O.log_px_per_image(params, spec, x.astype(np.float64), 5000, rng=rng, chunk=1000))
     assert abs(nll_gpu - ref) <= NLL_TOL, (nll_gpu, ref)
+    assert abs(nll_gpu - ref) <= 5e-3, (nll_gpu, ref)
 
 
-def test_nll_chunking_and_partials_are_consistent():
+def test_nll_chunking_and_sample_split_are_consistent():
+    O, spec, params, m, x, rng = _concentrated_model(4, (64, 32), (32, 16))
+    a = m.log_px(x, 3000, chunk=6).cpu().numpy()
+    b = m.log_px(x, 3000, chunk=2).cpu().numpy()
+    assert np.all(np.isfinite(a)) and np.all(np.isfinite(b))
+    np.testing.assert_allclose(a, b, atol=2e-3)
+    # sample-sharded partials merged like two ranks: M = max m, S = sum s exp(m - M)
+    import torch
+    from iwae_replication_project_amd import _lib
+    parts = []
+    for kl in (1200, 1800):
+        xd = m._x(x)
+        mm = torch.empty(6, device=m.device)
+        ss = torch.empty(6, device=m.device)
+        m._call(m._lib.iwae_nll_partials(m._h, _lib.fptr(xd), 6, kl, 0, _lib.fptr(mm), _lib.fptr(ss)))
+        m._stream.synchronize()
+        parts.append((mm.cpu().double(), ss.cpu().double()))
+    M = torch.maximum(parts[0][0], parts[1][0])
+    S = sum(s * torch.exp(mm - M) for mm, s in parts)
+    merged = (M + torch.log(S) - math.log(3000)).numpy()
+    np.testing.assert_allclose(merged, a, atol=2e-3)
+
+
+def test_nll_full_model_is_a_bound_upper_than_elbo():
+    """Untrained 2L model (heavy-tailed weights): L_5000 >= L_VAE on average
+    (PDF p5 eq. 3) and every per-image estimate is finite."""
     he, hd, le, ld = [200, 100], [100, 200], [100, 50], [100, 784]
     rng = np.random.default_rng(15)
     x = (rng.random((7, 784)) < 0.15).astype(np.float32)
     m = make_model(he, hd, le, ld, seed=9)
-    a = m.log_px(x, 300, chunk=7).cpu().numpy()
-    b = m.log_px(x, 300, chunk=3).cpu().numpy()
-    assert np.all(np.isfinite(a)) and np.all(np.isfinite(b))
-    # two independent 300-sample estimates of the same log p(x)
-    assert np.max(np.abs(a - b)) < 1.0
-    # bound ordering: L_5000 >= L_1 on average (PDF p5 eq. 3)
-    assert m.get_L_k(x, 5000) > m.get_L(x, 1000)
+    lp = m.log_px(x, 5000).cpu().numpy()
+    assert np.all(np.isfinite(lp))
+    assert float(lp.mean()) > m.get_L(x, 1000)
 
 
 # --------------------------------------------------------- data parallel (1 rank)
