@@ -93,6 +93,7 @@ __global__ __launch_bounds__(256) void gauss_fwd_kernel(GaussArgs a) {
         const float e = eps_at(a.eps_a, a.eps_b, a.kS, a.Bsplit, a.Bimg, a.d, r, j, a.seed, base, a.layer);
         h = __fadd_rn(__fmul_rn(e, sc), mu);
         a.H[(size_t)r * a.ldH + j] = h;
+        if (a.eps_out) a.eps_out[(size_t)r * a.ld_eps_out + j] = e;
       } else {
         h = a.H[(size_t)r * a.ldH + j];
       }
@@ -126,8 +127,6 @@ __global__ __launch_bounds__(256) void gauss_bwd_enc_kernel(GaussBwdArgs a) {
   const int pr = per_image ? blockIdx.x : blockIdx.x * 4 + wave;
   const int nP = (a.M + a.prow_div - 1) / a.prow_div;
   const bool row_ok = pr < nP;
-  uint64_t base = 0;
-  if (a.rng_base && !(a.eps_a)) base = *a.rng_base;
   for (int j0 = 0; j0 < a.d; j0 += 64) {
     const int j = j0 + lane;
     const bool act = row_ok && j < a.d;
@@ -146,7 +145,7 @@ __global__ __launch_bounds__(256) void gauss_bwd_enc_kernel(GaussBwdArgs a) {
         const int r = r_begin + s;
         if (r >= a.M) break;
         const float h = a.H[(size_t)r * a.ldH + j];
-        const float ev = eps_at(a.eps_a, a.eps_b, a.kS, a.Bsplit, a.Bimg, a.d, r, j, a.seed, base, a.layer);
+        const float ev = a.eps_rows[(size_t)r * a.ld_eps + j];
         const float dlq = -a.dlw[r];
         const float z = __fsub_rn(h / sc, mu / sc);
         float G = 0.f;
@@ -327,11 +326,13 @@ __device__ __forceinline__ void image_grad(const BoundArgs& a, int mode, int row
   }
 }
 
-__global__ __launch_bounds__(256) void bound_kernel(BoundArgs a) {
-  __shared__ float sh_all[4][1024];
+constexpr int kBoundWaves = 8;
+
+__global__ __launch_bounds__(kBoundWaves * 64) void bound_kernel(BoundArgs a) {
+  __shared__ float sh_all[kBoundWaves][1024];
+  __shared__ float red[kBoundWaves];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int b = blockIdx.x * 4 + wave;
-  if (b < a.Bimg) {
+  for (int b = blockIdx.x * kBoundWaves + wave; b < a.Bimg; b += gridDim.x * kBoundWaves) {
     const bool ga = b < a.Bsplit;
     const int mode = ga ? a.mode_a : a.mode_b;
     const float w = ga ? a.w_a : a.w_b;
@@ -368,24 +369,38 @@ __global__ __launch_bounds__(256) void bound_kernel(BoundArgs a) {
         for (int q = lane; q < a.kS; q += 64) a.dpx2[row0 + q] = a.dlw2[row0 + q];
     }
   }
-  if (a.ticket && last_block_arrive(a.ticket)) {
-    if (threadIdx.x < 64) {
-      float s = 0.f;
-      for (int i = lane; i < a.Bimg; i += 64) s += a.contrib[i];
-      s = wave_sum(s);
-      if (lane == 0) {
-        if (a.loss) *a.loss = a.loss_sign * s + (a.loss_add ? a.loss_add_coef * *a.loss_add : 0.f);
-        if (a.rng_base) *a.rng_base += 1;
-        *a.ticket = 0u;
-      }
+  bool finalize;
+  if (gridDim.x == 1) {
+    __syncthreads();       // one workgroup: its own contrib writes are visible after the barrier
+    finalize = true;
+  } else {
+    finalize = a.ticket && last_block_arrive(a.ticket);
+  }
+  if (finalize) {
+    float s = 0.f;
+    for (int i = threadIdx.x; i < a.Bimg; i += blockDim.x) s += a.contrib[i];
+    s = wave_sum(s);
+    if (lane == 0) red[wave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float tot = 0.f;
+      for (int i = 0; i < kBoundWaves; ++i) tot += red[i];
+      if (a.loss) *a.loss = a.loss_sign * tot + (a.loss_add ? a.loss_add_coef * *a.loss_add : 0.f);
+      if (a.rng_base) { a.rng_base[1] = a.rng_base[0]; a.rng_base[0] += 1; }
+      if (gridDim.x > 1) *a.ticket = 0u;
     }
   }
 }
 
 hipError_t launch_bound(hipStream_t st, const BoundArgs& a) {
   if (a.Bimg <= 0) return hipSuccess;
-  if ((a.mode_a == BM_MEDIAN || a.mode_b == BM_MEDIAN) && a.kS > 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bound_kernel, dim3((a.Bimg + 3) / 4), dim3(256), 0, st, a);
+  if ((a.mode_a == BM_MEDIAN || a.mode_b == BM_MEDIAN || a.mode2 == BM_MEDIAN) && a.kS > 1024)
+    return hipErrorInvalidValue;
+  // small batches: one workgroup (no cross-workgroup hand-off at all)
+  const int rows = a.Bimg * a.kS;
+  int grid = (a.Bimg <= 4 * kBoundWaves || rows <= 8192) ? 1 : (a.Bimg + kBoundWaves - 1) / kBoundWaves;
+  if (grid > 1 && !a.ticket) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bound_kernel, dim3(grid), dim3(kBoundWaves * 64), 0, st, a);
   return hipGetLastError();
 }
 
@@ -416,7 +431,7 @@ __global__ __launch_bounds__(256) void lse_kernel(LseArgs a) {
   }
   if (a.ticket && last_block_arrive(a.ticket)) {
     if (threadIdx.x == 0) {
-      if (a.rng_base) *a.rng_base += 1;
+      if (a.rng_base) { a.rng_base[1] = a.rng_base[0]; a.rng_base[0] += 1; }
       *a.ticket = 0u;
     }
   }
@@ -495,13 +510,9 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
       a.param[pidx] = a.param[pidx] - (m * alpha) / (sqrtf(v) + st.eps);
     }
   }
-  if (a.do_adam && last_block_arrive(a.ticket)) {
-    if (threadIdx.x == 0) {
-      a.state->t = st.t + 1;
-      *a.ticket = 0u;
-    }
-  }
 }
+
+__global__ void adam_tick_kernel(AdamState* s) { s->t += 1; }
 
 hipError_t launch_adam(hipStream_t st, const AdamArgs& a, long long max_seg_n) {
   if (a.nseg <= 0) return hipSuccess;
@@ -509,6 +520,7 @@ hipError_t launch_adam(hipStream_t st, const AdamArgs& a, long long max_seg_n) {
   if (bx > 64) bx = 64;
   if (bx < 1) bx = 1;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)bx, a.nseg), dim3(256), 0, st, a);
+  if (a.do_adam) hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(1), 0, st, a.state);
   return hipGetLastError();
 }
 

@@ -200,10 +200,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs a) {
     // Bernoulli epilogue.  Per element: TFP Bernoulli(probs=p).log_prob(x)
     // = log1p(-p)*(1-x) + log(p)*x with p = sigmoid(l)*(1-1e-6) + 1e-7.
     float* S = smem + wave * 32 * 33;  // per-wave 32x33 scratch (main loop done)
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
+    // one 32x32 accumulator tile; called with compile-time (i, j) so acc stays in registers
+    auto bern_tile = [&](const f32x16& t, const int i, const int j) {
         const int ncol0 = n0 + wn * TN * 32 + j * 32;
         const int n = ncol0 + (lane & 31);
         float vb[16];
@@ -212,27 +210,36 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs a) {
           const int ml = (r & 3) + 8 * (r >> 2) + rowq;
           const int m = m0 + wm * TM * 32 + i * 32 + ml;
           float val = 0.f, bce = 0.f;
-          if (m < M && n < N) {
-            const float l = acc[i][j][r];
-            const float xv = a.aux[(size_t)(m / a.x_row_div) * a.ldaux + n];
-            const float s = 1.f / (1.f + expf(-l));
-            const float p = __fadd_rn(__fmul_rn(s, kProbScale), kProbShift);
+          const bool ok = (m < M && n < N);
+          const float xv = ok ? a.aux[(size_t)(m / a.x_row_div) * a.ldaux + n] : 0.f;
+          const float l = t[r];
+          const float s = __fdividef(1.f, 1.f + __expf(-l));
+          const float p = __fadd_rn(__fmul_rn(s, kProbScale), kProbShift);
+          const float dsig = kProbScale * (s * (1.f - s));
+          float g = 0.f;
+          if (__all((xv == 0.f) || (xv == 1.f))) {
+            // binarised pixels (every wave of the hot path): one log per element.
+            // log(1-p) stands in for log1p(-p); they differ by <1e-7 absolute here.
+            const float sel = xv != 0.f ? p : 1.f - p;
+            val = __logf(sel);
+            g = (xv != 0.f ? 1.f : -1.f) * __fdividef(1.f, sel);
+          } else {
             const float lp1 = logf(p), lp0 = log1pf(-p);
             val = __fadd_rn(__fmul_rn(lp0, 1.f - xv), __fmul_rn(lp1, xv));
-            float gt = xv / p - (1.f - xv) / (1.f - p);
-            float gb = 0.f;
-            if (a.need_bce || a.wb != 0.f) {
-              const float pc = fminf(fmaxf(p, kKerasEps), 1.f - kKerasEps);
-              if (a.need_bce)
-                bce = xv * logf(pc + kKerasEps) + (1.f - xv) * logf(1.f - pc + kKerasEps);
-              const bool inr = (p >= kKerasEps) && (p <= 1.f - kKerasEps);
-              gb = inr ? (xv / (pc + kKerasEps) - (1.f - xv) / (1.f - pc + kKerasEps)) : 0.f;
-            }
-            if (a.store_g) {
-              const float g = (a.wa * gt + a.wb * gb) * kProbScale * (s * (1.f - s));
-              C[(size_t)m * a.ldc + n] = g;
-            }
+            g = xv / p - (1.f - xv) / (1.f - p);
           }
+          if (!ok) val = 0.f;
+          if (a.need_bce || a.wb != 0.f) {
+            const float pc = fminf(fmaxf(p, kKerasEps), 1.f - kKerasEps);
+            if (a.need_bce && ok)
+              bce = xv * logf(pc + kKerasEps) + (1.f - xv) * logf(1.f - pc + kKerasEps);
+            const bool inr = (p >= kKerasEps) && (p <= 1.f - kKerasEps);
+            const float gb = inr ? (xv / (pc + kKerasEps) - (1.f - xv) / (1.f - pc + kKerasEps)) : 0.f;
+            g = a.wa * g + a.wb * gb;
+          } else {
+            g = a.wa * g;
+          }
+          if (a.store_g && ok) C[(size_t)m * a.ldc + n] = g * dsig;
           S[ml * 33 + (lane & 31)] = val;
           vb[r] = bce;
         }
@@ -263,7 +270,12 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs a) {
           if (half == 0 && m < M && ncol0 < N) a.part2[(size_t)m * a.ldpart + ncol0 / 32] = sum;
           __syncthreads();
         }
-      }
+    };
+    bern_tile(acc[0][0], 0, 0);
+    if constexpr (TN > 1) bern_tile(acc[0][TN - 1], 0, TN - 1);
+    if constexpr (TM > 1) bern_tile(acc[TM - 1][0], TM - 1, 0);
+    if constexpr (TM > 1 && TN > 1) bern_tile(acc[TM - 1][TN - 1], TM - 1, TN - 1);
+    static_assert(TM <= 2 && TN <= 2, "bern_tile dispatch covers up to 2x2 tiles");
   }
 }
 

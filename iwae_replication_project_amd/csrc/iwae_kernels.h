@@ -55,6 +55,7 @@ struct GaussArgs {
   int kS, Bsplit, Bimg;                     // samples per image, images in group a, total images
   uint64_t seed; const uint64_t* rng_base; int layer;
   float* out; int accumulate;               // per-row log density (set or +=)
+  float* eps_out; int ld_eps_out;           // mode 0: keep the noise for the backward pass
   int M;
 };
 // mode 0: sample h = eps*scale+mu and log N(h; mu, scale)   (Encoder.call F:58-F:70)
@@ -65,8 +66,7 @@ hipError_t launch_gauss_fwd(hipStream_t st, int mode, const GaussArgs& a);
 struct GaussBwdArgs {
   const float* P; int ldP; int prow_div; int d;
   const float* H; int ldH;
-  const float* eps_a; const float* eps_b; int kS, Bsplit, Bimg;
-  uint64_t seed; const uint64_t* rng_base; int layer;
+  const float* eps_rows; int ld_eps;        // noise stored by the forward pass, [M][ld_eps]
   const float* src[4]; int ldsrc[4]; int nsrc;   // dL/dh contributions (dX outputs)
   int std_normal;            // this h is h_L: add dL/dlogp * (-h)
   const float* dlw;          // dL/dlw per row (dL/dlogp = dlw, dL/dlogq = -dlw)

@@ -106,7 +106,7 @@ struct iwae_handle {
   Mat x_in;
   std::vector<LayerBufs> eb, db;
   LayerBufs ob;                      // output MLP: y1 = o1, y2 = o2, P = g
-  std::vector<Mat> h, dh_out, dh_prior, dh_dec, dh_enc;
+  std::vector<Mat> h, eps_st, dh_out, dh_prior, dh_dec, dh_enc;
   float *logq = nullptr, *logp = nullptr, *lw = nullptr, *dlw = nullptr, *dpx = nullptr;
   float *dlw2 = nullptr, *dpx2 = nullptr, *contrib = nullptr, *part = nullptr, *part2 = nullptr;
   float *run_m = nullptr, *run_s = nullptr;
@@ -199,6 +199,7 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
   h->eb.assign(L, LayerBufs());
   h->db.assign(std::max(L - 1, 0), LayerBufs());
   h->h.assign(L, Mat());
+  h->eps_st.assign(L, Mat());
   h->dh_out.assign(1, Mat());
   h->dh_prior.assign(L, Mat());
   h->dh_dec.assign(L, Mat());
@@ -216,6 +217,7 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
       mat(h->eb[i].dY1, R, s.H);
     }
     mat(h->h[i], rows, s.d + 1);
+    if (train) mat(h->eps_st[i], rows, s.d);
   }
   for (int i = 0; i < L - 1; ++i) {
     const StochL& s = h->dec[i];
@@ -482,6 +484,7 @@ static int forward_core(iwae_handle* h, const Plan& P, const EpsSet& E, bool tra
     g.kS = kS; g.Bsplit = P.Bsplit; g.Bimg = P.Bimg;
     g.seed = h->seed; g.rng_base = &h->ds->rng[0]; g.layer = i;
     g.out = h->logq; g.accumulate = i > 0; g.M = M;
+    if (train) { g.eps_out = h->eps_st[i].p; g.ld_eps_out = h->eps_st[i].ld; }
     HIPCHK(launch_gauss_fwd(h->stream, 0, g));
   }
   // prior log p(h) (F:134-F:142)
@@ -572,14 +575,13 @@ static int decoder_bwd(iwae_handle* h, const Plan& P, const float* dlw, const fl
   return IWAE_OK;
 }
 
-static int encoder_bwd(iwae_handle* h, const Plan& P, const EpsSet& E, const float* dlw) {
+static int encoder_bwd(iwae_handle* h, const Plan& P, const float* dlw) {
   const int L = h->L, kS = P.kS, M = P.Bimg * kS;
   for (int i = L - 1; i >= 0; --i) {
     GaussBwdArgs g{};
     g.P = h->eb[i].P.p; g.ldP = h->eb[i].P.ld; g.prow_div = i == 0 ? kS : 1; g.d = h->enc[i].d;
     g.H = h->h[i].p; g.ldH = h->h[i].ld;
-    g.eps_a = E.a[i]; g.eps_b = E.b[i]; g.kS = kS; g.Bsplit = P.Bsplit; g.Bimg = P.Bimg;
-    g.seed = h->seed; g.rng_base = &h->ds->rng[1]; g.layer = i;
+    g.eps_rows = h->eps_st[i].p; g.ld_eps = h->eps_st[i].ld;
     int n = 0;
     if (i == 0) { g.src[n] = h->dh_out[0].p; g.ldsrc[n++] = h->dh_out[0].ld; }
     if (i <= L - 2) {
@@ -640,10 +642,10 @@ static int train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam)
   if (P.piwae) {
     CHK(decoder_bwd(h, P, h->dlw, h->dpx, true, false));      // decoder: IWAE_{k1 k2}
     CHK(decoder_bwd(h, P, h->dlw2, h->dpx2, false, true));    // encoder path: MIWAE(k1,k2)
-    CHK(encoder_bwd(h, P, E, h->dlw2));
+    CHK(encoder_bwd(h, P, h->dlw2));
   } else {
     CHK(decoder_bwd(h, P, h->dlw, h->dpx, true, true));
-    CHK(encoder_bwd(h, P, E, h->dlw));
+    CHK(encoder_bwd(h, P, h->dlw));
   }
   CHK(run_adam(h, true, true, adam, 1.f));
   return IWAE_OK;
