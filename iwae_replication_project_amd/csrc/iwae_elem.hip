@@ -141,15 +141,18 @@ __global__ __launch_bounds__(256) void gauss_bwd_enc_kernel(GaussBwdArgs a) {
     if (act) {
       const int r_begin = pr * a.prow_div;
       const int s_begin = per_image ? wave : 0, s_step = per_image ? 4 : 1;
-      for (int s = s_begin; s < a.prow_div; s += s_step) {
+      const int s_end = min(a.prow_div, a.M - r_begin);
+#pragma unroll 4
+      for (int s = s_begin; s < s_end; s += s_step) {
         const int r = r_begin + s;
-        if (r >= a.M) break;
         const float h = a.H[(size_t)r * a.ldH + j];
         const float ev = a.eps_rows[(size_t)r * a.ld_eps + j];
         const float dlq = -a.dlw[r];
         const float z = __fsub_rn(h / sc, mu / sc);
         float G = 0.f;
-        for (int q = 0; q < a.nsrc; ++q) G += a.src[q][(size_t)r * a.ldsrc[q] + j];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (q < a.nsrc) G += a.src[q][(size_t)r * a.ldsrc[q] + j];
         if (a.std_normal) G += a.dlw[r] * (-h);
         G += dlq * (-z / sc);
         amu += G + dlq * (z / sc);
@@ -212,9 +215,17 @@ hipError_t launch_gauss_bwd(hipStream_t st, int mode, const GaussBwdArgs& a) {
 // One wave per image.  lw = (logp + logpx) - logq (F:345, F:349) with logpx
 // the sum of the Bernoulli epilogue's per-32-column partials.
 __device__ __forceinline__ float row_sum_parts(const float* part, int ldpart, int npart, int r) {
-  const float* p = part + (size_t)r * ldpart;
+  // ldpart is a multiple of 4 and the pad columns are zero: independent float4
+  // loads (no serialized latency chain), summed in column order.
+  const float4* p = reinterpret_cast<const float4*>(part + (size_t)r * ldpart);
+  const int n4 = (npart + 3) >> 2;
+  float4 v[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) v[t] = t < n4 ? p[t] : make_float4(0.f, 0.f, 0.f, 0.f);
   float s = 0.f;
-  for (int t = 0; t < npart; ++t) s += p[t];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) s += ((v[t].x + v[t].y) + v[t].z) + v[t].w;
+  for (int t = 8; t < n4; ++t) s += ((p[t].x + p[t].y) + p[t].z) + p[t].w;
   return s;
 }
 __device__ __forceinline__ float lw_at(const BoundArgs& a, int r) {
@@ -224,28 +235,35 @@ __device__ __forceinline__ float lw_at(const BoundArgs& a, int r) {
 struct ImgBound {
   float val;
   float mx, se;  // IWAE / POWER
-  int lo, hi;    // MEDIAN (row offsets)
+  int lo, hi;    // MEDIAN (sample indices)
 };
 
-// value of the per-image bound; LSE-type statistics kept for the gradient pass
-__device__ ImgBound image_bound(const BoundArgs& a, int mode, int row0, float* sh) {
+// Per-image bound value.  lw of the image is staged in `sh` (LDS, one wave's
+// slice) when kS <= 1024, otherwise re-read from the lw row the same lane wrote.
+struct LwView {
+  const float* sh;   // LDS copy or nullptr
+  const float* g;    // global lw row (written by this wave, same-lane reads only)
+  __device__ float operator()(int q) const { return sh ? sh[q] : g[q]; }
+};
+
+__device__ ImgBound image_bound(const BoundArgs& a, int mode, const LwView& lw) {
   const int lane = threadIdx.x & 63;
   const int kS = a.kS;
   ImgBound o{0.f, 0.f, 0.f, 0, 0};
   if (mode == BM_NONE) return o;
   if (mode == BM_VAE) {
     float s = 0.f;
-    for (int q = lane; q < kS; q += 64) s += lw_at(a, row0 + q);
+    for (int q = lane; q < kS; q += 64) s += lw(q);
     o.val = wave_sum(s) / (float)kS;          // reduce_mean (F:430)
     return o;
   }
   if (mode == BM_IWAE || mode == BM_POWER) {
     const float pp = mode == BM_POWER ? a.p : 1.f;
     float mx = -INFINITY;
-    for (int q = lane; q < kS; q += 64) mx = fmaxf(mx, lw_at(a, row0 + q));
+    for (int q = lane; q < kS; q += 64) mx = fmaxf(mx, lw(q));
     mx = wave_max(mx);
     float se = 0.f;
-    for (int q = lane; q < kS; q += 64) se += expf((lw_at(a, row0 + q) - mx) * pp);
+    for (int q = lane; q < kS; q += 64) se += expf((lw(q) - mx) * pp);
     se = wave_sum(se);
     o.mx = mx; o.se = se;
     // F:369: log(reduce_mean(exp(lw - max))) + max ; F:408: .../p + max
@@ -254,40 +272,36 @@ __device__ ImgBound image_bound(const BoundArgs& a, int mode, int row0, float* s
   }
   if (mode == BM_MEDIAN) {
     // tfp.stats.percentile(50, 'midpoint') = mean of order statistics
-    // floor((k-1)/2) and ceil((k-1)/2) (F:377).  Rank by counting (kS <= 1024).
-    for (int q = lane; q < kS; q += 64) sh[q] = lw_at(a, row0 + q);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // floor((k-1)/2) and ceil((k-1)/2) (F:377).  Rank by counting (kS <= 1024, LDS).
     const int klo = (kS - 1) / 2, khi = kS / 2;
     float vlo = 0.f, vhi = 0.f;
     int ilo = 0, ihi = 0;
     for (int q = lane; q < kS; q += 64) {
-      const float v = sh[q];
+      const float v = lw.sh[q];
       int rank = 0;
       for (int t = 0; t < kS; ++t) {
-        const float u = sh[t];
+        const float u = lw.sh[t];
         rank += (u < v) || (u == v && t < q);
       }
       if (rank == klo) { vlo = v; ilo = q + 1; }
       if (rank == khi) { vhi = v; ihi = q + 1; }
     }
-    // exactly one lane found each rank: combine by max over (index+1 > 0) lanes
+    // exactly one lane found each rank
     vlo = wave_sum(ilo ? vlo : 0.f); vhi = wave_sum(ihi ? vhi : 0.f);
-    float flo = wave_max((float)ilo), fhi = wave_max((float)ihi);
+    const float flo = wave_max((float)ilo), fhi = wave_max((float)ihi);
     o.lo = (int)flo - 1; o.hi = (int)fhi - 1;
     o.val = (vlo + vhi) * 0.5f;
     return o;
   }
-  // BM_MIWAE: sample s = j*k1 + i; mean_j [log mean_i exp(lw - m_j) + m_j]
+  // BM_MIWAE: sample s = j*k1 + i; mean_j [log mean_i exp(lw - m_j) + m_j]  (LDS)
   float tot = 0.f;
   for (int j = 0; j < a.k2; ++j) {
-    const int g0 = row0 + j * a.k1;
+    const int g0 = j * a.k1;
     float mx = -INFINITY;
-    for (int i = lane; i < a.k1; i += 64) mx = fmaxf(mx, lw_at(a, g0 + i));
+    for (int i = lane; i < a.k1; i += 64) mx = fmaxf(mx, lw.sh[g0 + i]);
     mx = wave_max(mx);
     float se = 0.f;
-    for (int i = lane; i < a.k1; i += 64) se += expf(lw_at(a, g0 + i) - mx);
+    for (int i = lane; i < a.k1; i += 64) se += expf(lw.sh[g0 + i] - mx);
     se = wave_sum(se);
     tot += logf(se / (float)a.k1) + mx;
   }
@@ -295,9 +309,9 @@ __device__ ImgBound image_bound(const BoundArgs& a, int mode, int row0, float* s
   return o;
 }
 
-// dBound/dlw at row r (q = sample index) times coef
+// coef * dBound/dlw written to out[row0 + q]
 __device__ __forceinline__ void image_grad(const BoundArgs& a, int mode, int row0, const ImgBound& ib,
-                                           float coef, float* out) {
+                                           float coef, const LwView& lw, float* out) {
   const int lane = threadIdx.x & 63;
   const int kS = a.kS;
   if (mode == BM_NONE) {
@@ -306,22 +320,21 @@ __device__ __forceinline__ void image_grad(const BoundArgs& a, int mode, int row
     for (int q = lane; q < kS; q += 64) out[row0 + q] = coef / (float)kS;
   } else if (mode == BM_IWAE || mode == BM_POWER) {
     const float pp = mode == BM_POWER ? a.p : 1.f;
-    for (int q = lane; q < kS; q += 64)
-      out[row0 + q] = coef * (expf((lw_at(a, row0 + q) - ib.mx) * pp) / ib.se);
+    for (int q = lane; q < kS; q += 64) out[row0 + q] = coef * (expf((lw(q) - ib.mx) * pp) / ib.se);
   } else if (mode == BM_MEDIAN) {
     for (int q = lane; q < kS; q += 64)
       out[row0 + q] = coef * (0.5f * (q == ib.lo) + 0.5f * (q == ib.hi));
   } else {  // MIWAE
     for (int j = 0; j < a.k2; ++j) {
-      const int g0 = row0 + j * a.k1;
+      const int g0 = j * a.k1;
       float mx = -INFINITY;
-      for (int i = lane; i < a.k1; i += 64) mx = fmaxf(mx, lw_at(a, g0 + i));
+      for (int i = lane; i < a.k1; i += 64) mx = fmaxf(mx, lw.sh[g0 + i]);
       mx = wave_max(mx);
       float se = 0.f;
-      for (int i = lane; i < a.k1; i += 64) se += expf(lw_at(a, g0 + i) - mx);
+      for (int i = lane; i < a.k1; i += 64) se += expf(lw.sh[g0 + i] - mx);
       se = wave_sum(se);
       for (int i = lane; i < a.k1; i += 64)
-        out[g0 + i] = coef * (expf(lw_at(a, g0 + i) - mx) / se) / (float)a.k2;
+        out[row0 + g0 + i] = coef * (expf(lw.sh[g0 + i] - mx) / se) / (float)a.k2;
     }
   }
 }
@@ -339,14 +352,23 @@ __global__ __launch_bounds__(kBoundWaves * 64) void bound_kernel(BoundArgs a) {
     const int Bg = ga ? a.Bsplit : a.Bimg - a.Bsplit;
     const int row0 = b * a.kS;
     // log weights (for get_log_weights) and the optional Keras-BCE mean
+    const bool staged = a.kS <= 1024;
     float bsum = 0.f;
     for (int q = lane; q < a.kS; q += 64) {
       const int r = row0 + q;
-      a.lw[r] = lw_at(a, r);
+      const float v = lw_at(a, r);
+      a.lw[r] = v;
+      if (staged) sh_all[wave][q] = v;
       if (a.part2) bsum += row_sum_parts(a.part2, a.ldpart, a.npart, r);
     }
     bsum = wave_sum(bsum);
-    const ImgBound ib = image_bound(a, mode, row0, sh_all[wave]);
+    if (staged) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const LwView lwv{staged ? sh_all[wave] : nullptr, a.lw + row0};
+    const ImgBound ib = image_bound(a, mode, lwv);
     if (lane == 0) {
       float c = w * ib.val / (float)Bg;
       if (a.part2) c += a.bce_w * (bsum / (float)a.kS) / (float)Bg;
@@ -354,7 +376,7 @@ __global__ __launch_bounds__(kBoundWaves * 64) void bound_kernel(BoundArgs a) {
     }
     if (a.dlw) {
       // loss = -objective: dL/dlw = -(w/Bg) * dBound/dlw
-      image_grad(a, mode, row0, ib, -w / (float)Bg, a.dlw);
+      image_grad(a, mode, row0, ib, -w / (float)Bg, lwv, a.dlw);
       if (a.dpx) {
         for (int q = lane; q < a.kS; q += 64) {
           const int r = row0 + q;
@@ -363,8 +385,8 @@ __global__ __launch_bounds__(kBoundWaves * 64) void bound_kernel(BoundArgs a) {
       }
     }
     if (a.dlw2) {
-      const ImgBound ib2 = image_bound(a, a.mode2, row0, sh_all[wave]);
-      image_grad(a, a.mode2, row0, ib2, -w / (float)Bg, a.dlw2);
+      const ImgBound ib2 = image_bound(a, a.mode2, lwv);
+      image_grad(a, a.mode2, row0, ib2, -w / (float)Bg, lwv, a.dlw2);
       if (a.dpx2)
         for (int q = lane; q < a.kS; q += 64) a.dpx2[row0 + q] = a.dlw2[row0 + q];
     }
@@ -394,7 +416,8 @@ __global__ __launch_bounds__(kBoundWaves * 64) void bound_kernel(BoundArgs a) {
 
 hipError_t launch_bound(hipStream_t st, const BoundArgs& a) {
   if (a.Bimg <= 0) return hipSuccess;
-  if ((a.mode_a == BM_MEDIAN || a.mode_b == BM_MEDIAN || a.mode2 == BM_MEDIAN) && a.kS > 1024)
+  auto needs_lds = [](int m) { return m == BM_MEDIAN || m == BM_MIWAE; };
+  if ((needs_lds(a.mode_a) || needs_lds(a.mode_b) || needs_lds(a.mode2)) && a.kS > 1024)
     return hipErrorInvalidValue;
   // small batches: one workgroup (no cross-workgroup hand-off at all)
   const int rows = a.Bimg * a.kS;
@@ -489,25 +512,46 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const float b1p = powf(st.b1, t), b2p = powf(st.b2, t);
   const float alpha = st.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float omb1 = 1.f - st.b1, omb2 = 1.f - st.b2;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < sg.n;
+  const long long n4 = sg.n >> 2;    // segment sizes and offsets are multiples of 4 floats
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (long long)gridDim.x * blockDim.x) {
-    const long long pidx = sg.off + i;
-    float g;
+    const long long pidx = sg.off + 4 * i;
+    float4 g;
     if (a.read_slabs && sg.splits > 0) {
-      g = 0.f;
-      for (int s = 0; s < sg.splits; ++s) g += a.slabs[sg.slab_off + (long long)s * sg.n + i];
+      const float4* sl = reinterpret_cast<const float4*>(a.slabs + sg.slab_off) + i;
+      const long long st4 = sg.n >> 2;
+      float4 acc0 = make_float4(0.f, 0.f, 0.f, 0.f), acc1 = acc0;
+      int s = 0;
+      for (; s + 4 <= sg.splits; s += 4) {
+        const float4 u0 = sl[(long long)s * st4], u1 = sl[(long long)(s + 1) * st4];
+        const float4 u2 = sl[(long long)(s + 2) * st4], u3 = sl[(long long)(s + 3) * st4];
+        acc0.x += u0.x + u1.x; acc0.y += u0.y + u1.y; acc0.z += u0.z + u1.z; acc0.w += u0.w + u1.w;
+        acc1.x += u2.x + u3.x; acc1.y += u2.y + u3.y; acc1.z += u2.z + u3.z; acc1.w += u2.w + u3.w;
+      }
+      for (; s < sg.splits; ++s) {
+        const float4 u = sl[(long long)s * st4];
+        acc0.x += u.x; acc0.y += u.y; acc0.z += u.z; acc0.w += u.w;
+      }
+      g = make_float4(acc0.x + acc1.x, acc0.y + acc1.y, acc0.z + acc1.z, acc0.w + acc1.w);
     } else {
-      g = a.grad[pidx];
+      g = *reinterpret_cast<const float4*>(a.grad + pidx);
     }
-    if (a.write_grad) a.grad[pidx] = g;
+    if (a.write_grad) *reinterpret_cast<float4*>(a.grad + pidx) = g;
     if (a.do_adam) {
-      g = g * scale;
-      float m = a.m[pidx], v = a.v[pidx];
-      m = m + (g - m) * omb1;
-      v = v + (g * g - v) * omb2;
-      a.m[pidx] = m;
-      a.v[pidx] = v;
-      a.param[pidx] = a.param[pidx] - (m * alpha) / (sqrtf(v) + st.eps);
+      float4 m = *reinterpret_cast<const float4*>(a.m + pidx);
+      float4 v = *reinterpret_cast<const float4*>(a.v + pidx);
+      float4 p = *reinterpret_cast<const float4*>(a.param + pidx);
+      float gg[4] = {g.x * scale, g.y * scale, g.z * scale, g.w * scale};
+      float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w}, pp[4] = {p.x, p.y, p.z, p.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        mm[q] = mm[q] + (gg[q] - mm[q]) * omb1;
+        vv[q] = vv[q] + (gg[q] * gg[q] - vv[q]) * omb2;
+        pp[q] = pp[q] - (mm[q] * alpha) / (sqrtf(vv[q]) + st.eps);
+      }
+      *reinterpret_cast<float4*>(a.m + pidx) = make_float4(mm[0], mm[1], mm[2], mm[3]);
+      *reinterpret_cast<float4*>(a.v + pidx) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+      *reinterpret_cast<float4*>(a.param + pidx) = make_float4(pp[0], pp[1], pp[2], pp[3]);
     }
   }
 }
@@ -516,7 +560,7 @@ __global__ void adam_tick_kernel(AdamState* s) { s->t += 1; }
 
 hipError_t launch_adam(hipStream_t st, const AdamArgs& a, long long max_seg_n) {
   if (a.nseg <= 0) return hipSuccess;
-  long long bx = (max_seg_n + 255) / 256;
+  long long bx = (max_seg_n / 4 + 255) / 256;
   if (bx > 64) bx = 64;
   if (bx < 1) bx = 1;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)bx, a.nseg), dim3(256), 0, st, a);

@@ -418,6 +418,7 @@ static int make_plan(iwae_handle* h, const iwae_loss_config* lc, int B, Plan& P)
     case IWAE_LOSS_PIWAE:
       if (lc->k1 <= 0 || lc->k2 <= 0 || lc->k1 * lc->k2 != lc->k)
         return fail(h, IWAE_EINVAL, "MIWAE/PIWAE need k1*k2 == k");
+      if (lc->k > 1024) return fail(h, IWAE_EINVAL, "MIWAE/PIWAE support k <= 1024");
       P.k1 = lc->k1; P.k2 = lc->k2;
       if (lc->loss == IWAE_LOSS_MIWAE) {
         P.mode_a = BM_MIWAE;
