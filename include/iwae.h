@@ -95,6 +95,9 @@ int iwae_synchronize(iwae_handle* h);
 int iwae_set_seed(iwae_handle* h, unsigned long long seed);
 /* 1 = capture the Philox train step in a hipGraph per shape and replay it. */
 int iwae_set_graphs(iwae_handle* h, int enable);
+/* Kernel path: 0 auto (fused row-block kernels up to 65536 sample rows, then
+ * layer-wise GEMMs), 1 layer-wise only, 2 fused whenever the widths allow. */
+int iwae_set_path(iwae_handle* h, int path);
 
 /* --- parameters (synchronous host copies) --------------------------------- */
 /* Flat float32 in Keras trainable_weights order: encoder then decoder, per

@@ -1,0 +1,529 @@
+// Fused row-block kernels for the small-batch train step (gfx950).
+//
+// One workgroup owns up to 16 rows (sample rows, or images for the first
+// encoder layer) and runs a whole Stochastic_layer (F:22-F:38) -- or the
+// decoder's two hidden layers (F:92-F:93) -- on them in one launch:
+//
+//   forward : [sample the input h from the previous layer's (mu, scale)]
+//             y1 = tanh(x W1) -> y2 = tanh(y1 W2) -> P = y2 [Wmu|Wstd]
+//             [-> sample h ~ N(mu, exp(zs)+1e-6), log q]      (Encoder.call F:56-F:75)
+//             [-> log p(h_target | P)]                         (Decoder.get_log_ph F:134-F:142)
+//   backward: [dP from the sampling / prior log-density partials]
+//             dY2 = dP W_head^T (1-y2^2) -> dY1 = dY2 W2^T (1-y1^2) -> dX = dY1 W1^T
+//
+// Activations live in LDS between the three chained GEMMs (never re-read from
+// HBM); weights stream from L2 straight into registers (each weight element is
+// used by exactly one wave, so there is nothing to share through LDS).  The
+// matrix core is v_mfma_f32_16x16x4_f32 (exact f32, 16-row tiles); the waves
+// of the workgroup split the output columns, two 16x16 tiles per wave in
+// flight to cover the 40-cycle dependent-accumulator latency.
+//
+// Philox counters, noise layout and every formula are the ones of the
+// layer-wise path (iwae_elem.hip), so both paths produce the same numbers up
+// to f32 summation order.
+#include "iwae_kernels.h"
+
+namespace iwae {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int RB_ROWS = 16;     // MFMA tile height = rows per workgroup (max)
+constexpr int RB_WAVES = 8;     // 512 threads
+
+__device__ __forceinline__ float rb_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ float rb_philox_normal(uint64_t seed, uint64_t base, unsigned row, unsigned layer,
+                                                  unsigned col) {
+  unsigned c0 = row, c1 = (layer << 20) | col, c2 = (unsigned)base, c3 = (unsigned)(base >> 32);
+  unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const unsigned lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const unsigned lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  const float u0 = ((float)c0 + 0.5f) * 2.3283064365386963e-10f;
+  const float u1 = ((float)c1 + 0.5f) * 2.3283064365386963e-10f;
+  return sqrtf(-2.f * logf(u0)) * cospif(2.f * u1);
+}
+
+__device__ __forceinline__ float rb_eps(const RbNoise& nz, int d, int r, int j, uint64_t base) {
+  const int bi = r / nz.kS, s = r - bi * nz.kS;
+  if (bi < nz.Bsplit) {
+    if (nz.eps_a) return nz.eps_a[((size_t)s * nz.Bsplit + bi) * d + j];
+  } else {
+    if (nz.eps_b) return nz.eps_b[((size_t)s * (nz.Bimg - nz.Bsplit) + (bi - nz.Bsplit)) * d + j];
+  }
+  return rb_philox_normal(nz.seed, base, (unsigned)r, (unsigned)nz.layer, (unsigned)j);
+}
+
+// OUT[16][N] = act(A[16][K] . B), A in LDS (zero-padded past K), B from global.
+// BT = false: B(k,n) = W[k*ldw + n] (forward, W_aug = [W; b]); k-step 4, scalar loads.
+// BT = true : B(k,n) = W[n*ldw + k] (backward, W^T); permuted k order so each
+//             lane loads 4 consecutive k with one 16-B load per 4 MFMAs.
+template <bool BT>
+__device__ void rb_dense(const float* A, int lda, const RbStage& S, int row0, int nrows, float* O, int ldo) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int K = S.K, N = S.N, ldw = S.ldw;
+  const float* W = S.W;
+  const int ntile = (N + 15) >> 4;
+  for (int t0 = wave; t0 < ntile; t0 += 2 * RB_WAVES) {
+    const int t1 = t0 + RB_WAVES;
+    const bool has1 = t1 < ntile;
+    const int na = t0 * 16 + r, nb = t1 * 16 + r;
+    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+    // Loads are unconditional on clamped addresses (selected to 0 when out of
+    // range) and issued one chunk ahead of the MFMAs that consume them, so the
+    // L2 latency of the weight stream overlaps the matrix-core work.
+    const int nca = min(na, N - 1), ncb = has1 ? min(nb, N - 1) : nca;
+    const bool oka = na < N, okb = has1 && nb < N;
+    if (!BT) {
+      constexpr int CH = 8;                         // k-steps of 4 per chunk
+      const int nsteps = (K + 3) >> 2;
+      const int nch = (nsteps + CH - 1) / CH;
+      float pa[CH], pb[CH];
+      auto fetch = [&](int ch, float* xa, float* xb) {
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int k = (ch * CH + u) * 4 + g;
+          const int kc = min(k, K - 1);
+          const float va = W[(size_t)kc * ldw + nca];
+          const float vb = W[(size_t)kc * ldw + ncb];
+          xa[u] = (k < K && oka) ? va : 0.f;
+          xb[u] = (k < K && okb) ? vb : 0.f;
+        }
+      };
+      fetch(0, pa, pb);
+      for (int ch = 0; ch < nch; ++ch) {
+        float qa[CH], qb[CH];
+        if (ch + 1 < nch) fetch(ch + 1, qa, qb);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int k = (ch * CH + u) * 4 + g;
+          const float av = A[r * lda + k];
+          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pa[u], c0, 0, 0, 0);
+          if (has1) c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pb[u], c1, 0, 0, 0);
+        }
+        if (ch + 1 < nch) {
+#pragma unroll
+          for (int u = 0; u < CH; ++u) { pa[u] = qa[u]; pb[u] = qb[u]; }
+        }
+      }
+    } else {
+      constexpr int CH = 4;                         // float4 k-steps (16 k) per chunk
+      const int nsteps = (K + 15) >> 4;
+      const int nch = (nsteps + CH - 1) / CH;
+      float4 pa[CH], pb[CH];
+      auto fetch = [&](int ch, float4* xa, float4* xb) {
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int k0 = (ch * CH + u) * 16 + 4 * g;
+          const int kc = min(k0, ((K - 1) & ~3));
+          const float4 va = *reinterpret_cast<const float4*>(W + (size_t)nca * ldw + kc);
+          const float4 vb = *reinterpret_cast<const float4*>(W + (size_t)ncb * ldw + kc);
+          const bool ka = k0 < K && oka, kb = k0 < K && okb;
+          xa[u] = ka ? va : make_float4(0.f, 0.f, 0.f, 0.f);
+          xb[u] = kb ? vb : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      };
+      fetch(0, pa, pb);
+      for (int ch = 0; ch < nch; ++ch) {
+        float4 qa[CH], qb[CH];
+        if (ch + 1 < nch) fetch(ch + 1, qa, qb);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int k0 = (ch * CH + u) * 16 + 4 * g;
+          const float4 a4 = *reinterpret_cast<const float4*>(A + r * lda + k0);
+          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, pa[u].x, c0, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, pa[u].y, c0, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, pa[u].z, c0, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, pa[u].w, c0, 0, 0, 0);
+          if (has1) {
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, pb[u].x, c1, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, pb[u].y, c1, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, pb[u].z, c1, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, pb[u].w, c1, 0, 0, 0);
+          }
+        }
+        if (ch + 1 < nch) {
+#pragma unroll
+          for (int u = 0; u < CH; ++u) { pa[u] = qa[u]; pb[u] = qb[u]; }
+        }
+      }
+    }
+    // epilogue: C[row = 4g + i][col = t*16 + r]
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (q == 1 && !has1) break;
+      const f32x4 c = q == 0 ? c0 : c1;
+      const int n = (q == 0 ? t0 : t1) * 16 + r;
+      if (n < N) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = 4 * g + i;
+          float v = c[i];
+          if (S.act == 1) {
+            v = tanhf(v);
+          } else if (S.act == 2) {
+            const float y = row < nrows ? S.y[(size_t)(row0 + row) * S.ldy + n] : 0.f;
+            v = v * (1.f - y * y);
+          }
+          if (O) O[row * ldo + n] = v;
+          if (S.out_g && row < nrows) S.out_g[(size_t)(row0 + row) * S.ld_out + n] = v;
+        }
+      }
+    }
+  }
+}
+
+// Copy rows [row0, row0+nrows) x [0, width) of a global matrix into LDS [16][lda],
+// zero-filling padding rows/columns up to `pad_to` columns.
+__device__ __forceinline__ void rb_load(float* A, int lda, const float* G, int ldg, int width, int pad_to,
+                                        int row0, int nrows) {
+  for (int e = threadIdx.x; e < RB_ROWS * pad_to; e += blockDim.x) {
+    const int row = e / pad_to, col = e - row * pad_to;
+    float v = 0.f;
+    if (row < nrows && col < width) v = G[(size_t)(row0 + row) * ldg + col];
+    A[row * lda + col] = v;
+  }
+}
+
+// set the ones column (bias row of W_aug) and zero the padding of an LDS buffer
+__device__ __forceinline__ void rb_pad(float* A, int lda, int width, int pad_to, bool ones) {
+  for (int e = threadIdx.x; e < RB_ROWS * (pad_to - width); e += blockDim.x) {
+    const int row = e / (pad_to - width), col = width + e % (pad_to - width);
+    A[row * lda + col] = (ones && col == width) ? 1.f : 0.f;
+  }
+}
+
+__device__ __forceinline__ int rb_k_pad(int K, bool bt) { return bt ? ((K + 15) & ~15) : ((K + 3) & ~3); }
+
+// ------------------------------------------------------------------ forward
+__global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
+  extern __shared__ __attribute__((aligned(16))) float rbs[];
+  // job lookup
+  int jb = 0;
+  while (jb + 1 < L.njobs && (int)blockIdx.x >= L.block_start[jb + 1]) ++jb;
+  const RbFwdJob& J = L.job[jb];
+  const int blk = blockIdx.x - L.block_start[jb];
+  const int row0 = blk * J.rpb;
+  const int nrows = min(J.rpb, J.rows - row0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* buf[3] = {rbs, rbs + RB_ROWS * L.ld_lds, rbs + 2 * RB_ROWS * L.ld_lds};
+  float* rowq = rbs + 3 * RB_ROWS * L.ld_lds;         // [16] log q of the sampled input
+  float* rowp = rowq + RB_ROWS;                        // [16] log N(input; 0, 1)
+  const int lda = L.ld_lds;
+  uint64_t base = 0;
+  if (L.rng_base) base = *L.rng_base;
+
+  // ---- input rows
+  const int K0 = J.st[0].K;                 // fin + 1 (ones column)
+  const int K0p = rb_k_pad(K0, false);
+  if (J.pr_slabs) {
+    // first encoder layer: y1 = tanh(sum of the split-K partial products of x W1)
+    const int H = J.pr_H;
+    for (int e = threadIdx.x; e < RB_ROWS * K0p; e += blockDim.x) {
+      const int rr = e / K0p, c = e - rr * K0p;
+      float v = 0.f;
+      if (rr < nrows && c < H) {
+        const float* sp = J.pr_slabs + (size_t)(row0 + rr) * J.pr_ld + c;
+        float acc = 0.f;
+        for (int q = 0; q < J.pr_nslab; ++q) acc += sp[(size_t)q * J.pr_stride];
+        v = tanhf(acc);
+        J.pr_y[(size_t)(row0 + rr) * J.pr_ldy + c] = v;
+      } else if (c == H) {
+        v = 1.f;
+      }
+      buf[0][rr * lda + c] = v;
+    }
+  } else if (J.pro_sample) {
+    // h = eps * scale + mu from the previous layer's P (Normal.sample, F:59/F:68)
+    const int d = J.ps_d;
+    for (int rr = wave; rr < RB_ROWS; rr += RB_WAVES) {
+      float accq = 0.f, accp = 0.f;
+      for (int j0 = 0; j0 < K0p; j0 += 64) {
+        const int j = j0 + lane;
+        float hv = 0.f;
+        if (rr < nrows && j < d) {
+          const int rg = row0 + rr;
+          const int pr = rg / J.ps_div;
+          const float mu = J.ps_P[(size_t)pr * J.ps_ldP + j];
+          const float zs = J.ps_P[(size_t)pr * J.ps_ldP + d + j];
+          const float sc = __fadd_rn(expf(zs), kScaleEps);
+          const float e = rb_eps(J.ps_noise, d, rg, j, base);
+          hv = __fadd_rn(__fmul_rn(e, sc), mu);
+          J.ps_h[(size_t)rg * J.ps_ldh + j] = hv;
+          if (J.ps_eps) J.ps_eps[(size_t)rg * J.ps_ldeps + j] = e;
+          const float z = __fsub_rn(hv / sc, mu / sc);
+          accq += __fsub_rn(-0.5f * (z * z), __fadd_rn(kHalfLog2Pi, logf(sc)));
+          accp += __fsub_rn(-0.5f * (hv * hv), kHalfLog2Pi);
+        } else if (j == d) {
+          hv = 1.f;                          // ones column (bias row of W_aug)
+        }
+        if (j < K0p) buf[0][rr * lda + j] = hv;
+      }
+      accq = rb_wave_sum(accq);
+      accp = rb_wave_sum(accp);
+      if (lane == 0) { rowq[rr] = accq; rowp[rr] = accp; }
+    }
+  } else {
+    rb_load(buf[0], lda, J.in, J.ld_in, K0, K0p, row0, nrows);
+    if (J.pro_stdnormal) {
+      // log N(h; 0, 1) summed over the latent dims (F:135-F:136)
+      for (int rr = wave; rr < RB_ROWS; rr += RB_WAVES) {
+        float acc = 0.f;
+        if (rr < nrows)
+          for (int j = lane; j < K0 - 1; j += 64) {
+            const float hv = J.in[(size_t)(row0 + rr) * J.ld_in + j];
+            acc += __fsub_rn(-0.5f * (hv * hv), kHalfLog2Pi);
+          }
+        acc = rb_wave_sum(acc);
+        if (lane == 0) rowp[rr] = acc;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- chained Dense layers; stage s reads buf[s % 3] and writes buf[(s+1) % 3]
+  for (int s = 0; s < J.nst; ++s) {
+    const RbStage& S = J.st[s];
+    float* out = buf[(s + 1) % 3];
+    if (s + 1 < J.nst) {
+      const int Kn = J.st[s + 1].K;        // next K = N + 1 (ones column)
+      rb_pad(out, lda, S.N, rb_k_pad(Kn, false), true);
+    }
+    __syncthreads();
+    rb_dense<false>(buf[s % 3], lda, S, row0, nrows, out, lda);
+    __syncthreads();
+  }
+  const float* P = buf[J.nst % 3];
+
+  // ---- epilogue
+  if (J.epi == 1) {
+    // encoder: sample the next h and add its log q (F:68, F:70, F:73)
+    const int d = J.ep_d;
+    for (int rr = wave; rr < RB_ROWS; rr += RB_WAVES) {
+      if (rr >= nrows) continue;
+      const int rg = row0 + rr;
+      float acc = 0.f;
+      for (int j = lane; j < d; j += 64) {
+        const float mu = P[rr * lda + j], zs = P[rr * lda + d + j];
+        const float sc = __fadd_rn(expf(zs), kScaleEps);
+        const float e = rb_eps(J.ep_noise, d, rg, j, base);
+        const float hv = __fadd_rn(__fmul_rn(e, sc), mu);
+        J.ep_h[(size_t)rg * J.ep_ldh + j] = hv;
+        if (J.ep_eps) J.ep_eps[(size_t)rg * J.ep_ldeps + j] = e;
+        const float z = __fsub_rn(hv / sc, mu / sc);
+        acc += __fsub_rn(-0.5f * (z * z), __fadd_rn(kHalfLog2Pi, logf(sc)));
+      }
+      acc = rb_wave_sum(acc);
+      if (lane == 0) {
+        const float prev = J.pro_sample ? rowq[rr] : (J.logq_acc ? J.logq[rg] : 0.f);
+        J.logq[rg] = prev + acc;
+      }
+    }
+  } else if (J.epi == 2) {
+    // decoder prior: log p(h_t | h_src) added to log p (F:139-F:141)
+    const int d = J.ep_d;
+    for (int rr = wave; rr < RB_ROWS; rr += RB_WAVES) {
+      if (rr >= nrows) continue;
+      const int rg = row0 + rr;
+      float acc = 0.f;
+      for (int j = lane; j < d; j += 64) {
+        const float mu = P[rr * lda + j], zs = P[rr * lda + d + j];
+        const float sc = __fadd_rn(expf(zs), kScaleEps);
+        const float hv = J.ep_tgt[(size_t)rg * J.ep_ldtgt + j];
+        const float z = __fsub_rn(hv / sc, mu / sc);
+        acc += __fsub_rn(-0.5f * (z * z), __fadd_rn(kHalfLog2Pi, logf(sc)));
+      }
+      acc = rb_wave_sum(acc);
+      if (lane == 0) {
+        const float prev = J.pro_stdnormal ? rowp[rr] : (J.logp_acc ? J.logp[rg] : 0.f);
+        J.logp[rg] = prev + acc;
+      }
+    }
+  }
+  if (threadIdx.x < nrows) {
+    const int rg = row0 + threadIdx.x;
+    if (J.epi != 1 && J.pro_sample && J.logq) J.logq[rg] = rowq[threadIdx.x];
+    if (J.epi != 2 && J.pro_stdnormal && J.logp) J.logp[rg] = rowp[threadIdx.x];
+  }
+}
+
+// ----------------------------------------------------------------- backward
+__global__ __launch_bounds__(RB_WAVES * 64) void rb_bwd_kernel(RbBwdLaunch L) {
+  extern __shared__ __attribute__((aligned(16))) float rbs[];
+  int jb = 0;
+  while (jb + 1 < L.njobs && (int)blockIdx.x >= L.block_start[jb + 1]) ++jb;
+  const RbBwdJob& J = L.job[jb];
+  const int blk = blockIdx.x - L.block_start[jb];
+  const int row0 = blk * J.rpb;
+  const int nrows = min(J.rpb, J.rows - row0);
+  const int lda = L.ld_lds;
+  float* buf[3] = {rbs, rbs + RB_ROWS * lda, rbs + 2 * RB_ROWS * lda};
+  float* red = rbs + 3 * RB_ROWS * lda;     // [4][2][128] partial sums (pro 3)
+
+  const int K0 = J.nst > 0 ? J.st[0].K : 0;   // = width of dP / dZ
+  const int K0p = rb_k_pad(K0, true);
+  float* D = buf[0];
+  if (J.pro == 0) {
+    rb_load(D, lda, J.dz_in, J.ld_dz_in, K0, K0p, row0, nrows);
+  } else if (J.pro == 1 || J.pro == 2) {
+    // per row: dP of an encoder sampling layer (pro 1) or a decoder prior head (pro 2)
+    const int d = J.d;
+    for (int e = threadIdx.x; e < RB_ROWS * K0p; e += blockDim.x) {
+      const int rr = e / K0p, c = e - rr * K0p;
+      if (c >= d || rr >= nrows) {
+        if (c >= 2 * d || rr >= nrows) D[rr * lda + c] = 0.f;
+        continue;
+      }
+      const int rg = row0 + rr;
+      const float mu = J.P[(size_t)rg * J.ldP + c];
+      const float zs = J.P[(size_t)rg * J.ldP + d + c];
+      const float ez = expf(zs);
+      const float sc = __fadd_rn(ez, kScaleEps);
+      const float hv = J.H[(size_t)rg * J.ldH + c];
+      const float z = __fsub_rn(hv / sc, mu / sc);
+      const float dl = J.dlw[rg];
+      float dmu, dsc;
+      if (J.pro == 2) {
+        // log p(h_t | .): dL/dlogp = dlw; the target h gets -z/s (kept for the encoder pass)
+        J.dh_out[(size_t)rg * J.ld_dh + c] = dl * (-z / sc);
+        dmu = dl * (z / sc);
+        dsc = dl * ((z * z - 1.f) / sc);
+      } else {
+        const float ev = J.eps[(size_t)rg * J.ld_eps + c];
+        const float dlq = -dl;
+        float G = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (q < J.nsrc) G += J.src[q][(size_t)rg * J.ldsrc[q] + c];
+        if (J.std_normal) G += dl * (-hv);
+        G += dlq * (-z / sc);
+        dmu = G + dlq * (z / sc);
+        dsc = G * ev + dlq * ((z * z - 1.f) / sc);
+        if (J.kl_coef != 0.f) {
+          dmu += J.kl_coef * mu / (float)J.kl_rows;
+          dsc += J.kl_coef * (sc - 1.f / sc) / (float)J.kl_rows;
+        }
+      }
+      const float dzs = dsc * ez;
+      D[rr * lda + c] = dmu;
+      D[rr * lda + d + c] = dzs;
+      J.dP_out[(size_t)rg * J.ld_dP + c] = dmu;
+      J.dP_out[(size_t)rg * J.ld_dP + d + c] = dzs;
+    }
+  } else {
+    // pro 3: first encoder layer, rows = images; reduce the sampling-layer
+    // partials over the kS sample rows of each image (mu, scale broadcast over k)
+    const int d = J.d, kS = J.kS;
+    for (int e = threadIdx.x; e < RB_ROWS * K0p; e += blockDim.x) {
+      const int rr = e / K0p, c = e - rr * K0p;
+      if (c >= 2 * d || rr >= nrows) D[rr * lda + c] = 0.f;
+    }
+    const int grp = threadIdx.x >> 7, tj = threadIdx.x & 127;   // 4 sample groups x 128 columns
+    for (int rr = 0; rr < nrows; ++rr) {
+      const int img = row0 + rr;
+      for (int j0 = 0; j0 < d; j0 += 128) {
+        const int c = j0 + tj;
+        float amu = 0.f, asc = 0.f, mu = 0.f, sc = 1.f, ez = 0.f;
+        if (c < d) {
+          mu = J.P[(size_t)img * J.ldP + c];
+          const float zs = J.P[(size_t)img * J.ldP + d + c];
+          ez = expf(zs);
+          sc = __fadd_rn(ez, kScaleEps);
+#pragma unroll 4
+          for (int s = grp; s < kS; s += 4) {
+            const int rg = img * kS + s;
+            const float hv = J.H[(size_t)rg * J.ldH + c];
+            const float ev = J.eps[(size_t)rg * J.ld_eps + c];
+            const float dl = J.dlw[rg], dlq = -dl;
+            const float z = __fsub_rn(hv / sc, mu / sc);
+            float G = 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (q < J.nsrc) G += J.src[q][(size_t)rg * J.ldsrc[q] + c];
+            if (J.std_normal) G += dl * (-hv);
+            G += dlq * (-z / sc);
+            amu += G + dlq * (z / sc);
+            asc += G * ev + dlq * ((z * z - 1.f) / sc);
+          }
+        }
+        red[(grp * 2 + 0) * 128 + tj] = amu;
+        red[(grp * 2 + 1) * 128 + tj] = asc;
+        __syncthreads();
+        if (grp == 0 && c < d) {
+          amu = red[0 * 128 + tj] + red[2 * 128 + tj] + red[4 * 128 + tj] + red[6 * 128 + tj];
+          asc = red[1 * 128 + tj] + red[3 * 128 + tj] + red[5 * 128 + tj] + red[7 * 128 + tj];
+          if (J.kl_coef != 0.f) {
+            amu += J.kl_coef * mu / (float)J.kl_rows;
+            asc += J.kl_coef * (sc - 1.f / sc) / (float)J.kl_rows;
+          }
+          const float dzs = asc * ez;
+          D[rr * lda + c] = amu;
+          D[rr * lda + d + c] = dzs;
+          J.dP_out[(size_t)img * J.ld_dP + c] = amu;
+          J.dP_out[(size_t)img * J.ld_dP + d + c] = dzs;
+        }
+        __syncthreads();
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- chain of transposed Dense layers (dX = dZ W^T, tanh-grad on the way)
+  for (int s = 0; s < J.nst; ++s) {
+    const RbStage& S = J.st[s];
+    float* out = buf[(s + 1) % 3];
+    const bool last = s + 1 == J.nst;
+    if (!last) rb_pad(out, lda, S.N, rb_k_pad(J.st[s + 1].K, true), false);
+    __syncthreads();
+    rb_dense<true>(buf[s % 3], lda, S, row0, nrows, last ? nullptr : out, lda);
+    __syncthreads();
+  }
+}
+
+static int launch_blocks(int njobs, const int* rows, const int* rpb, int* start) {
+  int tot = 0;
+  for (int i = 0; i < njobs; ++i) {
+    start[i] = tot;
+    tot += (rows[i] + rpb[i] - 1) / rpb[i];
+  }
+  start[njobs] = tot;
+  return tot;
+}
+
+hipError_t launch_rb_fwd(hipStream_t st, RbFwdLaunch& L) {
+  int rows[kRbMaxJobs], rpb[kRbMaxJobs];
+  for (int i = 0; i < L.njobs; ++i) { rows[i] = L.job[i].rows; rpb[i] = L.job[i].rpb; }
+  const int nb = launch_blocks(L.njobs, rows, rpb, L.block_start);
+  if (nb <= 0) return hipSuccess;
+  const size_t lds = (size_t)(3 * RB_ROWS * L.ld_lds + 2 * RB_ROWS) * sizeof(float);
+  hipLaunchKernelGGL(rb_fwd_kernel, dim3(nb), dim3(RB_WAVES * 64), lds, st, L);
+  return hipGetLastError();
+}
+
+hipError_t launch_rb_bwd(hipStream_t st, RbBwdLaunch& L) {
+  int rows[kRbMaxJobs], rpb[kRbMaxJobs];
+  for (int i = 0; i < L.njobs; ++i) { rows[i] = L.job[i].rows; rpb[i] = L.job[i].rpb; }
+  const int nb = launch_blocks(L.njobs, rows, rpb, L.block_start);
+  if (nb <= 0) return hipSuccess;
+  const size_t lds = (size_t)(3 * RB_ROWS * L.ld_lds + 8 * 128) * sizeof(float);
+  hipLaunchKernelGGL(rb_bwd_kernel, dim3(nb), dim3(RB_WAVES * 64), lds, st, L);
+  return hipGetLastError();
+}
+
+hipError_t rb_setup_attributes() {
+  hipError_t e = hipFuncSetAttribute((const void*)rb_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)rb_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+}  // namespace iwae

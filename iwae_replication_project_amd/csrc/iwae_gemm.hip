@@ -31,7 +31,7 @@ namespace iwae {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KSCALE>
-__global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs a) {
+__device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const int by, const int bz) {
   constexpr int NTH = WM * WN * 64;
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 16;
   // k-major LDS images.  Transposed (scalar) writes want a row stride = 2 mod 32
@@ -50,8 +50,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int kbeg = blockIdx.z * a.kchunk;
+  const int m0 = by * BM, n0 = bx * BN;
+  const int kbeg = bz * a.kchunk;
   const int kend = min(a.K, kbeg + a.kchunk);
   const int M = a.M, N = a.N;
 
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs a) {
         const int gk = k0 + kr, gn = n0 + 4 * nq;
         if (gk < kend && gn < N) {
           v = *reinterpret_cast<const float4*>(a.B + (size_t)gk * a.ldb + gn);
-          if (KSCALE) {
+          if (KSCALE && a.kscale) {
             const float s = a.kscale[gk];
             v.x *= s; v.y *= s; v.z *= s; v.w *= s;
           }
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs a) {
   }
 
   // ---------------------------------------------------------------- epilogue
-  float* C = a.C + (size_t)blockIdx.z * a.c_split_stride;
+  float* C = a.C + (size_t)bz * a.c_split_stride;
   const int rowq = 4 * (lane >> 5);
   if (EPI != EPI_BERN) {
 #pragma unroll
@@ -277,6 +277,38 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs a) {
     if constexpr (TM > 1 && TN > 1) bern_tile(acc[TM - 1][TN - 1], TM - 1, TN - 1);
     static_assert(TM <= 2 && TN <= 2, "bern_tile dispatch covers up to 2x2 tiles");
   }
+}
+
+template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KSCALE>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs a) {
+  gemm_body<WM, WN, TM, TN, TA, TB, EPI, KSCALE>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// Several independent GEMMs of one kind in ONE launch (the weight gradients of
+// every Dense layer): workgroup b runs tile (b - start[i]) of GEMM i.
+template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KSCALE>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_group_kernel(GemmGroup gg) {
+  const int b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < gg.n && b >= gg.start[i + 1]) ++i;
+  const int local = b - gg.start[i];
+  const int tx = gg.tiles_x[i], ty = gg.tiles_y[i];
+  gemm_body<WM, WN, TM, TN, TA, TB, EPI, KSCALE>(gg.g[i], local % tx, (local / tx) % ty, local / (tx * ty));
+}
+
+hipError_t launch_gemm_group_bwd_weight(hipStream_t st, GemmGroup& gg) {
+  if (gg.n <= 0) return hipSuccess;
+  constexpr int BM = 64, BN = 64;
+  int tot = 0;
+  for (int i = 0; i < gg.n; ++i) {
+    gg.start[i] = tot;
+    gg.tiles_x[i] = (gg.g[i].N + BN - 1) / BN;
+    gg.tiles_y[i] = (gg.g[i].M + BM - 1) / BM;
+    tot += gg.tiles_x[i] * gg.tiles_y[i] * gg.splits[i];
+  }
+  gg.start[gg.n] = tot;
+  hipLaunchKernelGGL((gemm_group_kernel<2, 2, 1, 1, true, false, EPI_STORE, true>), dim3(tot), dim3(256), 0, st, gg);
+  return hipGetLastError();
 }
 
 template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KS>

@@ -46,6 +46,17 @@ struct GemmArgs {
 hipError_t launch_gemm(hipStream_t st, GemmKind kind, GemmEpi epi, int tile, int splits,
                        bool kscale, const GemmArgs& a);
 
+// grouped backward-weight GEMMs (64x64 tiles, split over K = rows)
+constexpr int kMaxGroup = 16;
+struct GemmGroup {
+  GemmArgs g[kMaxGroup];
+  int splits[kMaxGroup];
+  int start[kMaxGroup + 1];
+  int tiles_x[kMaxGroup], tiles_y[kMaxGroup];
+  int n;
+};
+hipError_t launch_gemm_group_bwd_weight(hipStream_t st, GemmGroup& gg);
+
 // ------------------------------------------------------------ Gaussians ----
 struct GaussArgs {
   const float* P; int ldP; int prow_div;   // head output rows (mu | zs), row = r / prow_div
@@ -135,6 +146,62 @@ struct AdamArgs {
   float grad_scale_override;   // >0: use this instead of state->grad_scale
 };
 hipError_t launch_adam(hipStream_t st, const AdamArgs& a, long long max_seg_n);
+
+// ------------------------------------------------- fused row-block kernels ----
+struct RbNoise {             // where a sampling layer's eps comes from (see eps_at)
+  const float* eps_a; const float* eps_b;
+  int kS, Bsplit, Bimg;
+  uint64_t seed; int layer;
+};
+struct RbStage {             // one Dense layer of a chain
+  const float* W; int ldw;   // W_aug [fin+1][ldw]
+  int K, N;                  // fwd: K = fin+1, N = fout; bwd: K = fout, N = fin
+  int act;                   // 0 none, 1 tanh, 2 tanh-grad (times 1 - y^2)
+  float* out_g; int ld_out;  // global copy of the stage output (rows of the job)
+  const float* y; int ldy;   // act 2: forward tanh output on the input side
+};
+constexpr int kRbMaxJobs = 4;
+struct RbFwdJob {
+  int rows, rpb;
+  const float* in; int ld_in;                  // input rows (with ones column) unless sampled
+  int pro_sample;                              // input h = eps*scale + mu of ps_P[row / ps_div]
+  const float* ps_P; int ps_ldP, ps_div, ps_d;
+  float* ps_h; int ps_ldh; float* ps_eps; int ps_ldeps; RbNoise ps_noise;
+  int pro_stdnormal;                           // log N(input h; 0, 1) into log p
+  const float* pr_slabs; int pr_nslab, pr_ld, pr_H; long long pr_stride;  // input = tanh(sum of split-K slabs)
+  float* pr_y; int pr_ldy;                     // ... also stored as the layer's y1
+  int nst; RbStage st[3];
+  int epi;                                     // 0 none, 1 encoder sample, 2 decoder prior
+  int ep_d; RbNoise ep_noise;
+  float* ep_h; int ep_ldh; float* ep_eps; int ep_ldeps;
+  const float* ep_tgt; int ep_ldtgt;
+  float* logq; int logq_acc; float* logp; int logp_acc;
+};
+struct RbFwdLaunch {
+  RbFwdJob job[kRbMaxJobs];
+  int block_start[kRbMaxJobs + 1];
+  int njobs, ld_lds;
+  const uint64_t* rng_base;
+};
+struct RbBwdJob {
+  int rows, rpb;
+  int pro;                   // 0 load dZ; 1 encoder sampling bwd; 2 decoder prior bwd; 3 encoder layer 0 (per image)
+  const float* dz_in; int ld_dz_in;
+  const float* P; int ldP; int d;
+  const float* H; int ldH; const float* eps; int ld_eps; const float* dlw;
+  const float* src[4]; int ldsrc[4]; int nsrc;
+  int std_normal; float kl_coef; int kl_rows; int kS;
+  float* dP_out; int ld_dP; float* dh_out; int ld_dh;
+  int nst; RbStage st[3];
+};
+struct RbBwdLaunch {
+  RbBwdJob job[kRbMaxJobs];
+  int block_start[kRbMaxJobs + 1];
+  int njobs, ld_lds;
+};
+hipError_t launch_rb_fwd(hipStream_t st, RbFwdLaunch& L);
+hipError_t launch_rb_bwd(hipStream_t st, RbBwdLaunch& L);
+hipError_t rb_setup_attributes();
 
 hipError_t launch_fill_col(hipStream_t st, float* buf, int rows, int ld, int col, float v);
 hipError_t launch_transpose_lw(hipStream_t st, const float* lw_img, int Bimg, int kS, float* out);

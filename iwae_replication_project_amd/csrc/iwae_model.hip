@@ -112,6 +112,9 @@ struct iwae_handle {
   float *run_m = nullptr, *run_s = nullptr;
   int ldpart = 0, npart = 0;
   float* slabs = nullptr;
+  float* fslab = nullptr;            // split-K partials of the first encoder layer (fused path)
+  int fslab_S = 0;
+  int path = 0;                      // 0 auto, 1 layer-wise kernels, 2 fused row-block kernels
   // graphs
   bool use_graphs = false;
   std::map<std::vector<long long>, hipGraphExec_t> graphs;
@@ -252,6 +255,8 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
   vec(h->logq, rows); vec(h->logp, rows); vec(h->lw, rows);
   vec(h->dlw, rows); vec(h->dpx, rows); vec(h->dlw2, rows); vec(h->dpx2, rows);
   vec(h->contrib, Bimg); vec(h->run_m, Bimg); vec(h->run_s, Bimg);
+  h->fslab_S = (int)std::min<long long>(16, cdiv(h->xdim + 1, 64));
+  vec(h->fslab, (size_t)h->fslab_S * Bimg * r4(h->enc[0].H + 1));
   size_t slab_total = 0;
   if (train) {
     for (auto& d : h->dense) {
@@ -472,7 +477,11 @@ static int parse_eps(iwae_handle* h, const Plan& P, const float* const* eps, int
 }
 
 // Encoder + prior + output layer.  Leaves part/logp/logq (and g when train).
+static bool use_fused(const iwae_handle* h, const Plan& P);
+static int fused_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool train);
+
 static int forward_core(iwae_handle* h, const Plan& P, const EpsSet& E, bool train) {
+  if (use_fused(h, P)) return fused_forward(h, P, E, train);
   const int L = h->L, kS = P.kS, M = P.Bimg * kS;
   // encoder (F:56-F:75)
   CHK(stoch_fwd(h, h->enc[0], h->x_in, P.Bimg, h->eb[0]));
@@ -636,8 +645,330 @@ static int copy_x(iwae_handle* h, const Plan& P, const float* x) {
   return IWAE_OK;
 }
 
+// ------------------------------------------------------- fused row-block path
+constexpr int kRbMaxWidth = 512;   // widest LDS row the row-block kernels accept
+
+static int rb_width_ok(const iwae_handle* h) {
+  for (const auto& d : h->dense) {
+    if (&d == &h->dense[h->enc[0].l1] || &d == &h->dense[h->o3]) continue;   // run as GEMMs
+    if (d.fin + 1 > kRbMaxWidth || d.fout + 1 > kRbMaxWidth) return 0;
+  }
+  return 1;
+}
+
+static bool use_fused(const iwae_handle* h, const Plan& P) {
+  if (h->path == 1 || h->L > kRbMaxJobs) return false;
+  if (!rb_width_ok(h)) return false;
+  if (h->path == 2) return true;
+  return (long long)P.Bimg * P.kS <= 65536;
+}
+
+static int rb_ld(const iwae_handle* h, bool bwd) {
+  int w = 0;
+  for (const auto& d : h->dense) w = std::max(w, std::max(d.fin + 1, d.fout + 1));
+  w = std::min(w, kRbMaxWidth);
+  w = (w + 15) & ~15;
+  return bwd ? ((w + 31) & ~31) + 4 : ((w + 31) & ~31) + 2;
+}
+
+static RbStage rb_fwd_stage(iwae_handle* h, int di, int act, Mat* out) {
+  const DenseL& d = h->dense[di];
+  RbStage s{};
+  s.W = h->params + d.off; s.ldw = d.ldw; s.K = d.fin + 1; s.N = d.fout; s.act = act;
+  if (out) { s.out_g = out->p; s.ld_out = out->ld; }
+  return s;
+}
+
+static RbStage rb_bwd_stage(iwae_handle* h, int di, const Mat* y, Mat* out) {
+  const DenseL& d = h->dense[di];
+  RbStage s{};
+  s.W = h->params + d.off; s.ldw = d.ldw; s.K = d.fout; s.N = d.fin; s.act = y ? 2 : 0;
+  if (y) { s.y = y->p; s.ldy = y->ld; }
+  if (out) { s.out_g = out->p; s.ld_out = out->ld; }
+  return s;
+}
+
+static RbNoise rb_noise(iwae_handle* h, const Plan& P, const EpsSet& E, int layer) {
+  RbNoise n{};
+  n.eps_a = E.a[layer]; n.eps_b = E.b[layer];
+  n.kS = P.kS; n.Bsplit = P.Bsplit; n.Bimg = P.Bimg;
+  n.seed = h->seed; n.layer = layer;
+  return n;
+}
+
+static int fused_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool train) {
+  const int L = h->L, kS = P.kS, M = P.Bimg * kS;
+  // (1) first encoder Dense (K = 785) as a split-K GEMM into partial slabs
+  {
+    const DenseL& d = h->dense[h->enc[0].l1];
+    GemmArgs a{};
+    a.A = h->x_in.p; a.lda = h->x_in.ld;
+    a.B = h->params + d.off; a.ldb = d.ldw;
+    a.C = h->fslab; a.ldc = h->eb[0].y1.ld;
+    a.M = P.Bimg; a.N = d.fout; a.K = d.fin + 1;
+    a.kchunk = (int)(cdiv(cdiv(a.K, h->fslab_S), 16) * 16);
+    const int S = (int)cdiv(a.K, a.kchunk);
+    a.c_split_stride = (long long)P.Bimg * a.ldc;
+    CHK(prof_begin(h, GEMM_FWD, EPI_STORE, 2.0 * P.Bimg * d.fout * d.fin));
+    HIPCHK(launch_gemm(h->stream, GEMM_FWD, EPI_STORE, 0, S, false, a));
+    CHK(prof_end(h, GEMM_FWD, EPI_STORE));
+    // (2) rest of encoder layer 0 on the images: tanh(sum) -> l2 -> head (P0)
+    RbFwdLaunch Lf{};
+    Lf.ld_lds = rb_ld(h, false);
+    Lf.rng_base = &h->ds->rng[0];
+    RbFwdJob& J = Lf.job[0];
+    J.rows = P.Bimg; J.rpb = 4;
+    J.pr_slabs = h->fslab; J.pr_nslab = S; J.pr_ld = a.ldc; J.pr_H = d.fout; J.pr_stride = a.c_split_stride;
+    J.pr_y = h->eb[0].y1.p; J.pr_ldy = h->eb[0].y1.ld;
+    J.nst = 2;
+    J.st[0] = rb_fwd_stage(h, h->enc[0].l2, 1, &h->eb[0].y2);
+    J.st[1] = rb_fwd_stage(h, h->enc[0].head, 0, &h->eb[0].P);
+    Lf.njobs = 1;
+    HIPCHK(launch_rb_fwd(h->stream, Lf));
+  }
+  // (3) encoder layers 1..L-1 (layer 1 samples h1 from P0 in its prologue)
+  for (int i = 1; i < L; ++i) {
+    RbFwdLaunch Lf{};
+    Lf.ld_lds = rb_ld(h, false);
+    Lf.rng_base = &h->ds->rng[0];
+    RbFwdJob& J = Lf.job[0];
+    J.rows = M; J.rpb = 16;
+    if (i == 1) {
+      J.pro_sample = 1;
+      J.ps_P = h->eb[0].P.p; J.ps_ldP = h->eb[0].P.ld; J.ps_div = kS; J.ps_d = h->enc[0].d;
+      J.ps_h = h->h[0].p; J.ps_ldh = h->h[0].ld;
+      J.ps_eps = train ? h->eps_st[0].p : nullptr; J.ps_ldeps = train ? h->eps_st[0].ld : 0;
+      J.ps_noise = rb_noise(h, P, E, 0);
+    } else {
+      J.in = h->h[i - 1].p; J.ld_in = h->h[i - 1].ld;
+      J.logq_acc = 1;
+    }
+    const StochL& S = h->enc[i];
+    J.nst = 3;
+    J.st[0] = rb_fwd_stage(h, S.l1, 1, &h->eb[i].y1);
+    J.st[1] = rb_fwd_stage(h, S.l2, 1, &h->eb[i].y2);
+    J.st[2] = rb_fwd_stage(h, S.head, 0, &h->eb[i].P);
+    J.epi = 1; J.ep_d = S.d; J.ep_noise = rb_noise(h, P, E, i);
+    J.ep_h = h->h[i].p; J.ep_ldh = h->h[i].ld;
+    J.ep_eps = train ? h->eps_st[i].p : nullptr; J.ep_ldeps = train ? h->eps_st[i].ld : 0;
+    J.logq = h->logq;
+    Lf.njobs = 1;
+    HIPCHK(launch_rb_fwd(h->stream, Lf));
+  }
+  // (4) decoder prior layers and the output MLP's two hidden layers
+  {
+    RbFwdLaunch Lf{};
+    Lf.ld_lds = rb_ld(h, false);
+    Lf.rng_base = &h->ds->rng[0];
+    int nj = 0;
+    if (L >= 2) {
+      RbFwdJob& J = Lf.job[nj++];
+      J.rows = M; J.rpb = 16;
+      J.in = h->h[L - 1].p; J.ld_in = h->h[L - 1].ld;
+      J.pro_stdnormal = 1;                                   // log N(h_L; 0, 1)
+      const StochL& S = h->dec[0];
+      J.nst = 3;
+      J.st[0] = rb_fwd_stage(h, S.l1, 1, &h->db[0].y1);
+      J.st[1] = rb_fwd_stage(h, S.l2, 1, &h->db[0].y2);
+      J.st[2] = rb_fwd_stage(h, S.head, 0, &h->db[0].P);
+      J.epi = 2; J.ep_d = S.d; J.ep_tgt = h->h[L - 2].p; J.ep_ldtgt = h->h[L - 2].ld;
+      J.logp = h->logp;
+    }
+    {
+      RbFwdJob& J = Lf.job[nj++];
+      J.rows = M; J.rpb = 16;
+      if (L == 1) {
+        J.pro_sample = 1;
+        J.ps_P = h->eb[0].P.p; J.ps_ldP = h->eb[0].P.ld; J.ps_div = kS; J.ps_d = h->enc[0].d;
+        J.ps_h = h->h[0].p; J.ps_ldh = h->h[0].ld;
+        J.ps_eps = train ? h->eps_st[0].p : nullptr; J.ps_ldeps = train ? h->eps_st[0].ld : 0;
+        J.ps_noise = rb_noise(h, P, E, 0);
+        J.pro_stdnormal = 1;
+        J.logq = h->logq; J.logp = h->logp;
+      } else {
+        J.in = h->h[0].p; J.ld_in = h->h[0].ld;
+      }
+      J.nst = 2;
+      J.st[0] = rb_fwd_stage(h, h->o1, 1, &h->ob.y1);
+      J.st[1] = rb_fwd_stage(h, h->o2, 1, &h->ob.y2);
+    }
+    Lf.njobs = nj;
+    HIPCHK(launch_rb_fwd(h->stream, Lf));
+  }
+  // deeper decoder layers (L >= 3) accumulate into log p one launch at a time
+  for (int i = 1; i < L - 1; ++i) {
+    RbFwdLaunch Lf{};
+    Lf.ld_lds = rb_ld(h, false);
+    RbFwdJob& J = Lf.job[0];
+    J.rows = M; J.rpb = 16;
+    J.in = h->h[L - 1 - i].p; J.ld_in = h->h[L - 1 - i].ld;
+    const StochL& S = h->dec[i];
+    J.nst = 3;
+    J.st[0] = rb_fwd_stage(h, S.l1, 1, &h->db[i].y1);
+    J.st[1] = rb_fwd_stage(h, S.l2, 1, &h->db[i].y2);
+    J.st[2] = rb_fwd_stage(h, S.head, 0, &h->db[i].P);
+    J.epi = 2; J.ep_d = S.d; J.ep_tgt = h->h[L - 2 - i].p; J.ep_ldtgt = h->h[L - 2 - i].ld;
+    J.logp = h->logp; J.logp_acc = 1;
+    Lf.njobs = 1;
+    HIPCHK(launch_rb_fwd(h->stream, Lf));
+  }
+  // (5) output layer 200 -> 784 with the fused Bernoulli epilogue
+  {
+    GemmArgs ex{};
+    ex.aux = h->x_in.p; ex.ldaux = h->x_in.ld; ex.x_row_div = kS;
+    ex.part = h->part; ex.part2 = h->part2; ex.ldpart = h->ldpart;
+    ex.wa = P.wa; ex.wb = P.wb;
+    ex.store_g = train ? 1 : 0;
+    ex.need_bce = P.need_bce;
+    Mat gm = h->ob.P;
+    if (!train) { gm.p = nullptr; gm.ld = 0; }
+    CHK(gemm_fwd(h, EPI_BERN, h->ob.y2, M, h->dense[h->o3], gm, ex));
+  }
+  return IWAE_OK;
+}
+
+// decoder backward: output MLP + prior layers (which: 1 = weights' dZ only, 2 = dh only, 3 = both)
+static int fused_decoder_bwd(iwae_handle* h, const Plan& P, const float* dlw, const float* dpx, bool need_dh) {
+  const int L = h->L, M = P.Bimg * P.kS;
+  if (L > kRbMaxJobs) return fail(h, IWAE_EINVAL, "fused path supports up to 4 stochastic layers");
+  CHK(gemm_bwd_data(h, h->ob.P, M, h->dense[h->o3], h->ob.dY2, &h->ob.y2, dpx));
+  RbBwdLaunch Lb{};
+  Lb.ld_lds = rb_ld(h, true);
+  int nj = 0;
+  {
+    RbBwdJob& J = Lb.job[nj++];
+    J.rows = M; J.rpb = 16; J.pro = 0;
+    J.dz_in = h->ob.dY2.p; J.ld_dz_in = h->ob.dY2.ld;
+    J.nst = need_dh ? 2 : 1;
+    J.st[0] = rb_bwd_stage(h, h->o2, &h->ob.y1, &h->ob.dY1);
+    if (need_dh) J.st[1] = rb_bwd_stage(h, h->o1, nullptr, &h->dh_out[0]);
+  }
+  for (int i = 0; i < L - 1 && nj < kRbMaxJobs; ++i) {
+    const int t = L - 2 - i, src = L - 1 - i;
+    const StochL& S = h->dec[i];
+    RbBwdJob& J = Lb.job[nj++];
+    J.rows = M; J.rpb = 16; J.pro = 2;
+    J.P = h->db[i].P.p; J.ldP = h->db[i].P.ld; J.d = S.d;
+    J.H = h->h[t].p; J.ldH = h->h[t].ld; J.dlw = dlw;
+    J.dP_out = h->db[i].dP.p; J.ld_dP = h->db[i].dP.ld;
+    J.dh_out = h->dh_prior[t].p; J.ld_dh = h->dh_prior[t].ld;
+    J.nst = need_dh ? 3 : 2;
+    J.st[0] = rb_bwd_stage(h, S.head, &h->db[i].y2, &h->db[i].dY2);
+    J.st[1] = rb_bwd_stage(h, S.l2, &h->db[i].y1, &h->db[i].dY1);
+    if (need_dh) J.st[2] = rb_bwd_stage(h, S.l1, nullptr, &h->dh_dec[src]);
+  }
+  Lb.njobs = nj;
+  HIPCHK(launch_rb_bwd(h->stream, Lb));
+  return IWAE_OK;
+}
+
+static int fused_encoder_bwd(iwae_handle* h, const Plan& P, const float* dlw) {
+  const int L = h->L, kS = P.kS, M = P.Bimg * kS;
+  for (int i = L - 1; i >= 0; --i) {
+    const StochL& S = h->enc[i];
+    RbBwdLaunch Lb{};
+    Lb.ld_lds = rb_ld(h, true);
+    RbBwdJob& J = Lb.job[0];
+    J.pro = i == 0 ? 3 : 1;
+    J.rows = i == 0 ? P.Bimg : M;
+    J.rpb = i == 0 ? 1 : 16;
+    J.kS = kS;
+    J.P = h->eb[i].P.p; J.ldP = h->eb[i].P.ld; J.d = S.d;
+    J.H = h->h[i].p; J.ldH = h->h[i].ld;
+    J.eps = h->eps_st[i].p; J.ld_eps = h->eps_st[i].ld;
+    J.dlw = dlw;
+    int n = 0;
+    if (i == 0) { J.src[n] = h->dh_out[0].p; J.ldsrc[n++] = h->dh_out[0].ld; }
+    if (i <= L - 2) {
+      J.src[n] = h->dh_prior[i].p; J.ldsrc[n++] = h->dh_prior[i].ld;
+      J.src[n] = h->dh_enc[i].p; J.ldsrc[n++] = h->dh_enc[i].ld;
+    }
+    if (i >= 1) { J.src[n] = h->dh_dec[i].p; J.ldsrc[n++] = h->dh_dec[i].ld; }
+    J.nsrc = n;
+    J.std_normal = i == L - 1;
+    if (P.kl && i == L - 1) { J.kl_coef = 1.f; J.kl_rows = (L == 1) ? P.Bimg : M; }
+    J.dP_out = h->eb[i].dP.p; J.ld_dP = h->eb[i].dP.ld;
+    J.nst = i == 0 ? 2 : 3;
+    J.st[0] = rb_bwd_stage(h, S.head, &h->eb[i].y2, &h->eb[i].dY2);
+    J.st[1] = rb_bwd_stage(h, S.l2, &h->eb[i].y1, &h->eb[i].dY1);
+    if (i > 0) J.st[2] = rb_bwd_stage(h, S.l1, nullptr, &h->dh_enc[i - 1]);
+    Lb.njobs = 1;
+    HIPCHK(launch_rb_bwd(h->stream, Lb));
+  }
+  return IWAE_OK;
+}
+
+// all weight gradients (X_aug^T dZ, split over rows) in grouped launches
+static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const float* dpx) {
+  const int L = h->L, M = P.Bimg * P.kS;
+  struct WJ { int di; const Mat* A; const Mat* dZ; int rows; const float* ks; };
+  std::vector<WJ> js;
+  if (enc) {
+    for (int i = 0; i < L; ++i) {
+      const StochL& S = h->enc[i];
+      const int rows = i == 0 ? P.Bimg : M;
+      js.push_back({S.l1, i == 0 ? &h->x_in : &h->h[i - 1], &h->eb[i].dY1, rows, nullptr});
+      js.push_back({S.l2, &h->eb[i].y1, &h->eb[i].dY2, rows, nullptr});
+      js.push_back({S.head, &h->eb[i].y2, &h->eb[i].dP, rows, nullptr});
+    }
+  }
+  if (dec) {
+    for (int i = 0; i < L - 1; ++i) {
+      const StochL& S = h->dec[i];
+      js.push_back({S.l1, &h->h[L - 1 - i], &h->db[i].dY1, M, nullptr});
+      js.push_back({S.l2, &h->db[i].y1, &h->db[i].dY2, M, nullptr});
+      js.push_back({S.head, &h->db[i].y2, &h->db[i].dP, M, nullptr});
+    }
+    js.push_back({h->o1, &h->h[0], &h->ob.dY1, M, nullptr});
+    js.push_back({h->o2, &h->ob.y1, &h->ob.dY2, M, nullptr});
+    js.push_back({h->o3, &h->ob.y2, &h->ob.P, M, dpx});
+  }
+  for (size_t b = 0; b < js.size(); b += kMaxGroup) {
+    GemmGroup gg{};
+    for (size_t q = b; q < std::min(js.size(), b + kMaxGroup); ++q) {
+      const WJ& w = js[q];
+      DenseL& d = h->dense[w.di];
+      GemmArgs& a = gg.g[gg.n];
+      a.A = w.A->p; a.lda = w.A->ld;
+      a.B = w.dZ->p; a.ldb = w.dZ->ld;
+      a.C = h->slabs + d.slab_off; a.ldc = d.ldw;
+      a.M = d.fin + 1; a.N = d.fout; a.K = w.rows;
+      long long S = std::min<long long>(d.max_splits, std::max(1LL, cdiv(w.rows, 64)));
+      const int kchunk = (int)(cdiv(cdiv(w.rows, S), 16) * 16);
+      S = cdiv(w.rows, kchunk);
+      d.splits = (int)S;
+      a.kchunk = kchunk;
+      a.c_split_stride = d.size();
+      a.kscale = w.ks;
+      gg.splits[gg.n] = (int)S;
+      gg.n++;
+    }
+    HIPCHK(launch_gemm_group_bwd_weight(h->stream, gg));
+  }
+  return IWAE_OK;
+}
+
+static int fused_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
+  CHK(fused_forward(h, P, E, true));
+  CHK(run_bound(h, P, true, -1.f, &h->ds->scalars[0]));
+  if (P.piwae) {
+    CHK(fused_decoder_bwd(h, P, h->dlw, h->dpx, false));      // decoder weights: IWAE_{k1 k2}
+    CHK(weight_grads(h, P, false, true, h->dpx));
+    CHK(fused_decoder_bwd(h, P, h->dlw2, h->dpx2, true));     // encoder path: MIWAE(k1, k2)
+    CHK(fused_encoder_bwd(h, P, h->dlw2));
+    CHK(weight_grads(h, P, true, false, nullptr));
+  } else {
+    CHK(fused_decoder_bwd(h, P, h->dlw, h->dpx, true));
+    CHK(fused_encoder_bwd(h, P, h->dlw));
+    CHK(weight_grads(h, P, true, true, h->dpx));
+  }
+  CHK(run_adam(h, true, true, adam, 1.f));
+  return IWAE_OK;
+}
+
 // forward + backward (+ Adam) after x is staged
 static int train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
+  if (use_fused(h, P)) return fused_train_body(h, P, E, adam);
   CHK(forward_core(h, P, E, true));
   CHK(run_bound(h, P, true, -1.f, &h->ds->scalars[0]));
   if (P.piwae) {
@@ -764,6 +1095,12 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
     return nullptr;
   }
   h->grad = h->grad_own;
+  e = rb_setup_attributes();
+  if (e != hipSuccess) {
+    g_create_error = std::string("hipFuncSetAttribute failed: ") + hipGetErrorString(e);
+    iwae_destroy(h);
+    return nullptr;
+  }
   return h;
 }
 
@@ -806,6 +1143,15 @@ int iwae_set_seed(iwae_handle* h, unsigned long long seed) {
   uint64_t z[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(h->ds->rng, z, sizeof(z), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  return IWAE_OK;
+}
+
+int iwae_set_path(iwae_handle* h, int path) {
+  if (!h) return IWAE_EINVAL;
+  if (path < 0 || path > 2) return fail(h, IWAE_EINVAL, "path must be 0 (auto), 1 (layer-wise) or 2 (fused)");
+  h->path = path;
+  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+  h->graphs.clear();
   return IWAE_OK;
 }
 

@@ -159,7 +159,8 @@ class Flexible_Model:
 
     def __init__(self, n_hidden_encoder, n_hidden_decoder, n_latent_encoder, n_latent_decoder,
                  dataset_bias="Binarized_MNIST", loss_function="VAE", k=50, p=1, alpha=1, beta=0.5,
-                 *, k1=None, k2=None, x_dim=784, device=None, seed=None, use_graphs=True, **kwargs):
+                 *, k1=None, k2=None, x_dim=784, device=None, seed=None, use_graphs=True,
+                 kernel_path="auto", **kwargs):
         self.dense = architecture(n_hidden_encoder, n_hidden_decoder, n_latent_encoder, n_latent_decoder, x_dim)
         loss_config(loss_function, k, p, alpha, beta, k1, k2)   # validate early
         if not torch.cuda.is_available():
@@ -201,6 +202,10 @@ class Flexible_Model:
             seed = int.from_bytes(os.urandom(8), "little")
         self._call(self._lib.iwae_set_seed(h, int(seed) & ((1 << 64) - 1)))
         self._call(self._lib.iwae_set_graphs(h, 1 if use_graphs else 0))
+        paths = {"auto": 0, "layerwise": 1, "fused": 2}
+        if kernel_path not in paths:
+            raise ValueError(f"kernel_path must be one of {tuple(paths)}")
+        self._call(self._lib.iwae_set_path(h, paths[kernel_path]))
         rng = np.random.default_rng(int(seed) & ((1 << 63) - 1))
         self.set_weights(glorot_weights(self.dense, rng, resolve_dataset_bias(dataset_bias, x_dim)))
         self._loss_buf = torch.zeros(1, device=self.device)
