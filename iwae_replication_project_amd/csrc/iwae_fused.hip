@@ -106,7 +106,9 @@ __device__ void rb_dense(const float* A, int lda, const RbStage& S, int row0, in
 #pragma unroll
         for (int u = 0; u < CH; ++u) {
           const int k = (ch * CH + u) * 4 + g;
-          const float av = A[r * lda + k];
+          // the last chunk may run past K: never read LDS there (stale bits
+          // could be NaN and NaN * 0 != 0)
+          const float av = k < K ? A[r * lda + k] : 0.f;
           c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pa[u], c0, 0, 0, 0);
           if (has1) c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pb[u], c1, 0, 0, 0);
         }
@@ -139,7 +141,8 @@ __device__ void rb_dense(const float* A, int lda, const RbStage& S, int row0, in
 #pragma unroll
         for (int u = 0; u < CH; ++u) {
           const int k0 = (ch * CH + u) * 16 + 4 * g;
-          const float4 a4 = *reinterpret_cast<const float4*>(A + r * lda + k0);
+          const float4 a4 = k0 < K ? *reinterpret_cast<const float4*>(A + r * lda + k0)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
           c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, pa[u].x, c0, 0, 0, 0);
           c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, pa[u].y, c0, 0, 0, 0);
           c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, pa[u].z, c0, 0, 0, 0);
