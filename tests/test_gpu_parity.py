@@ -157,8 +157,9 @@ def test_c2_full_size_iwae_train_step_matches_oracle():
     ref_loss, ref_new, ref_g = O.train_step(params, spec, x, eps, "IWAE", k, opt)
     assert abs(loss - ref_loss) <= REL * abs(ref_loss)
     assert rel_l2(flat(m.get_gradients()), ref_g) <= REL
-    # first Adam step moves each weight by up to ~lr; allow 0.5% of it
-    np.testing.assert_allclose(flat(m.get_weights()), O.flatten_params(spec, ref_new), atol=5e-6)
+    # Adam's first step lr*g/(|g|+eps) amplifies gradient rounding by up to lr/eps = 10
+    # for near-zero gradients: allow 2% of lr on the updated weights
+    np.testing.assert_allclose(flat(m.get_weights()), O.flatten_params(spec, ref_new), atol=2e-5)
 
 
 @pytest.mark.parametrize("loss", ["IWAE", "CIWAE", "PIWAE", "VAE_V1", "L_alpha", "L_median"])
@@ -183,7 +184,7 @@ def test_fused_and_layerwise_paths_agree(arch, loss):
     (a1, a2, ga, wa), (b1, b2, gb, wb) = outs
     assert abs(a1 - b1) <= REL * abs(a1) and abs(a2 - b2) <= REL * abs(a2)
     assert rel_l2(gb, ga) <= REL
-    np.testing.assert_allclose(wb, wa, atol=1e-6)
+    np.testing.assert_allclose(wb, wa, atol=2e-5)      # see the Adam note above
 
 
 # ----------------------------------------------- multi-step training parity
