@@ -62,102 +62,103 @@ __device__ __forceinline__ float rb_eps(const RbNoise& nz, int d, int r, int j, 
   return rb_philox_normal(nz.seed, base, (unsigned)r, (unsigned)nz.layer, (unsigned)j);
 }
 
-// OUT[16][N] = act(A[16][K] . B), A in LDS (zero-padded past K), B from global.
-// BT = false: B(k,n) = W[k*ldw + n] (forward, W_aug = [W; b]); k-step 4, scalar loads.
+extern __shared__ __attribute__((aligned(16))) float rbs[];
+
+// chunk widths of the k loops (the LDS operand is zero-padded up to them)
+constexpr int RB_FWD_KCH = 32;   // 8 MFMA k-steps of 4
+constexpr int RB_BWD_KCH = 64;   // 4 float4 k-steps of 16
+__device__ __forceinline__ int rb_k_pad(int K, bool bt) {
+  return bt ? ((K + RB_BWD_KCH - 1) / RB_BWD_KCH) * RB_BWD_KCH : ((K + RB_FWD_KCH - 1) / RB_FWD_KCH) * RB_FWD_KCH;
+}
+
+// OUT[16][N] = act(A[16][K] . B).  A is the LDS image at offset `ao` (row
+// stride lda, zero from K up to rb_k_pad(K)); B streams from global memory.
+// BT = false: B(k,n) = W[k*ldw + n] (forward, W_aug = [W; b]); scalar loads.
 // BT = true : B(k,n) = W[n*ldw + k] (backward, W^T); permuted k order so each
 //             lane loads 4 consecutive k with one 16-B load per 4 MFMAs.
+// Weight addresses are clamped into the matrix instead of masked, so every
+// load is unconditional (no exec-masked branch, no per-load wait): values
+// fetched for k >= K meet zeros in A, columns n >= N are never stored.
 template <bool BT>
-__device__ void rb_dense(const float* A, int lda, const RbStage& S, int row0, int nrows, float* O, int ldo) {
+__device__ void rb_dense(int ao, int lda, const RbStage& S, int row0, int nrows, int oo, int ldo) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int K = S.K, N = S.N, ldw = S.ldw;
-  const float* W = S.W;
+  const float* __restrict__ W = S.W;
   const int ntile = (N + 15) >> 4;
   for (int t0 = wave; t0 < ntile; t0 += 2 * RB_WAVES) {
     const int t1 = t0 + RB_WAVES;
     const bool has1 = t1 < ntile;
-    const int na = t0 * 16 + r, nb = t1 * 16 + r;
+    const int na = min(t0 * 16 + r, N - 1), nb = has1 ? min(t1 * 16 + r, N - 1) : na;
     f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-    // Loads are unconditional on clamped addresses (selected to 0 when out of
-    // range) and issued one chunk ahead of the MFMAs that consume them, so the
-    // L2 latency of the weight stream overlaps the matrix-core work.
-    const int nca = min(na, N - 1), ncb = has1 ? min(nb, N - 1) : nca;
-    const bool oka = na < N, okb = has1 && nb < N;
     if (!BT) {
-      constexpr int CH = 8;                         // k-steps of 4 per chunk
-      const int nsteps = (K + 3) >> 2;
-      const int nch = (nsteps + CH - 1) / CH;
+      constexpr int CH = RB_FWD_KCH / 4;
+      const int nch = (K + RB_FWD_KCH - 1) / RB_FWD_KCH;
+      const float* __restrict__ Wa = W + na;
+      const float* __restrict__ Wb = W + nb;
       float pa[CH], pb[CH];
-      auto fetch = [&](int ch, float* xa, float* xb) {
 #pragma unroll
-        for (int u = 0; u < CH; ++u) {
-          const int k = (ch * CH + u) * 4 + g;
-          const int kc = min(k, K - 1);
-          const float va = W[(size_t)kc * ldw + nca];
-          const float vb = W[(size_t)kc * ldw + ncb];
-          xa[u] = (k < K && oka) ? va : 0.f;
-          xb[u] = (k < K && okb) ? vb : 0.f;
-        }
-      };
-      fetch(0, pa, pb);
+      for (int u = 0; u < CH; ++u) {
+        const int kc = min(u * 4 + g, K - 1);
+        pa[u] = Wa[(size_t)kc * ldw];
+        pb[u] = Wb[(size_t)kc * ldw];
+      }
       for (int ch = 0; ch < nch; ++ch) {
         float qa[CH], qb[CH];
-        if (ch + 1 < nch) fetch(ch + 1, qa, qb);
+        const int kn = (ch + 1) * RB_FWD_KCH;
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {      // next chunk's weights, in flight during this chunk's MFMAs
+          const int kc = min(kn + u * 4 + g, K - 1);
+          qa[u] = Wa[(size_t)kc * ldw];
+          qb[u] = Wb[(size_t)kc * ldw];
+        }
+        const int abase = ao + r * lda + ch * RB_FWD_KCH + g;
 #pragma unroll
         for (int u = 0; u < CH; ++u) {
-          const int k = (ch * CH + u) * 4 + g;
-          // the last chunk may run past K: never read LDS there (stale bits
-          // could be NaN and NaN * 0 != 0)
-          const float av = k < K ? A[r * lda + k] : 0.f;
+          const float av = rbs[abase + u * 4];
           c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pa[u], c0, 0, 0, 0);
-          if (has1) c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pb[u], c1, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pb[u], c1, 0, 0, 0);
         }
-        if (ch + 1 < nch) {
 #pragma unroll
-          for (int u = 0; u < CH; ++u) { pa[u] = qa[u]; pb[u] = qb[u]; }
-        }
+        for (int u = 0; u < CH; ++u) { pa[u] = qa[u]; pb[u] = qb[u]; }
       }
     } else {
-      constexpr int CH = 4;                         // float4 k-steps (16 k) per chunk
-      const int nsteps = (K + 15) >> 4;
-      const int nch = (nsteps + CH - 1) / CH;
+      constexpr int CH = RB_BWD_KCH / 16;
+      const int nch = (K + RB_BWD_KCH - 1) / RB_BWD_KCH;
+      const int kmax = (K - 1) & ~3;
+      const float* __restrict__ Wa = W + (size_t)na * ldw + 4 * g;
+      const float* __restrict__ Wb = W + (size_t)nb * ldw + 4 * g;
       float4 pa[CH], pb[CH];
-      auto fetch = [&](int ch, float4* xa, float4* xb) {
 #pragma unroll
-        for (int u = 0; u < CH; ++u) {
-          const int k0 = (ch * CH + u) * 16 + 4 * g;
-          const int kc = min(k0, ((K - 1) & ~3));
-          const float4 va = *reinterpret_cast<const float4*>(W + (size_t)nca * ldw + kc);
-          const float4 vb = *reinterpret_cast<const float4*>(W + (size_t)ncb * ldw + kc);
-          const bool ka = k0 < K && oka, kb = k0 < K && okb;
-          xa[u] = ka ? va : make_float4(0.f, 0.f, 0.f, 0.f);
-          xb[u] = kb ? vb : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-      };
-      fetch(0, pa, pb);
+      for (int u = 0; u < CH; ++u) {
+        const int kc = min(u * 16, kmax - 4 * g < 0 ? 0 : kmax - 4 * g);
+        pa[u] = *reinterpret_cast<const float4*>(Wa + kc);
+        pb[u] = *reinterpret_cast<const float4*>(Wb + kc);
+      }
       for (int ch = 0; ch < nch; ++ch) {
         float4 qa[CH], qb[CH];
-        if (ch + 1 < nch) fetch(ch + 1, qa, qb);
+        const int kn = (ch + 1) * RB_BWD_KCH;
 #pragma unroll
         for (int u = 0; u < CH; ++u) {
-          const int k0 = (ch * CH + u) * 16 + 4 * g;
-          const float4 a4 = k0 < K ? *reinterpret_cast<const float4*>(A + r * lda + k0)
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, pa[u].x, c0, 0, 0, 0);
-          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, pa[u].y, c0, 0, 0, 0);
-          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, pa[u].z, c0, 0, 0, 0);
-          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, pa[u].w, c0, 0, 0, 0);
-          if (has1) {
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, pb[u].x, c1, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, pb[u].y, c1, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, pb[u].z, c1, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, pb[u].w, c1, 0, 0, 0);
-          }
+          const int kc = min(kn + u * 16, kmax - 4 * g < 0 ? 0 : kmax - 4 * g);
+          qa[u] = *reinterpret_cast<const float4*>(Wa + kc);
+          qb[u] = *reinterpret_cast<const float4*>(Wb + kc);
         }
-        if (ch + 1 < nch) {
+        const int abase = ao + r * lda + ch * RB_BWD_KCH + 4 * g;
 #pragma unroll
-          for (int u = 0; u < CH; ++u) { pa[u] = qa[u]; pb[u] = qb[u]; }
+        for (int u = 0; u < CH; ++u) {
+          const float4 a4 = *reinterpret_cast<const float4*>(&rbs[abase + u * 16]);
+          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, pa[u].x, c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, pb[u].x, c1, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, pa[u].y, c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, pb[u].y, c1, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, pa[u].z, c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, pb[u].z, c1, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, pa[u].w, c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, pb[u].w, c1, 0, 0, 0);
         }
+#pragma unroll
+        for (int u = 0; u < CH; ++u) { pa[u] = qa[u]; pb[u] = qb[u]; }
       }
     }
     // epilogue: C[row = 4g + i][col = t*16 + r]
@@ -177,7 +178,7 @@ __device__ void rb_dense(const float* A, int lda, const RbStage& S, int row0, in
             const float y = row < nrows ? S.y[(size_t)(row0 + row) * S.ldy + n] : 0.f;
             v = v * (1.f - y * y);
           }
-          if (O) O[row * ldo + n] = v;
+          if (oo >= 0) rbs[oo + row * ldo + n] = v;
           if (S.out_g && row < nrows) S.out_g[(size_t)(row0 + row) * S.ld_out + n] = v;
         }
       }
@@ -185,32 +186,29 @@ __device__ void rb_dense(const float* A, int lda, const RbStage& S, int row0, in
   }
 }
 
-// Copy rows [row0, row0+nrows) x [0, width) of a global matrix into LDS [16][lda],
-// zero-filling padding rows/columns up to `pad_to` columns.
-__device__ __forceinline__ void rb_load(float* A, int lda, const float* G, int ldg, int width, int pad_to,
+// Copy rows [row0, row0+nrows) x [0, width) of a global matrix into the LDS
+// image at offset `ao`, zero-filling padding rows/columns up to `pad_to`.
+__device__ __forceinline__ void rb_load(int ao, int lda, const float* G, int ldg, int width, int pad_to,
                                         int row0, int nrows) {
+#pragma unroll 4
   for (int e = threadIdx.x; e < RB_ROWS * pad_to; e += blockDim.x) {
     const int row = e / pad_to, col = e - row * pad_to;
-    float v = 0.f;
-    if (row < nrows && col < width) v = G[(size_t)(row0 + row) * ldg + col];
-    A[row * lda + col] = v;
+    const bool ok = row < nrows && col < width;
+    const float v = G[(size_t)(row0 + (ok ? row : 0)) * ldg + (ok ? col : 0)];
+    rbs[ao + row * lda + col] = ok ? v : 0.f;
   }
 }
 
-// set the ones column (bias row of W_aug) and zero the padding of an LDS buffer
-__device__ __forceinline__ void rb_pad(float* A, int lda, int width, int pad_to, bool ones) {
+// set the ones column (bias row of W_aug) and zero the padding of an LDS image
+__device__ __forceinline__ void rb_pad(int ao, int lda, int width, int pad_to, bool ones) {
   for (int e = threadIdx.x; e < RB_ROWS * (pad_to - width); e += blockDim.x) {
     const int row = e / (pad_to - width), col = width + e % (pad_to - width);
-    A[row * lda + col] = (ones && col == width) ? 1.f : 0.f;
+    rbs[ao + row * lda + col] = (ones && col == width) ? 1.f : 0.f;
   }
 }
-
-__device__ __forceinline__ int rb_k_pad(int K, bool bt) { return bt ? ((K + 15) & ~15) : ((K + 3) & ~3); }
 
 // ------------------------------------------------------------------ forward
 __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
-  extern __shared__ __attribute__((aligned(16))) float rbs[];
-  // job lookup
   int jb = 0;
   while (jb + 1 < L.njobs && (int)blockIdx.x >= L.block_start[jb + 1]) ++jb;
   const RbFwdJob& J = L.job[jb];
@@ -218,14 +216,14 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
   const int row0 = blk * J.rpb;
   const int nrows = min(J.rpb, J.rows - row0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float* buf[3] = {rbs, rbs + RB_ROWS * L.ld_lds, rbs + 2 * RB_ROWS * L.ld_lds};
-  float* rowq = rbs + 3 * RB_ROWS * L.ld_lds;         // [16] log q of the sampled input
-  float* rowp = rowq + RB_ROWS;                        // [16] log N(input; 0, 1)
   const int lda = L.ld_lds;
+  const int bo[3] = {0, RB_ROWS * lda, 2 * RB_ROWS * lda};   // LDS images (offsets into rbs)
+  const int oq = 3 * RB_ROWS * lda;                           // [16] log q of the sampled input
+  const int op = oq + RB_ROWS;                                // [16] log N(input; 0, 1)
   uint64_t base = 0;
   if (L.rng_base) base = *L.rng_base;
 
-  // ---- input rows
+  // ---- input rows into image 0
   const int K0 = J.st[0].K;                 // fin + 1 (ones column)
   const int K0p = rb_k_pad(K0, false);
   if (J.pr_slabs) {
@@ -236,14 +234,21 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
       float v = 0.f;
       if (rr < nrows && c < H) {
         const float* sp = J.pr_slabs + (size_t)(row0 + rr) * J.pr_ld + c;
-        float acc = 0.f;
-        for (int q = 0; q < J.pr_nslab; ++q) acc += sp[(size_t)q * J.pr_stride];
-        v = tanhf(acc);
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        int q = 0;
+        for (; q + 4 <= J.pr_nslab; q += 4) {
+          a0 += sp[(size_t)q * J.pr_stride];
+          a1 += sp[(size_t)(q + 1) * J.pr_stride];
+          a2 += sp[(size_t)(q + 2) * J.pr_stride];
+          a3 += sp[(size_t)(q + 3) * J.pr_stride];
+        }
+        for (; q < J.pr_nslab; ++q) a0 += sp[(size_t)q * J.pr_stride];
+        v = tanhf((a0 + a1) + (a2 + a3));
         J.pr_y[(size_t)(row0 + rr) * J.pr_ldy + c] = v;
       } else if (c == H) {
         v = 1.f;
       }
-      buf[0][rr * lda + c] = v;
+      rbs[bo[0] + rr * lda + c] = v;
     }
   } else if (J.pro_sample) {
     // h = eps * scale + mu from the previous layer's P (Normal.sample, F:59/F:68)
@@ -269,14 +274,14 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
         } else if (j == d) {
           hv = 1.f;                          // ones column (bias row of W_aug)
         }
-        if (j < K0p) buf[0][rr * lda + j] = hv;
+        if (j < K0p) rbs[bo[0] + rr * lda + j] = hv;
       }
       accq = rb_wave_sum(accq);
       accp = rb_wave_sum(accp);
-      if (lane == 0) { rowq[rr] = accq; rowp[rr] = accp; }
+      if (lane == 0) { rbs[oq + rr] = accq; rbs[op + rr] = accp; }
     }
   } else {
-    rb_load(buf[0], lda, J.in, J.ld_in, K0, K0p, row0, nrows);
+    rb_load(bo[0], lda, J.in, J.ld_in, K0, K0p, row0, nrows);
     if (J.pro_stdnormal) {
       // log N(h; 0, 1) summed over the latent dims (F:135-F:136)
       for (int rr = wave; rr < RB_ROWS; rr += RB_WAVES) {
@@ -287,25 +292,22 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
             acc += __fsub_rn(-0.5f * (hv * hv), kHalfLog2Pi);
           }
         acc = rb_wave_sum(acc);
-        if (lane == 0) rowp[rr] = acc;
+        if (lane == 0) rbs[op + rr] = acc;
       }
     }
   }
   __syncthreads();
 
-  // ---- chained Dense layers; stage s reads buf[s % 3] and writes buf[(s+1) % 3]
+  // ---- chained Dense layers; stage s reads image s % 3 and writes image (s+1) % 3
   for (int s = 0; s < J.nst; ++s) {
     const RbStage& S = J.st[s];
-    float* out = buf[(s + 1) % 3];
-    if (s + 1 < J.nst) {
-      const int Kn = J.st[s + 1].K;        // next K = N + 1 (ones column)
-      rb_pad(out, lda, S.N, rb_k_pad(Kn, false), true);
-    }
+    const int out = bo[(s + 1) % 3];
+    if (s + 1 < J.nst) rb_pad(out, lda, S.N, rb_k_pad(J.st[s + 1].K, false), true);
     __syncthreads();
-    rb_dense<false>(buf[s % 3], lda, S, row0, nrows, out, lda);
+    rb_dense<false>(bo[s % 3], lda, S, row0, nrows, out, lda);
     __syncthreads();
   }
-  const float* P = buf[J.nst % 3];
+  const int P = bo[J.nst % 3];
 
   // ---- epilogue
   if (J.epi == 1) {
@@ -316,7 +318,7 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
       const int rg = row0 + rr;
       float acc = 0.f;
       for (int j = lane; j < d; j += 64) {
-        const float mu = P[rr * lda + j], zs = P[rr * lda + d + j];
+        const float mu = rbs[P + rr * lda + j], zs = rbs[P + rr * lda + d + j];
         const float sc = __fadd_rn(expf(zs), kScaleEps);
         const float e = rb_eps(J.ep_noise, d, rg, j, base);
         const float hv = __fadd_rn(__fmul_rn(e, sc), mu);
@@ -327,7 +329,7 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
       }
       acc = rb_wave_sum(acc);
       if (lane == 0) {
-        const float prev = J.pro_sample ? rowq[rr] : (J.logq_acc ? J.logq[rg] : 0.f);
+        const float prev = J.pro_sample ? rbs[oq + rr] : (J.logq_acc ? J.logq[rg] : 0.f);
         J.logq[rg] = prev + acc;
       }
     }
@@ -339,7 +341,7 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
       const int rg = row0 + rr;
       float acc = 0.f;
       for (int j = lane; j < d; j += 64) {
-        const float mu = P[rr * lda + j], zs = P[rr * lda + d + j];
+        const float mu = rbs[P + rr * lda + j], zs = rbs[P + rr * lda + d + j];
         const float sc = __fadd_rn(expf(zs), kScaleEps);
         const float hv = J.ep_tgt[(size_t)rg * J.ep_ldtgt + j];
         const float z = __fsub_rn(hv / sc, mu / sc);
@@ -347,21 +349,20 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
       }
       acc = rb_wave_sum(acc);
       if (lane == 0) {
-        const float prev = J.pro_stdnormal ? rowp[rr] : (J.logp_acc ? J.logp[rg] : 0.f);
+        const float prev = J.pro_stdnormal ? rbs[op + rr] : (J.logp_acc ? J.logp[rg] : 0.f);
         J.logp[rg] = prev + acc;
       }
     }
   }
-  if (threadIdx.x < nrows) {
+  if ((int)threadIdx.x < nrows) {
     const int rg = row0 + threadIdx.x;
-    if (J.epi != 1 && J.pro_sample && J.logq) J.logq[rg] = rowq[threadIdx.x];
-    if (J.epi != 2 && J.pro_stdnormal && J.logp) J.logp[rg] = rowp[threadIdx.x];
+    if (J.epi != 1 && J.pro_sample && J.logq) J.logq[rg] = rbs[oq + threadIdx.x];
+    if (J.epi != 2 && J.pro_stdnormal && J.logp) J.logp[rg] = rbs[op + threadIdx.x];
   }
 }
 
 // ----------------------------------------------------------------- backward
 __global__ __launch_bounds__(RB_WAVES * 64) void rb_bwd_kernel(RbBwdLaunch L) {
-  extern __shared__ __attribute__((aligned(16))) float rbs[];
   int jb = 0;
   while (jb + 1 < L.njobs && (int)blockIdx.x >= L.block_start[jb + 1]) ++jb;
   const RbBwdJob& J = L.job[jb];
@@ -369,31 +370,39 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_bwd_kernel(RbBwdLaunch L) {
   const int row0 = blk * J.rpb;
   const int nrows = min(J.rpb, J.rows - row0);
   const int lda = L.ld_lds;
-  float* buf[3] = {rbs, rbs + RB_ROWS * lda, rbs + 2 * RB_ROWS * lda};
-  float* red = rbs + 3 * RB_ROWS * lda;     // [4][2][128] partial sums (pro 3)
+  const int bo[3] = {0, RB_ROWS * lda, 2 * RB_ROWS * lda};
+  const int ored = 3 * RB_ROWS * lda;     // [4][2][128] partial sums (pro 3)
 
   const int K0 = J.nst > 0 ? J.st[0].K : 0;   // = width of dP / dZ
   const int K0p = rb_k_pad(K0, true);
-  float* D = buf[0];
+  const int D = bo[0];
   if (J.pro == 0) {
     rb_load(D, lda, J.dz_in, J.ld_dz_in, K0, K0p, row0, nrows);
   } else if (J.pro == 1 || J.pro == 2) {
     // per row: dP of an encoder sampling layer (pro 1) or a decoder prior head (pro 2)
     const int d = J.d;
+#pragma unroll 2
     for (int e = threadIdx.x; e < RB_ROWS * K0p; e += blockDim.x) {
       const int rr = e / K0p, c = e - rr * K0p;
       if (c >= d || rr >= nrows) {
-        if (c >= 2 * d || rr >= nrows) D[rr * lda + c] = 0.f;
+        if (c >= 2 * d || rr >= nrows) rbs[D + rr * lda + c] = 0.f;
         continue;
       }
       const int rg = row0 + rr;
       const float mu = J.P[(size_t)rg * J.ldP + c];
       const float zs = J.P[(size_t)rg * J.ldP + d + c];
+      const float hv = J.H[(size_t)rg * J.ldH + c];
+      const float dl = J.dlw[rg];
+      float G = 0.f, ev = 0.f;
+      if (J.pro == 1) {
+        ev = J.eps[(size_t)rg * J.ld_eps + c];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (q < J.nsrc) G += J.src[q][(size_t)rg * J.ldsrc[q] + c];
+      }
       const float ez = expf(zs);
       const float sc = __fadd_rn(ez, kScaleEps);
-      const float hv = J.H[(size_t)rg * J.ldH + c];
       const float z = __fsub_rn(hv / sc, mu / sc);
-      const float dl = J.dlw[rg];
       float dmu, dsc;
       if (J.pro == 2) {
         // log p(h_t | .): dL/dlogp = dlw; the target h gets -z/s (kept for the encoder pass)
@@ -401,12 +410,7 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_bwd_kernel(RbBwdLaunch L) {
         dmu = dl * (z / sc);
         dsc = dl * ((z * z - 1.f) / sc);
       } else {
-        const float ev = J.eps[(size_t)rg * J.ld_eps + c];
         const float dlq = -dl;
-        float G = 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (q < J.nsrc) G += J.src[q][(size_t)rg * J.ldsrc[q] + c];
         if (J.std_normal) G += dl * (-hv);
         G += dlq * (-z / sc);
         dmu = G + dlq * (z / sc);
@@ -417,8 +421,8 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_bwd_kernel(RbBwdLaunch L) {
         }
       }
       const float dzs = dsc * ez;
-      D[rr * lda + c] = dmu;
-      D[rr * lda + d + c] = dzs;
+      rbs[D + rr * lda + c] = dmu;
+      rbs[D + rr * lda + d + c] = dzs;
       J.dP_out[(size_t)rg * J.ld_dP + c] = dmu;
       J.dP_out[(size_t)rg * J.ld_dP + d + c] = dzs;
     }
@@ -428,7 +432,7 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_bwd_kernel(RbBwdLaunch L) {
     const int d = J.d, kS = J.kS;
     for (int e = threadIdx.x; e < RB_ROWS * K0p; e += blockDim.x) {
       const int rr = e / K0p, c = e - rr * K0p;
-      if (c >= 2 * d || rr >= nrows) D[rr * lda + c] = 0.f;
+      if (c >= 2 * d || rr >= nrows) rbs[D + rr * lda + c] = 0.f;
     }
     const int grp = threadIdx.x >> 7, tj = threadIdx.x & 127;   // 4 sample groups x 128 columns
     for (int rr = 0; rr < nrows; ++rr) {
@@ -447,30 +451,32 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_bwd_kernel(RbBwdLaunch L) {
             const float hv = J.H[(size_t)rg * J.ldH + c];
             const float ev = J.eps[(size_t)rg * J.ld_eps + c];
             const float dl = J.dlw[rg], dlq = -dl;
-            const float z = __fsub_rn(hv / sc, mu / sc);
             float G = 0.f;
 #pragma unroll
             for (int q = 0; q < 4; ++q)
               if (q < J.nsrc) G += J.src[q][(size_t)rg * J.ldsrc[q] + c];
+            const float z = __fsub_rn(hv / sc, mu / sc);
             if (J.std_normal) G += dl * (-hv);
             G += dlq * (-z / sc);
             amu += G + dlq * (z / sc);
             asc += G * ev + dlq * ((z * z - 1.f) / sc);
           }
         }
-        red[(grp * 2 + 0) * 128 + tj] = amu;
-        red[(grp * 2 + 1) * 128 + tj] = asc;
+        rbs[ored + (grp * 2 + 0) * 128 + tj] = amu;
+        rbs[ored + (grp * 2 + 1) * 128 + tj] = asc;
         __syncthreads();
         if (grp == 0 && c < d) {
-          amu = red[0 * 128 + tj] + red[2 * 128 + tj] + red[4 * 128 + tj] + red[6 * 128 + tj];
-          asc = red[1 * 128 + tj] + red[3 * 128 + tj] + red[5 * 128 + tj] + red[7 * 128 + tj];
+          amu = rbs[ored + 0 * 128 + tj] + rbs[ored + 2 * 128 + tj] + rbs[ored + 4 * 128 + tj] +
+                rbs[ored + 6 * 128 + tj];
+          asc = rbs[ored + 1 * 128 + tj] + rbs[ored + 3 * 128 + tj] + rbs[ored + 5 * 128 + tj] +
+                rbs[ored + 7 * 128 + tj];
           if (J.kl_coef != 0.f) {
             amu += J.kl_coef * mu / (float)J.kl_rows;
             asc += J.kl_coef * (sc - 1.f / sc) / (float)J.kl_rows;
           }
           const float dzs = asc * ez;
-          D[rr * lda + c] = amu;
-          D[rr * lda + d + c] = dzs;
+          rbs[D + rr * lda + c] = amu;
+          rbs[D + rr * lda + d + c] = dzs;
           J.dP_out[(size_t)img * J.ld_dP + c] = amu;
           J.dP_out[(size_t)img * J.ld_dP + d + c] = dzs;
         }
@@ -483,11 +489,11 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_bwd_kernel(RbBwdLaunch L) {
   // ---- chain of transposed Dense layers (dX = dZ W^T, tanh-grad on the way)
   for (int s = 0; s < J.nst; ++s) {
     const RbStage& S = J.st[s];
-    float* out = buf[(s + 1) % 3];
+    const int out = bo[(s + 1) % 3];
     const bool last = s + 1 == J.nst;
     if (!last) rb_pad(out, lda, S.N, rb_k_pad(J.st[s + 1].K, true), false);
     __syncthreads();
-    rb_dense<true>(buf[s % 3], lda, S, row0, nrows, last ? nullptr : out, lda);
+    rb_dense<true>(bo[s % 3], lda, S, row0, nrows, last ? -1 : out, lda);
     __syncthreads();
   }
 }
