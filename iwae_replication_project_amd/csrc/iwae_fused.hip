@@ -23,6 +23,8 @@
 // to f32 summation order.
 #include "iwae_kernels.h"
 
+#include <vector>
+
 namespace iwae {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -64,11 +66,117 @@ __device__ __forceinline__ float rb_eps(const RbNoise& nz, int d, int r, int j, 
 
 extern __shared__ __attribute__((aligned(16))) float rbs[];
 
-// chunk widths of the k loops (the LDS operand is zero-padded up to them)
-constexpr int RB_FWD_KCH = 32;   // 8 MFMA k-steps of 4
-constexpr int RB_BWD_KCH = 64;   // 4 float4 k-steps of 16
-__device__ __forceinline__ int rb_k_pad(int K, bool bt) {
-  return bt ? ((K + RB_BWD_KCH - 1) / RB_BWD_KCH) * RB_BWD_KCH : ((K + RB_FWD_KCH - 1) / RB_FWD_KCH) * RB_FWD_KCH;
+#ifdef IWAE_RB_TRACE
+// Debug build only (-DIWAE_RB_TRACE): 100 MHz timestamps of workgroup 0 of
+// every job at the phase boundaries of the fused kernels.
+__device__ unsigned long long g_rb_trace[16384];
+__device__ unsigned g_rb_trace_n;
+#define RB_TRACE_OPEN(kind)                                                    \
+  int tr_ = -1;                                                                \
+  if (threadIdx.x == 0 && blk == 0) {                                          \
+    const unsigned long long t_ = wall_clock64();                              \
+    tr_ = (int)atomicAdd(&g_rb_trace_n, 32u);                                  \
+    if (tr_ + 32 > 16384) tr_ = -1;                                            \
+    else { g_rb_trace[tr_] = (kind) * 256 + jb; g_rb_trace[tr_ + 1] = t_; }    \
+  }
+#define RB_TRACE(slot) \
+  if (tr_ >= 0) g_rb_trace[tr_ + (slot)] = wall_clock64();
+#define RB_TR_PARAM , int tr_
+#define RB_TR_ARG(x) , (x)
+#else
+#define RB_TR_PARAM
+#define RB_TR_ARG(x)
+#define RB_TRACE_OPEN(kind)
+#define RB_TRACE(slot)
+#endif
+
+// Buffer descriptor over a weight matrix (wave-uniform inputs made provable
+// with readfirstlane, so no waterfall loops).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rb_rsrc(const float* p, unsigned bytes) {
+  const uint64_t a = (uint64_t)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const uint64_t u = ((uint64_t)hi << 32) | lo;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)u, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes),
+                                           0x00020000);
+}
+
+// One pair of 16x16 output tiles over k in [0, 4*NS) (fwd) or [0, 16*NS)
+// (bwd).  Every weight this wave needs is requested before the first MFMA --
+// buffer loads with a per-lane 32-bit offset and a uniform (SGPR) step, so
+// the requests cost no address registers and all of them are in flight at
+// once (one memory round trip per stage); sched_barrier keeps the compiler
+// from re-interleaving them with the MFMAs.
+template <bool BT, int NS>
+__device__ __forceinline__ void rb_tile_pair(int ao, int lda, const RbStage& S, int t0, int t1, bool has1,
+                                             f32x4& c0, f32x4& c1, const int kofs RB_TR_PARAM) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  const int N = S.N, ldw = S.ldw;
+  const int na = min(t0 * 16 + r, N - 1), nb = has1 ? min(t1 * 16 + r, N - 1) : na;
+  if (!BT) {
+    // rows k >= K read the following parameters or the zero tail of the
+    // allocation (finite) against zeros in A.  (The range check does not see
+    // the SGPR step, so it cannot be what guards these reads.)
+    const __amdgpu_buffer_rsrc_t rs = rb_rsrc(S.W, S.W_bytes);
+    const int va = ((kofs + g) * ldw + na) * 4, vb = ((kofs + g) * ldw + nb) * 4;
+    const int step = 16 * ldw;                         // 4 rows of W, bytes
+    float pa[NS], pb[NS];
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      pa[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, va, u * step, 0));
+      pb[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vb, u * step, 0));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    RB_TRACE(1)
+    const int abase = ao + r * lda + kofs + g;
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const float av = rbs[abase + u * 4];
+      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pa[u], c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pb[u], c1, 0, 0, 0);
+    }
+#ifdef IWAE_RB_TRACE
+    if (tr_ >= 0) {
+      asm volatile("" ::"v"(c0[0] + c1[0]) : "memory");
+      g_rb_trace[tr_ + 2] = wall_clock64();
+    }
+#endif
+  } else {
+    // permuted k order: lane (r, g) holds k = 16u + 4g .. +3 of output column n;
+    // k >= K reads the next row's weights (finite) against zeros in A
+    const __amdgpu_buffer_rsrc_t rs = rb_rsrc(S.W, S.W_bytes);
+    const int va = (na * ldw + kofs + 4 * g) * 4, vb = (nb * ldw + kofs + 4 * g) * 4;
+    float4 pa[NS], pb[NS];
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, va, u * 64, 0);
+      const auto y = __builtin_amdgcn_raw_buffer_load_b128(rs, vb, u * 64, 0);
+      pa[u] = make_float4(__uint_as_float(x[0]), __uint_as_float(x[1]), __uint_as_float(x[2]), __uint_as_float(x[3]));
+      pb[u] = make_float4(__uint_as_float(y[0]), __uint_as_float(y[1]), __uint_as_float(y[2]), __uint_as_float(y[3]));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    RB_TRACE(1)
+    const int abase = ao + r * lda + kofs + 4 * g;
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const float4 a4 = *reinterpret_cast<const float4*>(&rbs[abase + u * 16]);
+      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, pa[u].x, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, pb[u].x, c1, 0, 0, 0);
+      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, pa[u].y, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, pb[u].y, c1, 0, 0, 0);
+      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, pa[u].z, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, pb[u].z, c1, 0, 0, 0);
+      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, pa[u].w, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, pb[u].w, c1, 0, 0, 0);
+    }
+#ifdef IWAE_RB_TRACE
+    if (tr_ >= 0) {
+      asm volatile("" ::"v"(c0[0] + c1[0]) : "memory");
+      g_rb_trace[tr_ + 2] = wall_clock64();
+    }
+#endif
+  }
 }
 
 // OUT[16][N] = act(A[16][K] . B).  A is the LDS image at offset `ao` (row
@@ -79,87 +187,46 @@ __device__ __forceinline__ int rb_k_pad(int K, bool bt) {
 // Weight addresses are clamped into the matrix instead of masked, so every
 // load is unconditional (no exec-masked branch, no per-load wait): values
 // fetched for k >= K meet zeros in A, columns n >= N are never stored.
+// K <= 256 (kRbMaxWidth-limited layers beyond that are not routed here).
 template <bool BT>
-__device__ void rb_dense(int ao, int lda, const RbStage& S, int row0, int nrows, int oo, int ldo) {
+__device__ void rb_dense(int ao, int lda, const RbStage& S, int row0, int nrows, int oo, int ldo RB_TR_PARAM) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int K = S.K, N = S.N, ldw = S.ldw;
-  const float* __restrict__ W = S.W;
+  const int K = S.K, N = S.N;
   const int ntile = (N + 15) >> 4;
   for (int t0 = wave; t0 < ntile; t0 += 2 * RB_WAVES) {
     const int t1 = t0 + RB_WAVES;
     const bool has1 = t1 < ntile;
-    const int na = min(t0 * 16 + r, N - 1), nb = has1 ? min(t1 * 16 + r, N - 1) : na;
     f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#ifdef IWAE_RB_TRACE
+    if (t0 != wave) tr_ = -1;
+    RB_TRACE(0)
+#endif
+    // tanh-grad epilogue operand, requested before the k loop
+    float yv[2][4];
+    if (BT && S.act == 2) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = min((q == 0 ? t0 : t1) * 16 + r, N - 1), row = min(4 * g + i, nrows - 1);
+          yv[q][i] = S.y[(size_t)(row0 + row) * S.ldy + n];
+        }
+    }
+    // whole K in one round trip up to K = 256; wider layers in 64-k rounds
     if (!BT) {
-      constexpr int CH = RB_FWD_KCH / 4;
-      const int nch = (K + RB_FWD_KCH - 1) / RB_FWD_KCH;
-      const float* __restrict__ Wa = W + na;
-      const float* __restrict__ Wb = W + nb;
-      float pa[CH], pb[CH];
-#pragma unroll
-      for (int u = 0; u < CH; ++u) {
-        const int kc = min(u * 4 + g, K - 1);
-        pa[u] = Wa[(size_t)kc * ldw];
-        pb[u] = Wb[(size_t)kc * ldw];
-      }
-      for (int ch = 0; ch < nch; ++ch) {
-        float qa[CH], qb[CH];
-        const int kn = (ch + 1) * RB_FWD_KCH;
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {      // next chunk's weights, in flight during this chunk's MFMAs
-          const int kc = min(kn + u * 4 + g, K - 1);
-          qa[u] = Wa[(size_t)kc * ldw];
-          qb[u] = Wb[(size_t)kc * ldw];
-        }
-        const int abase = ao + r * lda + ch * RB_FWD_KCH + g;
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-          const float av = rbs[abase + u * 4];
-          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pa[u], c0, 0, 0, 0);
-          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pb[u], c1, 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < CH; ++u) { pa[u] = qa[u]; pb[u] = qb[u]; }
-      }
+      if (K <= 32) rb_tile_pair<false, 8>(ao, lda, S, t0, t1, has1, c0, c1, 0 RB_TR_ARG(tr_));
+      else if (K <= 64) rb_tile_pair<false, 16>(ao, lda, S, t0, t1, has1, c0, c1, 0 RB_TR_ARG(tr_));
+      else if (K <= 128) rb_tile_pair<false, 32>(ao, lda, S, t0, t1, has1, c0, c1, 0 RB_TR_ARG(tr_));
+      else if (K <= 256) rb_tile_pair<false, 64>(ao, lda, S, t0, t1, has1, c0, c1, 0 RB_TR_ARG(tr_));
+      else
+        for (int k0 = 0; k0 < K; k0 += 64) rb_tile_pair<false, 16>(ao, lda, S, t0, t1, has1, c0, c1, k0 RB_TR_ARG(tr_));
     } else {
-      constexpr int CH = RB_BWD_KCH / 16;
-      const int nch = (K + RB_BWD_KCH - 1) / RB_BWD_KCH;
-      const int kmax = (K - 1) & ~3;
-      const float* __restrict__ Wa = W + (size_t)na * ldw + 4 * g;
-      const float* __restrict__ Wb = W + (size_t)nb * ldw + 4 * g;
-      float4 pa[CH], pb[CH];
-#pragma unroll
-      for (int u = 0; u < CH; ++u) {
-        const int kc = min(u * 16, kmax - 4 * g < 0 ? 0 : kmax - 4 * g);
-        pa[u] = *reinterpret_cast<const float4*>(Wa + kc);
-        pb[u] = *reinterpret_cast<const float4*>(Wb + kc);
-      }
-      for (int ch = 0; ch < nch; ++ch) {
-        float4 qa[CH], qb[CH];
-        const int kn = (ch + 1) * RB_BWD_KCH;
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-          const int kc = min(kn + u * 16, kmax - 4 * g < 0 ? 0 : kmax - 4 * g);
-          qa[u] = *reinterpret_cast<const float4*>(Wa + kc);
-          qb[u] = *reinterpret_cast<const float4*>(Wb + kc);
-        }
-        const int abase = ao + r * lda + ch * RB_BWD_KCH + 4 * g;
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-          const float4 a4 = *reinterpret_cast<const float4*>(&rbs[abase + u * 16]);
-          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, pa[u].x, c0, 0, 0, 0);
-          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, pb[u].x, c1, 0, 0, 0);
-          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, pa[u].y, c0, 0, 0, 0);
-          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, pb[u].y, c1, 0, 0, 0);
-          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, pa[u].z, c0, 0, 0, 0);
-          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, pb[u].z, c1, 0, 0, 0);
-          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, pa[u].w, c0, 0, 0, 0);
-          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, pb[u].w, c1, 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < CH; ++u) { pa[u] = qa[u]; pb[u] = qb[u]; }
-      }
+      if (K <= 64) rb_tile_pair<true, 4>(ao, lda, S, t0, t1, has1, c0, c1, 0 RB_TR_ARG(tr_));
+      else if (K <= 128) rb_tile_pair<true, 8>(ao, lda, S, t0, t1, has1, c0, c1, 0 RB_TR_ARG(tr_));
+      else if (K <= 256) rb_tile_pair<true, 16>(ao, lda, S, t0, t1, has1, c0, c1, 0 RB_TR_ARG(tr_));
+      else
+        for (int k0 = 0; k0 < K; k0 += 64) rb_tile_pair<true, 4>(ao, lda, S, t0, t1, has1, c0, c1, k0 RB_TR_ARG(tr_));
     }
     // epilogue: C[row = 4g + i][col = t*16 + r]
 #pragma unroll
@@ -174,8 +241,8 @@ __device__ void rb_dense(int ao, int lda, const RbStage& S, int row0, int nrows,
           float v = c[i];
           if (S.act == 1) {
             v = tanhf(v);
-          } else if (S.act == 2) {
-            const float y = row < nrows ? S.y[(size_t)(row0 + row) * S.ldy + n] : 0.f;
+          } else if (BT && S.act == 2) {
+            const float y = yv[q][i];
             v = v * (1.f - y * y);
           }
           if (oo >= 0) rbs[oo + row * ldo + n] = v;
@@ -183,6 +250,7 @@ __device__ void rb_dense(int ao, int lda, const RbStage& S, int row0, int nrows,
         }
       }
     }
+    RB_TRACE(3)
   }
 }
 
@@ -220,6 +288,7 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
   const int bo[3] = {0, RB_ROWS * lda, 2 * RB_ROWS * lda};   // LDS images (offsets into rbs)
   const int oq = 3 * RB_ROWS * lda;                           // [16] log q of the sampled input
   const int op = oq + RB_ROWS;                                // [16] log N(input; 0, 1)
+  RB_TRACE_OPEN(1)
   uint64_t base = 0;
   if (L.rng_base) base = *L.rng_base;
 
@@ -251,52 +320,100 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
       rbs[bo[0] + rr * lda + c] = v;
     }
   } else if (J.pro_sample) {
-    // h = eps * scale + mu from the previous layer's P (Normal.sample, F:59/F:68)
+    // h = eps * scale + mu from the previous layer's P (Normal.sample, F:59/F:68).
+    // Each wave owns rows wave and wave+8; their (mu, zs[, eps]) are requested
+    // before any is used (one round trip), then Philox / log-density run.
     const int d = J.ps_d;
-    for (int rr = wave; rr < RB_ROWS; rr += RB_WAVES) {
-      float accq = 0.f, accp = 0.f;
-      for (int j0 = 0; j0 < K0p; j0 += 64) {
-        const int j = j0 + lane;
-        float hv = 0.f;
-        if (rr < nrows && j < d) {
-          const int rg = row0 + rr;
+    constexpr int RPW = RB_ROWS / RB_WAVES;          // rows per wave
+    const int npass = (K0p + 63) >> 6;
+    if (npass <= 2) {
+      float mu[RPW][2], zs[RPW][2];
+#pragma unroll
+      for (int q = 0; q < RPW; ++q)
+#pragma unroll
+        for (int pj = 0; pj < 2; ++pj) {
+          const int rr = wave + q * RB_WAVES, j = pj * 64 + lane;
+          const int rg = row0 + min(rr, nrows - 1);
+          const int jc = min(j, d - 1);
           const int pr = rg / J.ps_div;
-          const float mu = J.ps_P[(size_t)pr * J.ps_ldP + j];
-          const float zs = J.ps_P[(size_t)pr * J.ps_ldP + d + j];
-          const float sc = __fadd_rn(expf(zs), kScaleEps);
-          const float e = rb_eps(J.ps_noise, d, rg, j, base);
-          hv = __fadd_rn(__fmul_rn(e, sc), mu);
-          J.ps_h[(size_t)rg * J.ps_ldh + j] = hv;
-          if (J.ps_eps) J.ps_eps[(size_t)rg * J.ps_ldeps + j] = e;
-          const float z = __fsub_rn(hv / sc, mu / sc);
-          accq += __fsub_rn(-0.5f * (z * z), __fadd_rn(kHalfLog2Pi, logf(sc)));
-          accp += __fsub_rn(-0.5f * (hv * hv), kHalfLog2Pi);
-        } else if (j == d) {
-          hv = 1.f;                          // ones column (bias row of W_aug)
+          mu[q][pj] = J.ps_P[(size_t)pr * J.ps_ldP + jc];
+          zs[q][pj] = J.ps_P[(size_t)pr * J.ps_ldP + d + jc];
         }
-        if (j < K0p) rbs[bo[0] + rr * lda + j] = hv;
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const int rr = wave + q * RB_WAVES;
+        float accq = 0.f, accp = 0.f;
+#pragma unroll
+        for (int pj = 0; pj < 2; ++pj) {
+          const int j = pj * 64 + lane;
+          if (pj >= npass) break;
+          float hv = 0.f;
+          if (rr < nrows && j < d) {
+            const int rg = row0 + rr;
+            const float sc = __fadd_rn(expf(zs[q][pj]), kScaleEps);
+            const float e = rb_eps(J.ps_noise, d, rg, j, base);
+            hv = __fadd_rn(__fmul_rn(e, sc), mu[q][pj]);
+            J.ps_h[(size_t)rg * J.ps_ldh + j] = hv;
+            if (J.ps_eps) J.ps_eps[(size_t)rg * J.ps_ldeps + j] = e;
+            const float z = __fsub_rn(hv / sc, mu[q][pj] / sc);
+            accq += __fsub_rn(-0.5f * (z * z), __fadd_rn(kHalfLog2Pi, logf(sc)));
+            accp += __fsub_rn(-0.5f * (hv * hv), kHalfLog2Pi);
+          } else if (j == d) {
+            hv = 1.f;                        // ones column (bias row of W_aug)
+          }
+          if (j < K0p) rbs[bo[0] + rr * lda + j] = hv;
+        }
+        accq = rb_wave_sum(accq);
+        accp = rb_wave_sum(accp);
+        if (lane == 0) { rbs[oq + rr] = accq; rbs[op + rr] = accp; }
       }
-      accq = rb_wave_sum(accq);
-      accp = rb_wave_sum(accp);
-      if (lane == 0) { rbs[oq + rr] = accq; rbs[op + rr] = accp; }
+    } else {
+      for (int rr = wave; rr < RB_ROWS; rr += RB_WAVES) {
+        float accq = 0.f, accp = 0.f;
+        for (int j0 = 0; j0 < K0p; j0 += 64) {
+          const int j = j0 + lane;
+          float hv = 0.f;
+          if (rr < nrows && j < d) {
+            const int rg = row0 + rr;
+            const int pr = rg / J.ps_div;
+            const float m = J.ps_P[(size_t)pr * J.ps_ldP + j];
+            const float z0 = J.ps_P[(size_t)pr * J.ps_ldP + d + j];
+            const float sc = __fadd_rn(expf(z0), kScaleEps);
+            const float e = rb_eps(J.ps_noise, d, rg, j, base);
+            hv = __fadd_rn(__fmul_rn(e, sc), m);
+            J.ps_h[(size_t)rg * J.ps_ldh + j] = hv;
+            if (J.ps_eps) J.ps_eps[(size_t)rg * J.ps_ldeps + j] = e;
+            const float z = __fsub_rn(hv / sc, m / sc);
+            accq += __fsub_rn(-0.5f * (z * z), __fadd_rn(kHalfLog2Pi, logf(sc)));
+            accp += __fsub_rn(-0.5f * (hv * hv), kHalfLog2Pi);
+          } else if (j == d) {
+            hv = 1.f;
+          }
+          if (j < K0p) rbs[bo[0] + rr * lda + j] = hv;
+        }
+        accq = rb_wave_sum(accq);
+        accp = rb_wave_sum(accp);
+        if (lane == 0) { rbs[oq + rr] = accq; rbs[op + rr] = accp; }
+      }
     }
   } else {
     rb_load(bo[0], lda, J.in, J.ld_in, K0, K0p, row0, nrows);
-    if (J.pro_stdnormal) {
-      // log N(h; 0, 1) summed over the latent dims (F:135-F:136)
-      for (int rr = wave; rr < RB_ROWS; rr += RB_WAVES) {
-        float acc = 0.f;
-        if (rr < nrows)
-          for (int j = lane; j < K0 - 1; j += 64) {
-            const float hv = J.in[(size_t)(row0 + rr) * J.ld_in + j];
-            acc += __fsub_rn(-0.5f * (hv * hv), kHalfLog2Pi);
-          }
-        acc = rb_wave_sum(acc);
-        if (lane == 0) rbs[op + rr] = acc;
-      }
-    }
   }
   __syncthreads();
+  if (!J.pro_sample && J.pro_stdnormal) {
+    // log N(h; 0, 1) summed over the latent dims (F:135-F:136), from the LDS copy
+    for (int rr = wave; rr < RB_ROWS; rr += RB_WAVES) {
+      float acc = 0.f;
+      if (rr < nrows)
+        for (int j = lane; j < K0 - 1; j += 64) {
+          const float hv = rbs[bo[0] + rr * lda + j];
+          acc += __fsub_rn(-0.5f * (hv * hv), kHalfLog2Pi);
+        }
+      acc = rb_wave_sum(acc);
+      if (lane == 0) rbs[op + rr] = acc;
+    }
+  }
+  RB_TRACE(2)
 
   // ---- chained Dense layers; stage s reads image s % 3 and writes image (s+1) % 3
   for (int s = 0; s < J.nst; ++s) {
@@ -304,8 +421,9 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
     const int out = bo[(s + 1) % 3];
     if (s + 1 < J.nst) rb_pad(out, lda, S.N, rb_k_pad(J.st[s + 1].K, false), true);
     __syncthreads();
-    rb_dense<false>(bo[s % 3], lda, S, row0, nrows, out, lda);
+    rb_dense<false>(bo[s % 3], lda, S, row0, nrows, out, lda RB_TR_ARG(tr_ >= 0 ? tr_ + 8 + 4 * s : -1));
     __syncthreads();
+    RB_TRACE(3 + s)
   }
   const int P = bo[J.nst % 3];
 
@@ -359,6 +477,7 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
     if (J.epi != 1 && J.pro_sample && J.logq) J.logq[rg] = rbs[oq + threadIdx.x];
     if (J.epi != 2 && J.pro_stdnormal && J.logp) J.logp[rg] = rbs[op + threadIdx.x];
   }
+  RB_TRACE(31)
 }
 
 // ----------------------------------------------------------------- backward
@@ -372,6 +491,7 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_bwd_kernel(RbBwdLaunch L) {
   const int lda = L.ld_lds;
   const int bo[3] = {0, RB_ROWS * lda, 2 * RB_ROWS * lda};
   const int ored = 3 * RB_ROWS * lda;     // [4][2][128] partial sums (pro 3)
+  RB_TRACE_OPEN(2)
 
   const int K0 = J.nst > 0 ? J.st[0].K : 0;   // = width of dP / dZ
   const int K0p = rb_k_pad(K0, true);
@@ -485,6 +605,7 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_bwd_kernel(RbBwdLaunch L) {
     }
   }
   __syncthreads();
+  RB_TRACE(2)
 
   // ---- chain of transposed Dense layers (dX = dZ W^T, tanh-grad on the way)
   for (int s = 0; s < J.nst; ++s) {
@@ -493,8 +614,9 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_bwd_kernel(RbBwdLaunch L) {
     const bool last = s + 1 == J.nst;
     if (!last) rb_pad(out, lda, S.N, rb_k_pad(J.st[s + 1].K, true), false);
     __syncthreads();
-    rb_dense<true>(bo[s % 3], lda, S, row0, nrows, last ? -1 : out, lda);
+    rb_dense<true>(bo[s % 3], lda, S, row0, nrows, last ? -1 : out, lda RB_TR_ARG(tr_ >= 0 ? tr_ + 8 + 4 * s : -1));
     __syncthreads();
+    RB_TRACE(3 + s)
   }
 }
 
@@ -536,3 +658,21 @@ hipError_t rb_setup_attributes() {
 }
 
 }  // namespace iwae
+
+#ifdef IWAE_RB_TRACE
+// copies (and clears) the trace records: 16 u64 per workgroup-0 of each job
+extern "C" int iwae_rb_trace_dump(unsigned long long* out, int cap) {
+  unsigned n = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(iwae::g_rb_trace_n), sizeof(n)) != hipSuccess) return -1;
+  n = n > 16384u ? 16384u : n;
+  const int m = (int)n < cap ? (int)n : cap;
+  if (m > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(iwae::g_rb_trace), m * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  std::vector<unsigned long long> z(16384, 0ull);
+  unsigned zero = 0;
+  hipMemcpyToSymbol(HIP_SYMBOL(iwae::g_rb_trace), z.data(), z.size() * sizeof(unsigned long long));
+  hipMemcpyToSymbol(HIP_SYMBOL(iwae::g_rb_trace_n), &zero, sizeof(zero));
+  return m;
+}
+#endif

@@ -153,8 +153,19 @@ struct RbNoise {             // where a sampling layer's eps comes from (see eps
   int kS, Bsplit, Bimg;
   uint64_t seed; int layer;
 };
+// Width the LDS operand of a row-block stage is zero-padded to (= the k range
+// its register-resident weight fetch covers): 32/64/128/256, then 64-multiples.
+__host__ __device__ inline int rb_k_pad(int K, bool bt) {
+  if (!bt && K <= 32) return 32;
+  if (K <= 64) return 64;
+  if (K <= 128) return 128;
+  if (K <= 256) return 256;
+  return (K + 63) & ~63;
+}
+
 struct RbStage {             // one Dense layer of a chain
   const float* W; int ldw;   // W_aug [fin+1][ldw]
+  unsigned W_bytes;          // readable bytes from W to the end of the (zero-slacked) allocation
   int K, N;                  // fwd: K = fin+1, N = fout; bwd: K = fout, N = fin
   int act;                   // 0 none, 1 tanh, 2 tanh-grad (times 1 - y^2)
   float* out_g; int ld_out;  // global copy of the stage output (rows of the job)

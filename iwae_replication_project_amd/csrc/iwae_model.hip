@@ -92,6 +92,7 @@ struct iwae_handle {
   long long nparam_int = 0, nparam_keras = 0;
   // persistent device state
   float* params = nullptr;
+  size_t params_bytes = 0;   // allocation incl. the zero tail the row-block weight fetch may over-read
   float* adam_m = nullptr;
   float* adam_v = nullptr;
   float* grad_own = nullptr;
@@ -663,18 +664,25 @@ static bool use_fused(const iwae_handle* h, const Plan& P) {
   return (long long)P.Bimg * P.kS <= 65536;
 }
 
+// LDS image row stride: the widest padded operand of any stage, + 4 floats
+// (rows then start 4 banks apart: the 16x4 MFMA A-fragment reads and the
+// epilogue writes are bank-conflict free)
 static int rb_ld(const iwae_handle* h, bool bwd) {
   int w = 0;
-  for (const auto& d : h->dense) w = std::max(w, std::max(d.fin + 1, d.fout + 1));
-  w = std::min(w, kRbMaxWidth);
-  w = (w + 15) & ~15;
-  return bwd ? ((w + 31) & ~31) + 4 : ((w + 31) & ~31) + 2;
+  for (const auto& d : h->dense) {
+    const bool first = &d == &h->dense[h->enc[0].l1], out = &d == &h->dense[h->o3];
+    if (!first) w = std::max(w, d.fin + 1);
+    if (!out) w = std::max(w, d.fout + 1);
+  }
+  (void)bwd;
+  return rb_k_pad(std::min(w, kRbMaxWidth), false) + 4;
 }
 
 static RbStage rb_fwd_stage(iwae_handle* h, int di, int act, Mat* out) {
   const DenseL& d = h->dense[di];
   RbStage s{};
   s.W = h->params + d.off; s.ldw = d.ldw; s.K = d.fin + 1; s.N = d.fout; s.act = act;
+  s.W_bytes = (unsigned)(h->params_bytes - (size_t)d.off * sizeof(float));
   if (out) { s.out_g = out->p; s.ld_out = out->ld; }
   return s;
 }
@@ -683,6 +691,7 @@ static RbStage rb_bwd_stage(iwae_handle* h, int di, const Mat* y, Mat* out) {
   const DenseL& d = h->dense[di];
   RbStage s{};
   s.W = h->params + d.off; s.ldw = d.ldw; s.K = d.fout; s.N = d.fin; s.act = y ? 2 : 0;
+  s.W_bytes = (unsigned)(h->params_bytes - (size_t)d.off * sizeof(float));
   if (y) { s.y = y->p; s.ldy = y->ld; }
   if (out) { s.out_g = out->p; s.ld_out = out->ld; }
   return s;
@@ -1074,12 +1083,17 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   hipError_t e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
   h->stream = h->own_stream;
   const size_t pb = (size_t)h->nparam_int * sizeof(float);
-  if (e == hipSuccess) e = hipMalloc(&h->params, pb);
+  // the row-block kernels fetch whole padded k ranges (up to 255 rows, or 256
+  // floats of a row, past a matrix's end): keep that inside a zeroed tail
+  int max_ldw = 4;
+  for (const auto& d : h->dense) max_ldw = std::max(max_ldw, d.ldw);
+  h->params_bytes = pb + (size_t)(256 * max_ldw + 256) * sizeof(float);
+  if (e == hipSuccess) e = hipMalloc(&h->params, h->params_bytes);
   if (e == hipSuccess) e = hipMalloc(&h->adam_m, pb);
   if (e == hipSuccess) e = hipMalloc(&h->adam_v, pb);
   if (e == hipSuccess) e = hipMalloc(&h->grad_own, pb);
   if (e == hipSuccess) e = hipMalloc(&h->ds, sizeof(DevState));
-  if (e == hipSuccess) e = hipMemset(h->params, 0, pb);
+  if (e == hipSuccess) e = hipMemset(h->params, 0, h->params_bytes);
   if (e == hipSuccess) e = hipMemset(h->adam_m, 0, pb);
   if (e == hipSuccess) e = hipMemset(h->adam_v, 0, pb);
   if (e == hipSuccess) e = hipMemset(h->grad_own, 0, pb);
