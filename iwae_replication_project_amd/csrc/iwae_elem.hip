@@ -18,33 +18,20 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Philox4x32-10 (Salmon et al. 2011), one normal per (row, layer, column)
-// via Box-Muller; counter = (row, layer<<20 | col, base_lo, base_hi).
-__device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t base, unsigned row,
-                                               unsigned layer, unsigned col) {
-  unsigned c0 = row, c1 = (layer << 20) | col, c2 = (unsigned)base, c3 = (unsigned)(base >> 32);
-  unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const unsigned lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-    const unsigned lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-    c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
-    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-  }
-  const float u0 = ((float)c0 + 0.5f) * 2.3283064365386963e-10f;  // (0,1)
-  const float u1 = ((float)c1 + 0.5f) * 2.3283064365386963e-10f;
-  return sqrtf(-2.f * logf(u0)) * cospif(2.f * u1);
-}
-
-__device__ __forceinline__ float eps_at(const float* ea, const float* eb, int kS, int Bsplit, int Bimg,
-                                        int d, int r, int j, uint64_t seed, uint64_t base, int layer) {
+// Noise of columns 4g..4g+3 of row r: injected (sample-major [k][B][d], the
+// reference's layout) when given for this row's draw, else device Philox.
+__device__ __forceinline__ float4 noise4(const float* ea, const float* eb, int kS, int Bsplit, int Bimg, int d,
+                                         int r, int g, uint64_t seed, uint64_t base, int layer) {
   const int bi = r / kS, s = r - bi * kS;
+  const float* src = nullptr;
   if (bi < Bsplit) {
-    if (ea) return ea[((size_t)s * Bsplit + bi) * d + j];
-  } else {
-    if (eb) return eb[((size_t)s * (Bimg - Bsplit) + (bi - Bsplit)) * d + j];
+    if (ea) src = ea + ((size_t)s * Bsplit + bi) * d;
+  } else if (eb) {
+    src = eb + ((size_t)s * (Bimg - Bsplit) + (bi - Bsplit)) * d;
   }
-  return philox_normal(seed, base, (unsigned)r, (unsigned)layer, (unsigned)j);
+  if (!src) return philox_normal4(seed, base, (unsigned)r, (unsigned)layer, (unsigned)g);
+  const int j = 4 * g;
+  return make_float4(src[min(j, d - 1)], src[min(j + 1, d - 1)], src[min(j + 2, d - 1)], src[min(j + 3, d - 1)]);
 }
 
 // Last-arriving workgroup detection (agent-scope release/acquire, counter form).
@@ -70,48 +57,78 @@ __device__ __forceinline__ bool last_block_arrive(unsigned* ticket) {
 // ------------------------------------------------------- Gaussian forward
 // TFP Normal._log_prob: -0.5*(x/s - loc/s)^2 - (0.5*log(2pi) + log(s)),
 // Normal.sample: eps*s + loc, with s = exp(zs) + 1e-6 (F:29, F:37).
+// A row is handled by `lpr` lanes (a power of two >= d/4), each owning four
+// consecutive columns (one Philox call); 64/lpr rows per wave.
 template <int MODE>
-__global__ __launch_bounds__(256) void gauss_fwd_kernel(GaussArgs a) {
+__global__ __launch_bounds__(256) void gauss_fwd_kernel(GaussArgs a, int lpr) {
   const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= a.M) return;
+  const int rpw = 64 / lpr;
+  const int r = (blockIdx.x * 4 + (threadIdx.x >> 6)) * rpw + lane / lpr;
+  const int sub = lane & (lpr - 1);
+  const bool ok = r < a.M;
   uint64_t base = 0;
   if (MODE == 0 && a.rng_base) base = *a.rng_base;
+  const float* __restrict__ P = a.P;
+  const float* __restrict__ Hin = a.H;
   float acc = 0.f;
-  for (int j = lane; j < a.d; j += 64) {
-    float lp;
-    if (MODE == 2) {
-      const float h = a.H[(size_t)r * a.ldH + j];
-      lp = __fsub_rn(-0.5f * (h * h), kHalfLog2Pi);
-    } else {
-      const int pr = r / a.prow_div;
-      const float mu = a.P[(size_t)pr * a.ldP + j];
-      const float zs = a.P[(size_t)pr * a.ldP + a.d + j];
-      const float sc = __fadd_rn(expf(zs), kScaleEps);
-      float h;
-      if (MODE == 0) {
-        const float e = eps_at(a.eps_a, a.eps_b, a.kS, a.Bsplit, a.Bimg, a.d, r, j, a.seed, base, a.layer);
-        h = __fadd_rn(__fmul_rn(e, sc), mu);
-        a.H[(size_t)r * a.ldH + j] = h;
-        if (a.eps_out) a.eps_out[(size_t)r * a.ld_eps_out + j] = e;
+  const int ng = (a.d + 3) >> 2;
+  for (int g = sub; ok && g < ng; g += lpr) {
+    float mu[4], zs[4], hv[4];
+    const int pr = r / a.prow_div;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = min(4 * g + q, a.d - 1);
+      if (MODE == 2) {
+        hv[q] = Hin[(size_t)r * a.ldH + j];
       } else {
-        h = a.H[(size_t)r * a.ldH + j];
+        mu[q] = P[(size_t)pr * a.ldP + j];
+        zs[q] = P[(size_t)pr * a.ldP + a.d + j];
+        if (MODE == 1) hv[q] = Hin[(size_t)r * a.ldH + j];
       }
-      const float z = __fsub_rn(h / sc, mu / sc);
-      lp = __fsub_rn(-0.5f * (z * z), __fadd_rn(kHalfLog2Pi, logf(sc)));
     }
-    acc += lp;
+    float4 e4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (MODE == 0) e4 = noise4(a.eps_a, a.eps_b, a.kS, a.Bsplit, a.Bimg, a.d, r, g, a.seed, base, a.layer);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = 4 * g + q;
+      if (j >= a.d) break;
+      float lp;
+      if (MODE == 2) {
+        lp = -0.5f * (hv[q] * hv[q]) - kHalfLog2Pi;
+      } else {
+        const float sc = fexp(zs[q]) + kScaleEps;
+        float h;
+        if (MODE == 0) {
+          const float e = f4_at(e4, q);
+          h = e * sc + mu[q];
+          a.H[(size_t)r * a.ldH + j] = h;
+          if (a.eps_out) a.eps_out[(size_t)r * a.ld_eps_out + j] = e;
+        } else {
+          h = hv[q];
+        }
+        lp = normal_logp(h, mu[q], sc);
+      }
+      acc += lp;
+    }
   }
-  acc = wave_sum(acc);
-  if (lane == 0) a.out[r] = a.accumulate ? a.out[r] + acc : acc;
+  for (int o = lpr >> 1; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (ok && sub == 0) a.out[r] = a.accumulate ? a.out[r] + acc : acc;
+}
+
+static int lanes_per_row(int d) {
+  int lpr = 1;
+  while (lpr < 64 && 4 * lpr < d) lpr <<= 1;
+  return lpr;
 }
 
 hipError_t launch_gauss_fwd(hipStream_t st, int mode, const GaussArgs& a) {
   if (a.M <= 0) return hipSuccess;
-  dim3 grid((a.M + 3) / 4);
-  if (mode == 0) hipLaunchKernelGGL(gauss_fwd_kernel<0>, grid, dim3(256), 0, st, a);
-  else if (mode == 1) hipLaunchKernelGGL(gauss_fwd_kernel<1>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(gauss_fwd_kernel<2>, grid, dim3(256), 0, st, a);
+  const int lpr = lanes_per_row(a.d);
+  const int rows_per_block = 4 * (64 / lpr);
+  dim3 grid((a.M + rows_per_block - 1) / rows_per_block);
+  if (mode == 0) hipLaunchKernelGGL(gauss_fwd_kernel<0>, grid, dim3(256), 0, st, a, lpr);
+  else if (mode == 1) hipLaunchKernelGGL(gauss_fwd_kernel<1>, grid, dim3(256), 0, st, a, lpr);
+  else hipLaunchKernelGGL(gauss_fwd_kernel<2>, grid, dim3(256), 0, st, a, lpr);
   return hipGetLastError();
 }
 
@@ -127,15 +144,22 @@ __global__ __launch_bounds__(256) void gauss_bwd_enc_kernel(GaussBwdArgs a) {
   const int pr = per_image ? blockIdx.x : blockIdx.x * 4 + wave;
   const int nP = (a.M + a.prow_div - 1) / a.prow_div;
   const bool row_ok = pr < nP;
+  const float* __restrict__ H = a.H;
+  const float* __restrict__ E = a.eps_rows;
+  const float* __restrict__ DL = a.dlw;
+  __amdgpu_buffer_rsrc_t rsrcs[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) rsrcs[q] = buf_rsrc(a.src[q]);
   for (int j0 = 0; j0 < a.d; j0 += 64) {
     const int j = j0 + lane;
     const bool act = row_ok && j < a.d;
-    float mu = 0.f, zs = 0.f, e = 0.f, sc = 1.f;
+    float mu = 0.f, zs = 0.f, e = 0.f, sc = 1.f, rs = 1.f;
     if (act) {
       mu = a.P[(size_t)pr * a.ldP + j];
       zs = a.P[(size_t)pr * a.ldP + a.d + j];
-      e = expf(zs);
-      sc = __fadd_rn(e, kScaleEps);
+      e = fexp(zs);
+      sc = e + kScaleEps;
+      rs = frcp(sc);
     }
     float amu = 0.f, asc = 0.f;
     if (act) {
@@ -145,18 +169,18 @@ __global__ __launch_bounds__(256) void gauss_bwd_enc_kernel(GaussBwdArgs a) {
 #pragma unroll 4
       for (int s = s_begin; s < s_end; s += s_step) {
         const int r = r_begin + s;
-        const float h = a.H[(size_t)r * a.ldH + j];
-        const float ev = a.eps_rows[(size_t)r * a.ld_eps + j];
-        const float dlq = -a.dlw[r];
-        const float z = __fsub_rn(h / sc, mu / sc);
+        const float h = H[(size_t)r * a.ldH + j];
+        const float ev = E[(size_t)r * a.ld_eps + j];
+        const float dl = DL[r], dlq = -dl;
+        const float z = h * rs - mu * rs;
         float G = 0.f;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          if (q < a.nsrc) G += a.src[q][(size_t)r * a.ldsrc[q] + j];
-        if (a.std_normal) G += a.dlw[r] * (-h);
-        G += dlq * (-z / sc);
-        amu += G + dlq * (z / sc);
-        asc += G * ev + dlq * ((z * z - 1.f) / sc);
+          G += bld1(rsrcs[q], q < a.nsrc ? (unsigned)(r * a.ldsrc[q] + j) * 4u : kOOB);
+        if (a.std_normal) G += dl * (-h);
+        G += dlq * (-z * rs);
+        amu += G + dlq * (z * rs);
+        asc += G * ev + dlq * ((z * z - 1.f) * rs);
       }
     }
     if (per_image) {
@@ -172,7 +196,7 @@ __global__ __launch_bounds__(256) void gauss_bwd_enc_kernel(GaussBwdArgs a) {
     if (act && (!per_image || wave == 0)) {
       if (a.kl_coef != 0.f) {
         amu += a.kl_coef * mu / (float)a.kl_rows;
-        asc += a.kl_coef * (sc - 1.f / sc) / (float)a.kl_rows;
+        asc += a.kl_coef * (sc - rs) / (float)a.kl_rows;
       }
       a.dP[(size_t)pr * a.lddP + j] = amu;
       a.dP[(size_t)pr * a.lddP + a.d + j] = asc * e;
@@ -185,17 +209,22 @@ __global__ __launch_bounds__(256) void gauss_bwd_prior_kernel(GaussBwdArgs a) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= a.M) return;
+  const float* __restrict__ P = a.P;
+  const float* __restrict__ H = a.H;
+  float* __restrict__ dh = a.dh_out;
+  float* __restrict__ dP = a.dP;
   const float dlp = a.dlw[r];
   for (int j = lane; j < a.d; j += 64) {
-    const float mu = a.P[(size_t)r * a.ldP + j];
-    const float zs = a.P[(size_t)r * a.ldP + a.d + j];
-    const float e = expf(zs);
-    const float sc = __fadd_rn(e, kScaleEps);
-    const float h = a.H[(size_t)r * a.ldH + j];
-    const float z = __fsub_rn(h / sc, mu / sc);
-    a.dh_out[(size_t)r * a.ldh_out + j] = dlp * (-z / sc);
-    a.dP[(size_t)r * a.lddP + j] = dlp * (z / sc);
-    a.dP[(size_t)r * a.lddP + a.d + j] = dlp * ((z * z - 1.f) / sc) * e;
+    const float mu = P[(size_t)r * a.ldP + j];
+    const float zs = P[(size_t)r * a.ldP + a.d + j];
+    const float h = H[(size_t)r * a.ldH + j];
+    const float e = fexp(zs);
+    const float sc = e + kScaleEps;
+    const float rs = frcp(sc);
+    const float z = h * rs - mu * rs;
+    dh[(size_t)r * a.ldh_out + j] = dlp * (-z * rs);
+    dP[(size_t)r * a.lddP + j] = dlp * (z * rs);
+    dP[(size_t)r * a.lddP + a.d + j] = dlp * ((z * z - 1.f) * rs) * e;
   }
 }
 
@@ -409,6 +438,7 @@ __global__ __launch_bounds__(kBoundWaves * 64) void bound_kernel(BoundArgs a) {
       for (int i = 0; i < kBoundWaves; ++i) tot += red[i];
       if (a.loss) *a.loss = a.loss_sign * tot + (a.loss_add ? a.loss_add_coef * *a.loss_add : 0.f);
       if (a.rng_base) { a.rng_base[1] = a.rng_base[0]; a.rng_base[0] += 1; }
+      if (a.adam_step) *a.adam_step += 1;      // the Adam launch of this train step reads it
       if (gridDim.x > 1) *a.ticket = 0u;
     }
   }
@@ -437,8 +467,8 @@ __global__ __launch_bounds__(256) void lse_kernel(LseArgs a) {
     for (int q = lane; q < a.kS; q += 64) {
       const int r = row0 + q;
       const float v = __fsub_rn(__fadd_rn(a.logp[r], row_sum_parts(a.part, a.ldpart, a.npart, r)), a.logq[r]);
-      if (v > m) { s = s * expf(m - v) + 1.f; m = v; }
-      else s += expf(v - m);
+      if (v > m) { s = s * fexp(m - v) + 1.f; m = v; }
+      else s += fexp(v - m);
     }
     const float M = wave_max(m);
     s = wave_sum(m == -INFINITY ? 0.f : s * expf(m - M));
@@ -508,7 +538,8 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const AdamSeg sg = a.seg[blockIdx.y];
   const AdamState st = *a.state;
   const float scale = a.grad_scale_override > 0.f ? a.grad_scale_override : st.grad_scale;
-  const float t = (float)(st.t + 1);
+  // state->t was already advanced for this step (bound kernel / adam_tick_kernel)
+  const float t = (float)st.t;
   const float b1p = powf(st.b1, t), b2p = powf(st.b2, t);
   const float alpha = st.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float omb1 = 1.f - st.b1, omb2 = 1.f - st.b2;
@@ -560,11 +591,11 @@ __global__ void adam_tick_kernel(AdamState* s) { s->t += 1; }
 
 hipError_t launch_adam(hipStream_t st, const AdamArgs& a, long long max_seg_n) {
   if (a.nseg <= 0) return hipSuccess;
+  if (a.do_adam && a.tick) hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(1), 0, st, a.state);
   long long bx = (max_seg_n / 4 + 255) / 256;
   if (bx > 64) bx = 64;
   if (bx < 1) bx = 1;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)bx, a.nseg), dim3(256), 0, st, a);
-  if (a.do_adam) hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(1), 0, st, a.state);
   return hipGetLastError();
 }
 

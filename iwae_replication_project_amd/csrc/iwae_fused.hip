@@ -38,30 +38,24 @@ __device__ __forceinline__ float rb_wave_sum(float v) {
   return v;
 }
 
-__device__ __forceinline__ float rb_philox_normal(uint64_t seed, uint64_t base, unsigned row, unsigned layer,
-                                                  unsigned col) {
-  unsigned c0 = row, c1 = (layer << 20) | col, c2 = (unsigned)base, c3 = (unsigned)(base >> 32);
-  unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const unsigned lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-    const unsigned lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-    c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
-    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+// Noise of columns 4g..4g+3 of sample row r (same stream as noise4 in iwae_elem.hip).
+__device__ __forceinline__ float4 rb_noise4(const RbNoise& nz, int d, int r, int g, uint64_t base) {
+  const int bi = r / nz.kS, s = r - bi * nz.kS;
+  const float* src = nullptr;
+  if (bi < nz.Bsplit) {
+    if (nz.eps_a) src = nz.eps_a + ((size_t)s * nz.Bsplit + bi) * d;
+  } else if (nz.eps_b) {
+    src = nz.eps_b + ((size_t)s * (nz.Bimg - nz.Bsplit) + (bi - nz.Bsplit)) * d;
   }
-  const float u0 = ((float)c0 + 0.5f) * 2.3283064365386963e-10f;
-  const float u1 = ((float)c1 + 0.5f) * 2.3283064365386963e-10f;
-  return sqrtf(-2.f * logf(u0)) * cospif(2.f * u1);
+  if (!src) return philox_normal4(nz.seed, base, (unsigned)r, (unsigned)nz.layer, (unsigned)g);
+  const int j = 4 * g;
+  return make_float4(src[min(j, d - 1)], src[min(j + 1, d - 1)], src[min(j + 2, d - 1)], src[min(j + 3, d - 1)]);
 }
 
-__device__ __forceinline__ float rb_eps(const RbNoise& nz, int d, int r, int j, uint64_t base) {
-  const int bi = r / nz.kS, s = r - bi * nz.kS;
-  if (bi < nz.Bsplit) {
-    if (nz.eps_a) return nz.eps_a[((size_t)s * nz.Bsplit + bi) * d + j];
-  } else {
-    if (nz.eps_b) return nz.eps_b[((size_t)s * (nz.Bimg - nz.Bsplit) + (bi - nz.Bsplit)) * d + j];
-  }
-  return rb_philox_normal(nz.seed, base, (unsigned)r, (unsigned)nz.layer, (unsigned)j);
+__device__ __forceinline__ float half_wave_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
 }
 
 extern __shared__ __attribute__((aligned(16))) float rbs[];
@@ -107,13 +101,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rb_rsrc(const float* p, unsign
 // the requests cost no address registers and all of them are in flight at
 // once (one memory round trip per stage); sched_barrier keeps the compiler
 // from re-interleaving them with the MFMAs.
-template <bool BT, int NS>
-__device__ __forceinline__ void rb_tile_pair(int ao, int lda, const RbStage& S, int t0, int t1, bool has1,
+template <bool BT, int NS, bool HAS1>
+__device__ __forceinline__ void rb_tile_pair(int ao, int lda, const RbStage& S, int t0, int t1,
                                              f32x4& c0, f32x4& c1, const int kofs RB_TR_PARAM) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
   const int N = S.N, ldw = S.ldw;
-  const int na = min(t0 * 16 + r, N - 1), nb = has1 ? min(t1 * 16 + r, N - 1) : na;
+  const int na = min(t0 * 16 + r, N - 1), nb = HAS1 ? min(t1 * 16 + r, N - 1) : na;
   if (!BT) {
     // rows k >= K read the following parameters or the zero tail of the
     // allocation (finite) against zeros in A.  (The range check does not see
@@ -125,7 +119,7 @@ __device__ __forceinline__ void rb_tile_pair(int ao, int lda, const RbStage& S, 
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
       pa[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, va, u * step, 0));
-      pb[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vb, u * step, 0));
+      if (HAS1) pb[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vb, u * step, 0));
     }
     __builtin_amdgcn_sched_barrier(0);
     RB_TRACE(1)
@@ -134,7 +128,7 @@ __device__ __forceinline__ void rb_tile_pair(int ao, int lda, const RbStage& S, 
     for (int u = 0; u < NS; ++u) {
       const float av = rbs[abase + u * 4];
       c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pa[u], c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pb[u], c1, 0, 0, 0);
+      if (HAS1) c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, pb[u], c1, 0, 0, 0);
     }
 #ifdef IWAE_RB_TRACE
     if (tr_ >= 0) {
@@ -151,9 +145,11 @@ __device__ __forceinline__ void rb_tile_pair(int ao, int lda, const RbStage& S, 
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
       const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, va, u * 64, 0);
-      const auto y = __builtin_amdgcn_raw_buffer_load_b128(rs, vb, u * 64, 0);
       pa[u] = make_float4(__uint_as_float(x[0]), __uint_as_float(x[1]), __uint_as_float(x[2]), __uint_as_float(x[3]));
-      pb[u] = make_float4(__uint_as_float(y[0]), __uint_as_float(y[1]), __uint_as_float(y[2]), __uint_as_float(y[3]));
+      if (HAS1) {
+        const auto y = __builtin_amdgcn_raw_buffer_load_b128(rs, vb, u * 64, 0);
+        pb[u] = make_float4(__uint_as_float(y[0]), __uint_as_float(y[1]), __uint_as_float(y[2]), __uint_as_float(y[3]));
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     RB_TRACE(1)
@@ -162,13 +158,13 @@ __device__ __forceinline__ void rb_tile_pair(int ao, int lda, const RbStage& S, 
     for (int u = 0; u < NS; ++u) {
       const float4 a4 = *reinterpret_cast<const float4*>(&rbs[abase + u * 16]);
       c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, pa[u].x, c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, pb[u].x, c1, 0, 0, 0);
+      if (HAS1) c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, pb[u].x, c1, 0, 0, 0);
       c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, pa[u].y, c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, pb[u].y, c1, 0, 0, 0);
+      if (HAS1) c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, pb[u].y, c1, 0, 0, 0);
       c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, pa[u].z, c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, pb[u].z, c1, 0, 0, 0);
+      if (HAS1) c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, pb[u].z, c1, 0, 0, 0);
       c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, pa[u].w, c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, pb[u].w, c1, 0, 0, 0);
+      if (HAS1) c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, pb[u].w, c1, 0, 0, 0);
     }
 #ifdef IWAE_RB_TRACE
     if (tr_ >= 0) {
@@ -176,6 +172,26 @@ __device__ __forceinline__ void rb_tile_pair(int ao, int lda, const RbStage& S, 
       g_rb_trace[tr_ + 2] = wall_clock64();
     }
 #endif
+  }
+}
+
+template <bool BT, bool HAS1>
+__device__ __forceinline__ void rb_tile_k(int ao, int lda, const RbStage& S, int t0, int t1, f32x4& c0, f32x4& c1
+                                          RB_TR_PARAM) {
+  const int K = S.K;
+  if (!BT) {
+    if (K <= 32) rb_tile_pair<false, 8, HAS1>(ao, lda, S, t0, t1, c0, c1, 0 RB_TR_ARG(tr_));
+    else if (K <= 64) rb_tile_pair<false, 16, HAS1>(ao, lda, S, t0, t1, c0, c1, 0 RB_TR_ARG(tr_));
+    else if (K <= 128) rb_tile_pair<false, 32, HAS1>(ao, lda, S, t0, t1, c0, c1, 0 RB_TR_ARG(tr_));
+    else if (K <= 256) rb_tile_pair<false, 64, HAS1>(ao, lda, S, t0, t1, c0, c1, 0 RB_TR_ARG(tr_));
+    else
+      for (int k0 = 0; k0 < K; k0 += 64) rb_tile_pair<false, 16, HAS1>(ao, lda, S, t0, t1, c0, c1, k0 RB_TR_ARG(tr_));
+  } else {
+    if (K <= 64) rb_tile_pair<true, 4, HAS1>(ao, lda, S, t0, t1, c0, c1, 0 RB_TR_ARG(tr_));
+    else if (K <= 128) rb_tile_pair<true, 8, HAS1>(ao, lda, S, t0, t1, c0, c1, 0 RB_TR_ARG(tr_));
+    else if (K <= 256) rb_tile_pair<true, 16, HAS1>(ao, lda, S, t0, t1, c0, c1, 0 RB_TR_ARG(tr_));
+    else
+      for (int k0 = 0; k0 < K; k0 += 64) rb_tile_pair<true, 4, HAS1>(ao, lda, S, t0, t1, c0, c1, k0 RB_TR_ARG(tr_));
   }
 }
 
@@ -192,7 +208,7 @@ template <bool BT>
 __device__ void rb_dense(int ao, int lda, const RbStage& S, int row0, int nrows, int oo, int ldo RB_TR_PARAM) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int K = S.K, N = S.N;
+  const int N = S.N;
   const int ntile = (N + 15) >> 4;
   for (int t0 = wave; t0 < ntile; t0 += 2 * RB_WAVES) {
     const int t1 = t0 + RB_WAVES;
@@ -214,20 +230,8 @@ __device__ void rb_dense(int ao, int lda, const RbStage& S, int row0, int nrows,
         }
     }
     // whole K in one round trip up to K = 256; wider layers in 64-k rounds
-    if (!BT) {
-      if (K <= 32) rb_tile_pair<false, 8>(ao, lda, S, t0, t1, has1, c0, c1, 0 RB_TR_ARG(tr_));
-      else if (K <= 64) rb_tile_pair<false, 16>(ao, lda, S, t0, t1, has1, c0, c1, 0 RB_TR_ARG(tr_));
-      else if (K <= 128) rb_tile_pair<false, 32>(ao, lda, S, t0, t1, has1, c0, c1, 0 RB_TR_ARG(tr_));
-      else if (K <= 256) rb_tile_pair<false, 64>(ao, lda, S, t0, t1, has1, c0, c1, 0 RB_TR_ARG(tr_));
-      else
-        for (int k0 = 0; k0 < K; k0 += 64) rb_tile_pair<false, 16>(ao, lda, S, t0, t1, has1, c0, c1, k0 RB_TR_ARG(tr_));
-    } else {
-      if (K <= 64) rb_tile_pair<true, 4>(ao, lda, S, t0, t1, has1, c0, c1, 0 RB_TR_ARG(tr_));
-      else if (K <= 128) rb_tile_pair<true, 8>(ao, lda, S, t0, t1, has1, c0, c1, 0 RB_TR_ARG(tr_));
-      else if (K <= 256) rb_tile_pair<true, 16>(ao, lda, S, t0, t1, has1, c0, c1, 0 RB_TR_ARG(tr_));
-      else
-        for (int k0 = 0; k0 < K; k0 += 64) rb_tile_pair<true, 4>(ao, lda, S, t0, t1, has1, c0, c1, k0 RB_TR_ARG(tr_));
-    }
+    if (has1) rb_tile_k<BT, true>(ao, lda, S, t0, t1, c0, c1 RB_TR_ARG(tr_));
+    else rb_tile_k<BT, false>(ao, lda, S, t0, t1, c0, c1 RB_TR_ARG(tr_));
     // epilogue: C[row = 4g + i][col = t*16 + r]
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -240,7 +244,7 @@ __device__ void rb_dense(int ao, int lda, const RbStage& S, int row0, int nrows,
           const int row = 4 * g + i;
           float v = c[i];
           if (S.act == 1) {
-            v = tanhf(v);
+            v = ftanh(v);
           } else if (BT && S.act == 2) {
             const float y = yv[q][i];
             v = v * (1.f - y * y);
@@ -258,12 +262,12 @@ __device__ void rb_dense(int ao, int lda, const RbStage& S, int row0, int nrows,
 // image at offset `ao`, zero-filling padding rows/columns up to `pad_to`.
 __device__ __forceinline__ void rb_load(int ao, int lda, const float* G, int ldg, int width, int pad_to,
                                         int row0, int nrows) {
-#pragma unroll 4
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(G + (size_t)row0 * ldg);
+#pragma unroll 8
   for (int e = threadIdx.x; e < RB_ROWS * pad_to; e += blockDim.x) {
     const int row = e / pad_to, col = e - row * pad_to;
     const bool ok = row < nrows && col < width;
-    const float v = G[(size_t)(row0 + (ok ? row : 0)) * ldg + (ok ? col : 0)];
-    rbs[ao + row * lda + col] = ok ? v : 0.f;
+    rbs[ao + row * lda + col] = bld1(rs, ok ? (unsigned)(row * ldg + col) * 4u : kOOB);
   }
 }
 
@@ -295,24 +299,27 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
   // ---- input rows into image 0
   const int K0 = J.st[0].K;                 // fin + 1 (ones column)
   const int K0p = rb_k_pad(K0, false);
+  const int t = threadIdx.x;
   if (J.pr_slabs) {
-    // first encoder layer: y1 = tanh(sum of the split-K partial products of x W1)
+    // first encoder layer: y1 = tanh(sum of the split-K partial products of x W1).
+    // Every slab value of this thread's elements is requested before any is summed.
     const int H = J.pr_H;
-    for (int e = threadIdx.x; e < RB_ROWS * K0p; e += blockDim.x) {
+    const float* __restrict__ sl = J.pr_slabs;
+    const __amdgpu_buffer_rsrc_t rsl = buf_rsrc(sl);
+    for (int e = t; e < RB_ROWS * K0p; e += blockDim.x) {
       const int rr = e / K0p, c = e - rr * K0p;
       float v = 0.f;
       if (rr < nrows && c < H) {
-        const float* sp = J.pr_slabs + (size_t)(row0 + rr) * J.pr_ld + c;
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-        int q = 0;
-        for (; q + 4 <= J.pr_nslab; q += 4) {
-          a0 += sp[(size_t)q * J.pr_stride];
-          a1 += sp[(size_t)(q + 1) * J.pr_stride];
-          a2 += sp[(size_t)(q + 2) * J.pr_stride];
-          a3 += sp[(size_t)(q + 3) * J.pr_stride];
-        }
-        for (; q < J.pr_nslab; ++q) a0 += sp[(size_t)q * J.pr_stride];
-        v = tanhf((a0 + a1) + (a2 + a3));
+        const unsigned o0 = (unsigned)((row0 + rr) * J.pr_ld + c);
+        float part[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          part[q] = bld1(rsl, q < J.pr_nslab ? (o0 + (unsigned)(q * J.pr_stride)) * 4u : kOOB);
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc += part[q];
+        for (int q = 16; q < J.pr_nslab; ++q) acc += sl[(size_t)q * J.pr_stride + o0];
+        v = ftanh(acc);
         J.pr_y[(size_t)(row0 + rr) * J.pr_ldy + c] = v;
       } else if (c == H) {
         v = 1.f;
@@ -321,97 +328,60 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
     }
   } else if (J.pro_sample) {
     // h = eps * scale + mu from the previous layer's P (Normal.sample, F:59/F:68).
-    // Each wave owns rows wave and wave+8; their (mu, zs[, eps]) are requested
-    // before any is used (one round trip), then Philox / log-density run.
+    // Thread t owns row t/32 and column quad t%32 (one Philox call = 4 normals);
+    // (mu, zs) of its quad are requested before any is used.
     const int d = J.ps_d;
-    constexpr int RPW = RB_ROWS / RB_WAVES;          // rows per wave
-    const int npass = (K0p + 63) >> 6;
-    if (npass <= 2) {
-      float mu[RPW][2], zs[RPW][2];
+    const int rr = t >> 5, gq = t & 31;
+    const int rg = row0 + min(rr, nrows - 1);
+    const int pr = rg / J.ps_div;
+    const float* __restrict__ Pp = J.ps_P + (size_t)pr * J.ps_ldP;
+    float accq = 0.f, accp = 0.f;
+    for (int g = gq; 4 * g < K0p; g += 32) {
+      float mu[4], zs[4];
 #pragma unroll
-      for (int q = 0; q < RPW; ++q)
-#pragma unroll
-        for (int pj = 0; pj < 2; ++pj) {
-          const int rr = wave + q * RB_WAVES, j = pj * 64 + lane;
-          const int rg = row0 + min(rr, nrows - 1);
-          const int jc = min(j, d - 1);
-          const int pr = rg / J.ps_div;
-          mu[q][pj] = J.ps_P[(size_t)pr * J.ps_ldP + jc];
-          zs[q][pj] = J.ps_P[(size_t)pr * J.ps_ldP + d + jc];
-        }
-#pragma unroll
-      for (int q = 0; q < RPW; ++q) {
-        const int rr = wave + q * RB_WAVES;
-        float accq = 0.f, accp = 0.f;
-#pragma unroll
-        for (int pj = 0; pj < 2; ++pj) {
-          const int j = pj * 64 + lane;
-          if (pj >= npass) break;
-          float hv = 0.f;
-          if (rr < nrows && j < d) {
-            const int rg = row0 + rr;
-            const float sc = __fadd_rn(expf(zs[q][pj]), kScaleEps);
-            const float e = rb_eps(J.ps_noise, d, rg, j, base);
-            hv = __fadd_rn(__fmul_rn(e, sc), mu[q][pj]);
-            J.ps_h[(size_t)rg * J.ps_ldh + j] = hv;
-            if (J.ps_eps) J.ps_eps[(size_t)rg * J.ps_ldeps + j] = e;
-            const float z = __fsub_rn(hv / sc, mu[q][pj] / sc);
-            accq += __fsub_rn(-0.5f * (z * z), __fadd_rn(kHalfLog2Pi, logf(sc)));
-            accp += __fsub_rn(-0.5f * (hv * hv), kHalfLog2Pi);
-          } else if (j == d) {
-            hv = 1.f;                        // ones column (bias row of W_aug)
-          }
-          if (j < K0p) rbs[bo[0] + rr * lda + j] = hv;
-        }
-        accq = rb_wave_sum(accq);
-        accp = rb_wave_sum(accp);
-        if (lane == 0) { rbs[oq + rr] = accq; rbs[op + rr] = accp; }
+      for (int q = 0; q < 4; ++q) {
+        const int jc = min(4 * g + q, d - 1);
+        mu[q] = Pp[jc];
+        zs[q] = Pp[d + jc];
       }
-    } else {
-      for (int rr = wave; rr < RB_ROWS; rr += RB_WAVES) {
-        float accq = 0.f, accp = 0.f;
-        for (int j0 = 0; j0 < K0p; j0 += 64) {
-          const int j = j0 + lane;
-          float hv = 0.f;
-          if (rr < nrows && j < d) {
-            const int rg = row0 + rr;
-            const int pr = rg / J.ps_div;
-            const float m = J.ps_P[(size_t)pr * J.ps_ldP + j];
-            const float z0 = J.ps_P[(size_t)pr * J.ps_ldP + d + j];
-            const float sc = __fadd_rn(expf(z0), kScaleEps);
-            const float e = rb_eps(J.ps_noise, d, rg, j, base);
-            hv = __fadd_rn(__fmul_rn(e, sc), m);
-            J.ps_h[(size_t)rg * J.ps_ldh + j] = hv;
-            if (J.ps_eps) J.ps_eps[(size_t)rg * J.ps_ldeps + j] = e;
-            const float z = __fsub_rn(hv / sc, m / sc);
-            accq += __fsub_rn(-0.5f * (z * z), __fadd_rn(kHalfLog2Pi, logf(sc)));
-            accp += __fsub_rn(-0.5f * (hv * hv), kHalfLog2Pi);
-          } else if (j == d) {
-            hv = 1.f;
-          }
-          if (j < K0p) rbs[bo[0] + rr * lda + j] = hv;
+      float4 e4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (rr < nrows && 4 * g < d) e4 = rb_noise4(J.ps_noise, d, rg, g, base);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = 4 * g + q;
+        float hv = 0.f;
+        if (rr < nrows && j < d) {
+          const float sc = fexp(zs[q]) + kScaleEps;
+          const float e = f4_at(e4, q);
+          hv = e * sc + mu[q];
+          J.ps_h[(size_t)rg * J.ps_ldh + j] = hv;
+          if (J.ps_eps) J.ps_eps[(size_t)rg * J.ps_ldeps + j] = e;
+          accq += normal_logp(hv, mu[q], sc);
+          accp += -0.5f * (hv * hv) - kHalfLog2Pi;
+        } else if (j == d) {
+          hv = 1.f;                        // ones column (bias row of W_aug)
         }
-        accq = rb_wave_sum(accq);
-        accp = rb_wave_sum(accp);
-        if (lane == 0) { rbs[oq + rr] = accq; rbs[op + rr] = accp; }
+        if (j < K0p) rbs[bo[0] + rr * lda + j] = hv;
       }
     }
+    accq = half_wave_sum(accq);
+    accp = half_wave_sum(accp);
+    if (gq == 0) { rbs[oq + rr] = accq; rbs[op + rr] = accp; }
   } else {
     rb_load(bo[0], lda, J.in, J.ld_in, K0, K0p, row0, nrows);
   }
   __syncthreads();
   if (!J.pro_sample && J.pro_stdnormal) {
     // log N(h; 0, 1) summed over the latent dims (F:135-F:136), from the LDS copy
-    for (int rr = wave; rr < RB_ROWS; rr += RB_WAVES) {
-      float acc = 0.f;
-      if (rr < nrows)
-        for (int j = lane; j < K0 - 1; j += 64) {
-          const float hv = rbs[bo[0] + rr * lda + j];
-          acc += __fsub_rn(-0.5f * (hv * hv), kHalfLog2Pi);
-        }
-      acc = rb_wave_sum(acc);
-      if (lane == 0) rbs[op + rr] = acc;
-    }
+    const int rr = t >> 5, gq = t & 31;
+    float acc = 0.f;
+    if (rr < nrows)
+      for (int j = gq; j < K0 - 1; j += 32) {
+        const float hv = rbs[bo[0] + rr * lda + j];
+        acc += -0.5f * (hv * hv) - kHalfLog2Pi;
+      }
+    acc = half_wave_sum(acc);
+    if (gq == 0) rbs[op + rr] = acc;
   }
   RB_TRACE(2)
 
@@ -427,46 +397,47 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
   }
   const int P = bo[J.nst % 3];
 
-  // ---- epilogue
-  if (J.epi == 1) {
-    // encoder: sample the next h and add its log q (F:68, F:70, F:73)
+  // ---- epilogue (thread t: row t/32, column quad t%32)
+  if (J.epi == 1 || J.epi == 2) {
     const int d = J.ep_d;
-    for (int rr = wave; rr < RB_ROWS; rr += RB_WAVES) {
-      if (rr >= nrows) continue;
-      const int rg = row0 + rr;
-      float acc = 0.f;
-      for (int j = lane; j < d; j += 64) {
-        const float mu = rbs[P + rr * lda + j], zs = rbs[P + rr * lda + d + j];
-        const float sc = __fadd_rn(expf(zs), kScaleEps);
-        const float e = rb_eps(J.ep_noise, d, rg, j, base);
-        const float hv = __fadd_rn(__fmul_rn(e, sc), mu);
-        J.ep_h[(size_t)rg * J.ep_ldh + j] = hv;
-        if (J.ep_eps) J.ep_eps[(size_t)rg * J.ep_ldeps + j] = e;
-        const float z = __fsub_rn(hv / sc, mu / sc);
-        acc += __fsub_rn(-0.5f * (z * z), __fadd_rn(kHalfLog2Pi, logf(sc)));
+    const int rr = t >> 5, gq = t & 31;
+    const int rg = row0 + min(rr, nrows - 1);
+    float acc = 0.f;
+    for (int g = gq; 4 * g < d; g += 32) {
+      float tg[4];
+      float4 e4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (J.epi == 2) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tg[q] = J.ep_tgt[(size_t)rg * J.ep_ldtgt + min(4 * g + q, d - 1)];
+      } else if (rr < nrows) {
+        e4 = rb_noise4(J.ep_noise, d, rg, g, base);
       }
-      acc = rb_wave_sum(acc);
-      if (lane == 0) {
-        const float prev = J.pro_sample ? rbs[oq + rr] : (J.logq_acc ? J.logq[rg] : 0.f);
-        J.logq[rg] = prev + acc;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = 4 * g + q;
+        if (rr >= nrows || j >= d) break;
+        const float mu = rbs[P + rr * lda + j], zs = rbs[P + rr * lda + d + j];
+        const float sc = fexp(zs) + kScaleEps;
+        float hv;
+        if (J.epi == 1) {
+          // encoder: sample the next h and add its log q (F:68, F:70, F:73)
+          const float e = f4_at(e4, q);
+          hv = e * sc + mu;
+          J.ep_h[(size_t)rg * J.ep_ldh + j] = hv;
+          if (J.ep_eps) J.ep_eps[(size_t)rg * J.ep_ldeps + j] = e;
+        } else {
+          // decoder prior: log p(h_t | h_src) added to log p (F:139-F:141)
+          hv = tg[q];
+        }
+        acc += normal_logp(hv, mu, sc);
       }
     }
-  } else if (J.epi == 2) {
-    // decoder prior: log p(h_t | h_src) added to log p (F:139-F:141)
-    const int d = J.ep_d;
-    for (int rr = wave; rr < RB_ROWS; rr += RB_WAVES) {
-      if (rr >= nrows) continue;
-      const int rg = row0 + rr;
-      float acc = 0.f;
-      for (int j = lane; j < d; j += 64) {
-        const float mu = rbs[P + rr * lda + j], zs = rbs[P + rr * lda + d + j];
-        const float sc = __fadd_rn(expf(zs), kScaleEps);
-        const float hv = J.ep_tgt[(size_t)rg * J.ep_ldtgt + j];
-        const float z = __fsub_rn(hv / sc, mu / sc);
-        acc += __fsub_rn(-0.5f * (z * z), __fadd_rn(kHalfLog2Pi, logf(sc)));
-      }
-      acc = rb_wave_sum(acc);
-      if (lane == 0) {
+    acc = half_wave_sum(acc);
+    if (gq == 0 && rr < nrows) {
+      if (J.epi == 1) {
+        const float prev = J.pro_sample ? rbs[oq + rr] : (J.logq_acc ? J.logq[rg] : 0.f);
+        J.logq[rg] = prev + acc;
+      } else {
         const float prev = J.pro_stdnormal ? rbs[op + rr] : (J.logp_acc ? J.logp[rg] : 0.f);
         J.logp[rg] = prev + acc;
       }
@@ -490,7 +461,7 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_bwd_kernel(RbBwdLaunch L) {
   const int nrows = min(J.rpb, J.rows - row0);
   const int lda = L.ld_lds;
   const int bo[3] = {0, RB_ROWS * lda, 2 * RB_ROWS * lda};
-  const int ored = 3 * RB_ROWS * lda;     // [4][2][128] partial sums (pro 3)
+  const int ored = 3 * RB_ROWS * lda;     // [512][8] partial sums (pro 3)
   RB_TRACE_OPEN(2)
 
   const int K0 = J.nst > 0 ? J.st[0].K : 0;   // = width of dP / dZ
@@ -499,109 +470,155 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_bwd_kernel(RbBwdLaunch L) {
   if (J.pro == 0) {
     rb_load(D, lda, J.dz_in, J.ld_dz_in, K0, K0p, row0, nrows);
   } else if (J.pro == 1 || J.pro == 2) {
-    // per row: dP of an encoder sampling layer (pro 1) or a decoder prior head (pro 2)
+    // per row: dP of an encoder sampling layer (pro 1) or a decoder prior head (pro 2).
+    // Thread t: row t/32, column quad t%32; all of its loads are issued first.
     const int d = J.d;
-#pragma unroll 2
-    for (int e = threadIdx.x; e < RB_ROWS * K0p; e += blockDim.x) {
-      const int rr = e / K0p, c = e - rr * K0p;
-      if (c >= d || rr >= nrows) {
-        if (c >= 2 * d || rr >= nrows) rbs[D + rr * lda + c] = 0.f;
-        continue;
-      }
-      const int rg = row0 + rr;
-      const float mu = J.P[(size_t)rg * J.ldP + c];
-      const float zs = J.P[(size_t)rg * J.ldP + d + c];
-      const float hv = J.H[(size_t)rg * J.ldH + c];
-      const float dl = J.dlw[rg];
-      float G = 0.f, ev = 0.f;
-      if (J.pro == 1) {
-        ev = J.eps[(size_t)rg * J.ld_eps + c];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (q < J.nsrc) G += J.src[q][(size_t)rg * J.ldsrc[q] + c];
-      }
-      const float ez = expf(zs);
-      const float sc = __fadd_rn(ez, kScaleEps);
-      const float z = __fsub_rn(hv / sc, mu / sc);
-      float dmu, dsc;
-      if (J.pro == 2) {
-        // log p(h_t | .): dL/dlogp = dlw; the target h gets -z/s (kept for the encoder pass)
-        J.dh_out[(size_t)rg * J.ld_dh + c] = dl * (-z / sc);
-        dmu = dl * (z / sc);
-        dsc = dl * ((z * z - 1.f) / sc);
-      } else {
-        const float dlq = -dl;
-        if (J.std_normal) G += dl * (-hv);
-        G += dlq * (-z / sc);
-        dmu = G + dlq * (z / sc);
-        dsc = G * ev + dlq * ((z * z - 1.f) / sc);
-        if (J.kl_coef != 0.f) {
-          dmu += J.kl_coef * mu / (float)J.kl_rows;
-          dsc += J.kl_coef * (sc - 1.f / sc) / (float)J.kl_rows;
-        }
-      }
-      const float dzs = dsc * ez;
-      rbs[D + rr * lda + c] = dmu;
-      rbs[D + rr * lda + d + c] = dzs;
-      J.dP_out[(size_t)rg * J.ld_dP + c] = dmu;
-      J.dP_out[(size_t)rg * J.ld_dP + d + c] = dzs;
-    }
-  } else {
-    // pro 3: first encoder layer, rows = images; reduce the sampling-layer
-    // partials over the kS sample rows of each image (mu, scale broadcast over k)
-    const int d = J.d, kS = J.kS;
-    for (int e = threadIdx.x; e < RB_ROWS * K0p; e += blockDim.x) {
+    const int t = threadIdx.x;
+    for (int e = t; e < RB_ROWS * K0p; e += blockDim.x) {     // zero padding / idle rows
       const int rr = e / K0p, c = e - rr * K0p;
       if (c >= 2 * d || rr >= nrows) rbs[D + rr * lda + c] = 0.f;
     }
-    const int grp = threadIdx.x >> 7, tj = threadIdx.x & 127;   // 4 sample groups x 128 columns
+    const int rr = t >> 5, gq = t & 31;
+    const __amdgpu_buffer_rsrc_t reps = buf_rsrc(J.eps);
+    __amdgpu_buffer_rsrc_t rsrcs[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) rsrcs[u] = buf_rsrc(J.src[u]);
+    if (rr < nrows) {
+      const int rg = row0 + rr;
+      const float* __restrict__ Pr = J.P + (size_t)rg * J.ldP;
+      const float* __restrict__ Hr = J.H + (size_t)rg * J.ldH;
+      const float dl = J.dlw[rg];
+      for (int g = gq; 4 * g < d; g += 32) {
+        float mu[4], zs[4], hv[4], ev[4], G[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = min(4 * g + q, d - 1);
+          mu[q] = Pr[c];
+          zs[q] = Pr[d + c];
+          hv[q] = Hr[c];
+          // pro 2 has no eps / dh sources: every such load reads 0 (kOOB)
+          const bool p1 = J.pro == 1;
+          ev[q] = bld1(reps, p1 ? (unsigned)(rg * J.ld_eps + c) * 4u : kOOB);
+          G[q] = 0.f;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            G[q] += bld1(rsrcs[u], (p1 && u < J.nsrc) ? (unsigned)(rg * J.ldsrc[u] + c) * 4u : kOOB);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = 4 * g + q;
+          if (c >= d) break;
+          const float ez = fexp(zs[q]);
+          const float sc = ez + kScaleEps;
+          const float rs = frcp(sc);
+          const float z = hv[q] * rs - mu[q] * rs;
+          float dmu, dsc;
+          if (J.pro == 2) {
+            // log p(h_t | .): dL/dlogp = dlw; the target h gets -z/s (kept for the encoder pass)
+            J.dh_out[(size_t)rg * J.ld_dh + c] = dl * (-z * rs);
+            dmu = dl * (z * rs);
+            dsc = dl * ((z * z - 1.f) * rs);
+          } else {
+            const float dlq = -dl;
+            float Gq = G[q];
+            if (J.std_normal) Gq += dl * (-hv[q]);
+            Gq += dlq * (-z * rs);
+            dmu = Gq + dlq * (z * rs);
+            dsc = Gq * ev[q] + dlq * ((z * z - 1.f) * rs);
+            if (J.kl_coef != 0.f) {
+              dmu += J.kl_coef * mu[q] / (float)J.kl_rows;
+              dsc += J.kl_coef * (sc - rs) / (float)J.kl_rows;
+            }
+          }
+          const float dzs = dsc * ez;
+          rbs[D + rr * lda + c] = dmu;
+          rbs[D + rr * lda + d + c] = dzs;
+          J.dP_out[(size_t)rg * J.ld_dP + c] = dmu;
+          J.dP_out[(size_t)rg * J.ld_dP + d + c] = dzs;
+        }
+      }
+    }
+  } else {
+    // pro 3: first encoder layer, rows = images; reduce the sampling-layer
+    // partials over the kS sample rows of each image (mu, scale broadcast over k).
+    // Thread t: column quad t % nq, samples s = t / nq (+ sgroups ...).
+    const int d = J.d, kS = J.kS;
+    const int t = threadIdx.x;
+    const int nq = (d + 3) >> 2;
+    const int sgroups = max(1, (int)blockDim.x / nq);
+    __amdgpu_buffer_rsrc_t rsrcs[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) rsrcs[u] = buf_rsrc(J.src[u]);
+    for (int e = t; e < RB_ROWS * K0p; e += blockDim.x) {
+      const int rr = e / K0p, c = e - rr * K0p;
+      if (c >= 2 * d || rr >= nrows) rbs[D + rr * lda + c] = 0.f;
+    }
     for (int rr = 0; rr < nrows; ++rr) {
       const int img = row0 + rr;
-      for (int j0 = 0; j0 < d; j0 += 128) {
-        const int c = j0 + tj;
-        float amu = 0.f, asc = 0.f, mu = 0.f, sc = 1.f, ez = 0.f;
-        if (c < d) {
-          mu = J.P[(size_t)img * J.ldP + c];
-          const float zs = J.P[(size_t)img * J.ldP + d + c];
-          ez = expf(zs);
-          sc = __fadd_rn(ez, kScaleEps);
-#pragma unroll 4
-          for (int s = grp; s < kS; s += 4) {
-            const int rg = img * kS + s;
-            const float hv = J.H[(size_t)rg * J.ldH + c];
-            const float ev = J.eps[(size_t)rg * J.ld_eps + c];
-            const float dl = J.dlw[rg], dlq = -dl;
-            float G = 0.f;
+      const int gq = t % nq, sg = t / nq;
+      float mu[4], ez[4], sc[4], rs[4], amu[4] = {0.f, 0.f, 0.f, 0.f}, asc[4] = {0.f, 0.f, 0.f, 0.f};
+      if (sg < sgroups) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-              if (q < J.nsrc) G += J.src[q][(size_t)rg * J.ldsrc[q] + c];
-            const float z = __fsub_rn(hv / sc, mu / sc);
-            if (J.std_normal) G += dl * (-hv);
-            G += dlq * (-z / sc);
-            amu += G + dlq * (z / sc);
-            asc += G * ev + dlq * ((z * z - 1.f) / sc);
+        for (int q = 0; q < 4; ++q) {
+          const int c = min(4 * gq + q, d - 1);
+          mu[q] = J.P[(size_t)img * J.ldP + c];
+          ez[q] = fexp(J.P[(size_t)img * J.ldP + d + c]);
+          sc[q] = ez[q] + kScaleEps;
+          rs[q] = frcp(sc[q]);
+        }
+#pragma unroll 4
+        for (int s = sg; s < kS; s += sgroups) {
+          const int rg = img * kS + s;
+          float hv[4], ev[4], G[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int c = min(4 * gq + q, d - 1);
+            hv[q] = J.H[(size_t)rg * J.ldH + c];
+            ev[q] = J.eps[(size_t)rg * J.ld_eps + c];
+            G[q] = 0.f;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              G[q] += bld1(rsrcs[u], u < J.nsrc ? (unsigned)(rg * J.ldsrc[u] + c) * 4u : kOOB);
+          }
+          const float dl = J.dlw[rg], dlq = -dl;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float z = hv[q] * rs[q] - mu[q] * rs[q];
+            float Gq = G[q];
+            if (J.std_normal) Gq += dl * (-hv[q]);
+            Gq += dlq * (-z * rs[q]);
+            amu[q] += Gq + dlq * (z * rs[q]);
+            asc[q] += Gq * ev[q] + dlq * ((z * z - 1.f) * rs[q]);
           }
         }
-        rbs[ored + (grp * 2 + 0) * 128 + tj] = amu;
-        rbs[ored + (grp * 2 + 1) * 128 + tj] = asc;
-        __syncthreads();
-        if (grp == 0 && c < d) {
-          amu = rbs[ored + 0 * 128 + tj] + rbs[ored + 2 * 128 + tj] + rbs[ored + 4 * 128 + tj] +
-                rbs[ored + 6 * 128 + tj];
-          asc = rbs[ored + 1 * 128 + tj] + rbs[ored + 3 * 128 + tj] + rbs[ored + 5 * 128 + tj] +
-                rbs[ored + 7 * 128 + tj];
-          if (J.kl_coef != 0.f) {
-            amu += J.kl_coef * mu / (float)J.kl_rows;
-            asc += J.kl_coef * (sc - 1.f / sc) / (float)J.kl_rows;
-          }
-          const float dzs = asc * ez;
-          rbs[D + rr * lda + c] = amu;
-          rbs[D + rr * lda + d + c] = dzs;
-          J.dP_out[(size_t)img * J.ld_dP + c] = amu;
-          J.dP_out[(size_t)img * J.ld_dP + d + c] = dzs;
-        }
-        __syncthreads();
       }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        rbs[ored + t * 8 + q] = amu[q];
+        rbs[ored + t * 8 + 4 + q] = asc[q];
+      }
+      __syncthreads();
+      if (t < d) {
+        const int c = t, cq = c >> 2, cr = c & 3;
+        float sm = 0.f, ss = 0.f;
+        for (int g2 = 0; g2 < sgroups; ++g2) {
+          sm += rbs[ored + (g2 * nq + cq) * 8 + cr];
+          ss += rbs[ored + (g2 * nq + cq) * 8 + 4 + cr];
+        }
+        const float m0 = J.P[(size_t)img * J.ldP + c];
+        const float e0 = fexp(J.P[(size_t)img * J.ldP + d + c]);
+        const float s0 = e0 + kScaleEps;
+        if (J.kl_coef != 0.f) {
+          sm += J.kl_coef * m0 / (float)J.kl_rows;
+          ss += J.kl_coef * (s0 - frcp(s0)) / (float)J.kl_rows;
+        }
+        const float dzs = ss * e0;
+        rbs[D + rr * lda + c] = sm;
+        rbs[D + rr * lda + d + c] = dzs;
+        J.dP_out[(size_t)img * J.ld_dP + c] = sm;
+        J.dP_out[(size_t)img * J.ld_dP + d + c] = dzs;
+      }
+      __syncthreads();
     }
   }
   __syncthreads();
@@ -645,7 +662,7 @@ hipError_t launch_rb_bwd(hipStream_t st, RbBwdLaunch& L) {
   for (int i = 0; i < L.njobs; ++i) { rows[i] = L.job[i].rows; rpb[i] = L.job[i].rpb; }
   const int nb = launch_blocks(L.njobs, rows, rpb, L.block_start);
   if (nb <= 0) return hipSuccess;
-  const size_t lds = (size_t)(3 * RB_ROWS * L.ld_lds + 8 * 128) * sizeof(float);
+  const size_t lds = (size_t)(3 * RB_ROWS * L.ld_lds + 8 * RB_WAVES * 64) * sizeof(float);
   hipLaunchKernelGGL(rb_bwd_kernel, dim3(nb), dim3(RB_WAVES * 64), lds, st, L);
   return hipGetLastError();
 }

@@ -33,7 +33,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KSCALE>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const int by, const int bz) {
   constexpr int NTH = WM * WN * 64;
-  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 16;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = (TM == 1 && TN == 1) ? 32 : 16;
   // k-major LDS images.  Transposed (scalar) writes want a row stride = 2 mod 32
   // floats (conflict-free, see header); float4 writes want a multiple of 4.
   constexpr int LDSA = BM + (TA ? 4 : 2);
@@ -56,43 +56,47 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
   const int M = a.M, N = a.N;
 
   float4 ra[A_F4], rb[B_F4];
+  // block-relative buffer bases (uniform); out-of-tile lanes read 0 via kOOB
+  const __amdgpu_buffer_rsrc_t rsA =
+      buf_rsrc(TA ? a.A + (size_t)kbeg * a.lda + m0 : a.A + (size_t)m0 * a.lda + kbeg);
+  const __amdgpu_buffer_rsrc_t rsB =
+      buf_rsrc(TB ? a.B + (size_t)n0 * a.ldb + kbeg : a.B + (size_t)kbeg * a.ldb + n0);
+  const int klen = kend - kbeg;
 
-  auto gload = [&](int k0) {
+  auto gload = [&](int k0) {      // k0 relative to kbeg
 #pragma unroll
     for (int i = 0; i < A_F4; ++i) {
       const int f = tid + i * NTH;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      unsigned off;
       if (!TA) {
-        const int mr = f >> 2, kq = f & 3;
-        const int gm = m0 + mr, gk = k0 + 4 * kq;
-        if (gm < M && gk < kend) v = *reinterpret_cast<const float4*>(a.A + (size_t)gm * a.lda + gk);
+        const int mr = f / (BK / 4), kq = f % (BK / 4);
+        const int gk = k0 + 4 * kq;
+        off = (m0 + mr < M && gk < klen) ? (unsigned)(mr * a.lda + gk) * 4u : kOOB;
       } else {
         const int kr = f / (BM / 4), mq = f % (BM / 4);
-        const int gk = k0 + kr, gm = m0 + 4 * mq;
-        if (gk < kend && gm < M) v = *reinterpret_cast<const float4*>(a.A + (size_t)gk * a.lda + gm);
+        const int gk = k0 + kr;
+        off = (gk < klen && m0 + 4 * mq < M) ? (unsigned)(gk * a.lda + 4 * mq) * 4u : kOOB;
       }
-      ra[i] = v;
+      ra[i] = bld4(rsA, off);
     }
 #pragma unroll
     for (int i = 0; i < B_F4; ++i) {
       const int f = tid + i * NTH;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (!TB) {
         const int kr = f / (BN / 4), nq = f % (BN / 4);
-        const int gk = k0 + kr, gn = n0 + 4 * nq;
-        if (gk < kend && gn < N) {
-          v = *reinterpret_cast<const float4*>(a.B + (size_t)gk * a.ldb + gn);
-          if (KSCALE && a.kscale) {
-            const float s = a.kscale[gk];
-            v.x *= s; v.y *= s; v.z *= s; v.w *= s;
-          }
+        const int gk = k0 + kr;
+        const bool ok = gk < klen && n0 + 4 * nq < N;
+        float4 v = bld4(rsB, ok ? (unsigned)(gk * a.ldb + 4 * nq) * 4u : kOOB);
+        if (KSCALE && a.kscale) {
+          const float s = a.kscale[kbeg + min(gk, klen - 1)];
+          v.x *= s; v.y *= s; v.z *= s; v.w *= s;
         }
+        rb[i] = v;
       } else {
-        const int nr = f >> 2, kq = f & 3;
-        const int gn = n0 + nr, gk = k0 + 4 * kq;
-        if (gn < N && gk < kend) v = *reinterpret_cast<const float4*>(a.B + (size_t)gn * a.ldb + gk);
+        const int nr = f / (BK / 4), kq = f % (BK / 4);
+        const int gk = k0 + 4 * kq;
+        rb[i] = bld4(rsB, (n0 + nr < N && gk < klen) ? (unsigned)(nr * a.ldb + gk) * 4u : kOOB);
       }
-      rb[i] = v;
     }
   };
 
@@ -103,7 +107,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
     for (int i = 0; i < A_F4; ++i) {
       const int f = tid + i * NTH;
       if (!TA) {
-        const int mr = f >> 2, kq = f & 3;
+        const int mr = f / (BK / 4), kq = f % (BK / 4);
         Ab[(4 * kq + 0) * LDSA + mr] = ra[i].x;
         Ab[(4 * kq + 1) * LDSA + mr] = ra[i].y;
         Ab[(4 * kq + 2) * LDSA + mr] = ra[i].z;
@@ -120,7 +124,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
         const int kr = f / (BN / 4), nq = f % (BN / 4);
         *reinterpret_cast<float4*>(Bb + kr * LDSB + 4 * nq) = rb[i];
       } else {
-        const int nr = f >> 2, kq = f & 3;
+        const int nr = f / (BK / 4), kq = f % (BK / 4);
         Bb[(4 * kq + 0) * LDSB + nr] = rb[i].x;
         Bb[(4 * kq + 1) * LDSB + nr] = rb[i].y;
         Bb[(4 * kq + 2) * LDSB + nr] = rb[i].z;
@@ -139,7 +143,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
 
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   if (nk > 0) {
-    gload(kbeg);
+    gload(0);
     sstore(0);
   }
   __syncthreads();
@@ -148,7 +152,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
   const int khalf = lane >> 5;
   for (int t = 0; t < nk; ++t) {
     const int cur = t & 1;
-    if (t + 1 < nk) gload(kbeg + (t + 1) * BK);
+    if (t + 1 < nk) gload((t + 1) * BK);
     const float* Ab = As + cur * BK * LDSA;
     const float* Bb = Bs + cur * BK * LDSB;
 #pragma unroll
@@ -178,19 +182,39 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+        // epilogue operands of all 16 elements requested before the first store
+        // (clamped addresses: unconditional loads, no per-element branch)
+        float yv[16], rsv[16];
+        const int nc = min(n, N - 1);
+        if (EPI == EPI_TANH_GRAD) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + rowq;
+            yv[r] = a.aux[(size_t)min(m, M - 1) * a.ldaux + nc];
+          }
+        }
+        if (EPI != EPI_TANH && a.rowscale) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + rowq;
+            rsv[r] = a.rowscale[min(m, M - 1)];
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) rsv[r] = 1.f;
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + rowq;
           if (m < M && n < N) {
             float v = acc[i][j][r];
             if (EPI == EPI_TANH) {
-              v = tanhf(v);
+              v = ftanh(v);
             } else if (EPI == EPI_TANH_GRAD) {
-              if (a.rowscale) v = v * a.rowscale[m];
-              const float y = a.aux[(size_t)m * a.ldaux + n];
-              v = v * (1.f - y * y);
+              v = v * rsv[r];
+              v = v * (1.f - yv[r] * yv[r]);
             } else {  // EPI_STORE
-              if (a.rowscale) v = v * a.rowscale[m];
+              v = v * rsv[r];
             }
             C[(size_t)m * a.ldc + n] = v;
           }
@@ -204,14 +228,22 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
     auto bern_tile = [&](const f32x16& t, const int i, const int j) {
         const int ncol0 = n0 + wn * TN * 32 + j * 32;
         const int n = ncol0 + (lane & 31);
-        float vb[16];
+        float vb[16], xs[16];
+        // pixels of all 16 elements requested before the first store (clamped,
+        // unconditional; out-of-tile elements are masked below)
+        const int nc = min(n, N - 1);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + rowq;
+          xs[r] = a.aux[(size_t)(min(m, M - 1) / a.x_row_div) * a.ldaux + nc];
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int ml = (r & 3) + 8 * (r >> 2) + rowq;
           const int m = m0 + wm * TM * 32 + i * 32 + ml;
           float val = 0.f, bce = 0.f;
           const bool ok = (m < M && n < N);
-          const float xv = ok ? a.aux[(size_t)(m / a.x_row_div) * a.ldaux + n] : 0.f;
+          const float xv = xs[r];
           const float l = t[r];
           const float s = __fdividef(1.f, 1.f + __expf(-l));
           const float p = __fadd_rn(__fmul_rn(s, kProbScale), kProbShift);

@@ -22,6 +22,85 @@ constexpr float kScaleEps = 1e-6f;           // F:37
 constexpr float kKerasEps = 1e-7f;           // keras.backend.epsilon()
 constexpr float kHalfLog2Pi = 0.918938533204672742f;
 
+// ------------------------------------------------------------ fast math ----
+// Hardware transcendentals (v_exp_f32 / v_log_f32 / v_rcp_f32 / v_sin_f32,
+// ~1 ulp) instead of the correctly-rounded library routines: the epilogues
+// and prologues of the small-batch kernels are VALU-latency bound, and the
+// parity budget (1e-4 relative on losses and gradients) is ~1000x their error.
+__device__ __forceinline__ float fexp(float x) { return __expf(x); }
+__device__ __forceinline__ float flog(float x) { return __logf(x); }
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// tanh: odd Taylor polynomial below |x| = 1/16 (truncation < 4e-9 relative),
+// (1 - e)/(1 + e) with e = exp(-2|x|) above (< 2e-7 absolute).
+__device__ __forceinline__ float ftanh(float x) {
+  const float ax = fabsf(x);
+  const float e = __expf(-2.f * ax);
+  const float big = (1.f - e) * frcp(1.f + e);
+  const float x2 = x * x;
+  const float small = ax * __builtin_fmaf(x2, __builtin_fmaf(x2, 0.133333333f, -0.333333333f), 1.f);
+  return copysignf(ax < 0.0625f ? small : big, x);
+}
+
+// Philox4x32-10 (Salmon et al. 2011) -> four N(0,1) by Box-Muller on both
+// uniform pairs.  Counter = (row, layer << 20 | column group, base_lo,
+// base_hi), key = seed; normal q of group g is the noise of column 4g + q.
+// Every kernel that draws noise (fused and layer-wise paths, training and NLL)
+// uses this one function, so both paths draw the identical stream.
+__device__ __forceinline__ float4 philox_normal4(uint64_t seed, uint64_t base, unsigned row, unsigned layer,
+                                                 unsigned grp) {
+  unsigned c0 = row, c1 = (layer << 20) | grp, c2 = (unsigned)base, c3 = (unsigned)(base >> 32);
+  unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const unsigned lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const unsigned lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  constexpr float k2m32 = 2.3283064365386963e-10f;
+  const float u0 = ((float)c0 + 0.5f) * k2m32, u1 = ((float)c1 + 0.5f) * k2m32;   // (0, 1]
+  const float u2 = ((float)c2 + 0.5f) * k2m32, u3 = ((float)c3 + 0.5f) * k2m32;
+  // sqrt(-2 ln u) = sqrt(-2 ln2 * log2 u); v_sin/v_cos take revolutions
+  const float r0 = __builtin_amdgcn_sqrtf(-1.38629436f * __builtin_amdgcn_logf(u0));
+  const float r1 = __builtin_amdgcn_sqrtf(-1.38629436f * __builtin_amdgcn_logf(u2));
+  return make_float4(r0 * __builtin_amdgcn_cosf(u1), r0 * __builtin_amdgcn_sinf(u1),
+                     r1 * __builtin_amdgcn_cosf(u3), r1 * __builtin_amdgcn_sinf(u3));
+}
+__device__ __forceinline__ float f4_at(const float4& v, int q) {
+  return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
+}
+
+// ------------------------------------------------- unconditional loads ----
+// Loads that may fall outside a tile are issued through a buffer resource with
+// a per-lane byte offset; an invalid lane gets offset kOOB, which the hardware
+// range check turns into a 0 -- no exec-masked branch around the load (hipcc
+// turns `cond ? load : 0` into a branch + vmcnt(0) wait per load, i.e. one
+// dependent memory round trip per element).  The base must be wave-uniform
+// (made provable with readfirstlane); valid offsets stay below 2 GiB.
+constexpr unsigned kOOB = 0x7FFFFFF0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes = kOOB) {
+  const uint64_t a = (uint64_t)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const uint64_t u = ((uint64_t)hi << 32) | lo;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)u, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ float bld1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+
+// TFP Normal(loc, s).log_prob(h) = -0.5 (h/s - loc/s)^2 - (0.5 log 2pi + log s)
+__device__ __forceinline__ float normal_logp(float h, float mu, float sc) {
+  const float rs = frcp(sc);
+  const float z = h * rs - mu * rs;
+  return -0.5f * (z * z) - (kHalfLog2Pi + flog(sc));
+}
+
 // ---------------------------------------------------------------- GEMM ----
 enum GemmKind { GEMM_FWD = 0, GEMM_BWD_DATA = 1, GEMM_BWD_WEIGHT = 2 };
 enum GemmEpi { EPI_STORE = 0, EPI_TANH = 1, EPI_BERN = 2, EPI_TANH_GRAD = 3 };
@@ -109,6 +188,7 @@ struct BoundArgs {
   const float* loss_add;                // optional device scalar (VAE_V1 KL) ...
   float loss_add_coef;                  // ... added as loss_add_coef * (*loss_add)
   unsigned* ticket; uint64_t* rng_base; // last-block bookkeeping
+  long long* adam_step;                 // train step with Adam: advance the step counter (or null)
 };
 hipError_t launch_bound(hipStream_t st, const BoundArgs& a);
 
@@ -135,7 +215,7 @@ struct AdamSeg {
 struct AdamState {         // device resident (graph-replay safe)
   float lr, b1, b2, eps;
   float grad_scale; int pad0;
-  long long t;             // Adam iterations applied so far
+  long long t;             // Adam steps, advanced BEFORE the step's Adam launch reads it
 };
 constexpr int kMaxSegs = 64;
 struct AdamArgs {
@@ -144,6 +224,7 @@ struct AdamArgs {
   int write_grad, do_adam, read_slabs;
   AdamState* state; unsigned* ticket;
   float grad_scale_override;   // >0: use this instead of state->grad_scale
+  int tick;                    // advance state->t in a tick kernel first (else the bound kernel did)
 };
 hipError_t launch_adam(hipStream_t st, const AdamArgs& a, long long max_seg_n);
 

@@ -120,6 +120,7 @@ struct iwae_handle {
   bool use_graphs = false;
   std::map<std::vector<long long>, hipGraphExec_t> graphs;
   // live kernel timing (HIP events around every launch of one GEMM class)
+  float* loss_out = nullptr;           // train-step loss destination (part of the graph key)
   int prof_kind = -1, prof_epi = -1;
   std::vector<hipEvent_t> prof_ev;
   size_t prof_used = 0;
@@ -530,7 +531,8 @@ static int forward_core(iwae_handle* h, const Plan& P, const EpsSet& E, bool tra
   return IWAE_OK;
 }
 
-static int run_bound(iwae_handle* h, const Plan& P, bool train, float sign, float* value_out) {
+static int run_bound(iwae_handle* h, const Plan& P, bool train, float sign, float* value_out,
+                     bool adam_tick = false) {
   if (P.kl) {
     const int Lm1 = h->L - 1;
     const int rows = Lm1 == 0 ? P.Bimg : P.Bimg * P.kS;
@@ -555,6 +557,7 @@ static int run_bound(iwae_handle* h, const Plan& P, bool train, float sign, floa
     b.loss_add_coef = sign > 0 ? -1.f : 1.f;
   }
   b.ticket = &h->ds->tickets[0]; b.rng_base = &h->ds->rng[0];
+  b.adam_step = adam_tick ? &h->ds->adam.t : nullptr;
   HIPCHK(launch_bound(h->stream, b));
   return IWAE_OK;
 }
@@ -617,7 +620,8 @@ static int encoder_bwd(iwae_handle* h, const Plan& P, const float* dlw) {
   return IWAE_OK;
 }
 
-static int run_adam(iwae_handle* h, bool read_slabs, bool write_grad, bool do_adam, float scale_override) {
+static int run_adam(iwae_handle* h, bool read_slabs, bool write_grad, bool do_adam, float scale_override,
+                    bool tick) {
   AdamArgs a{};
   a.param = h->params; a.m = h->adam_m; a.v = h->adam_v; a.grad = h->grad; a.slabs = h->slabs;
   long long mx = 0;
@@ -631,6 +635,7 @@ static int run_adam(iwae_handle* h, bool read_slabs, bool write_grad, bool do_ad
   a.write_grad = write_grad; a.do_adam = do_adam; a.read_slabs = read_slabs;
   a.state = &h->ds->adam; a.ticket = &h->ds->tickets[2];
   a.grad_scale_override = scale_override;
+  a.tick = tick;
   HIPCHK(launch_adam(h->stream, a, mx));
   return IWAE_OK;
 }
@@ -957,9 +962,11 @@ static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const
   return IWAE_OK;
 }
 
+static float* train_loss_ptr(iwae_handle* h) { return h->loss_out ? h->loss_out : &h->ds->scalars[0]; }
+
 static int fused_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
   CHK(fused_forward(h, P, E, true));
-  CHK(run_bound(h, P, true, -1.f, &h->ds->scalars[0]));
+  CHK(run_bound(h, P, true, -1.f, train_loss_ptr(h), adam));
   if (P.piwae) {
     CHK(fused_decoder_bwd(h, P, h->dlw, h->dpx, false));      // decoder weights: IWAE_{k1 k2}
     CHK(weight_grads(h, P, false, true, h->dpx));
@@ -971,7 +978,7 @@ static int fused_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool
     CHK(fused_encoder_bwd(h, P, h->dlw));
     CHK(weight_grads(h, P, true, true, h->dpx));
   }
-  CHK(run_adam(h, true, true, adam, 1.f));
+  CHK(run_adam(h, true, true, adam, 1.f, false));
   return IWAE_OK;
 }
 
@@ -979,7 +986,7 @@ static int fused_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool
 static int train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
   if (use_fused(h, P)) return fused_train_body(h, P, E, adam);
   CHK(forward_core(h, P, E, true));
-  CHK(run_bound(h, P, true, -1.f, &h->ds->scalars[0]));
+  CHK(run_bound(h, P, true, -1.f, train_loss_ptr(h), adam));
   if (P.piwae) {
     CHK(decoder_bwd(h, P, h->dlw, h->dpx, true, false));      // decoder: IWAE_{k1 k2}
     CHK(decoder_bwd(h, P, h->dlw2, h->dpx2, false, true));    // encoder path: MIWAE(k1,k2)
@@ -988,7 +995,7 @@ static int train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam)
     CHK(decoder_bwd(h, P, h->dlw, h->dpx, true, true));
     CHK(encoder_bwd(h, P, h->dlw));
   }
-  CHK(run_adam(h, true, true, adam, 1.f));
+  CHK(run_adam(h, true, true, adam, 1.f, false));
   return IWAE_OK;
 }
 
@@ -1002,8 +1009,9 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
   CHK(ensure_capacity(h, P.Bimg, P.Bimg * P.kS, true));
   CHK(copy_x(h, P, x));
   const bool philox = (E.a[0] == nullptr);
+  h->loss_out = loss_dev;
   if (h->use_graphs && philox && h->prof_kind < 0) {
-    std::vector<long long> key = {adam ? 1 : 0, lc->loss, B, lc->k, lc->k1, lc->k2};
+    std::vector<long long> key = {adam ? 1 : 0, lc->loss, B, lc->k, lc->k1, lc->k2, (long long)(uintptr_t)loss_dev};
     float fk[3] = {lc->p, lc->alpha, lc->beta};
     for (float f : fk) {
       int bits;
@@ -1027,8 +1035,6 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
   } else {
     CHK(train_body(h, P, E, adam));
   }
-  if (loss_dev)
-    HIPCHK(hipMemcpyAsync(loss_dev, &h->ds->scalars[0], sizeof(float), hipMemcpyDeviceToDevice, h->stream));
   return IWAE_OK;
 }
 
@@ -1303,7 +1309,7 @@ int iwae_bind_grad_buffer(iwae_handle* h, float* g, long long n) {
 int iwae_apply_adam(iwae_handle* h, float grad_scale) {
   if (!h) return IWAE_EINVAL;
   if (!(grad_scale > 0.f)) return fail(h, IWAE_EINVAL, "grad_scale must be > 0");
-  return run_adam(h, false, false, true, grad_scale);
+  return run_adam(h, false, false, true, grad_scale, true);
 }
 
 static int eval_forward(iwae_handle* h, const Plan& P, const float* x, const float* const* eps, int n_eps,
