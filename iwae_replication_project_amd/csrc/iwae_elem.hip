@@ -368,12 +368,13 @@ __device__ __forceinline__ void image_grad(const BoundArgs& a, int mode, int row
   }
 }
 
-constexpr int kBoundWaves = 8;
+constexpr int kBoundWaves = 16;
 
 __global__ __launch_bounds__(kBoundWaves * 64) void bound_kernel(BoundArgs a) {
   __shared__ float sh_all[kBoundWaves][1024];
   __shared__ float red[kBoundWaves];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float wsum = 0.f;                       // this wave's images (single-workgroup finalize)
   for (int b = blockIdx.x * kBoundWaves + wave; b < a.Bimg; b += gridDim.x * kBoundWaves) {
     const bool ga = b < a.Bsplit;
     const int mode = ga ? a.mode_a : a.mode_b;
@@ -402,6 +403,7 @@ __global__ __launch_bounds__(kBoundWaves * 64) void bound_kernel(BoundArgs a) {
       float c = w * ib.val / (float)Bg;
       if (a.part2) c += a.bce_w * (bsum / (float)a.kS) / (float)Bg;
       a.contrib[b] = c;
+      wsum += c;
     }
     if (a.dlw) {
       // loss = -objective: dL/dlw = -(w/Bg) * dBound/dlw
@@ -422,17 +424,21 @@ __global__ __launch_bounds__(kBoundWaves * 64) void bound_kernel(BoundArgs a) {
   }
   bool finalize;
   if (gridDim.x == 1) {
-    __syncthreads();       // one workgroup: its own contrib writes are visible after the barrier
+    // one workgroup: per-wave sums in a fixed order, no global round trip
+    if (lane == 0) red[wave] = wsum;
+    __syncthreads();
     finalize = true;
   } else {
     finalize = a.ticket && last_block_arrive(a.ticket);
+    if (finalize) {
+      float s = 0.f;
+      for (int i = threadIdx.x; i < a.Bimg; i += blockDim.x) s += a.contrib[i];
+      s = wave_sum(s);
+      if (lane == 0) red[wave] = s;
+      __syncthreads();
+    }
   }
   if (finalize) {
-    float s = 0.f;
-    for (int i = threadIdx.x; i < a.Bimg; i += blockDim.x) s += a.contrib[i];
-    s = wave_sum(s);
-    if (lane == 0) red[wave] = s;
-    __syncthreads();
     if (threadIdx.x == 0) {
       float tot = 0.f;
       for (int i = 0; i < kBoundWaves; ++i) tot += red[i];

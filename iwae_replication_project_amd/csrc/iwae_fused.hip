@@ -468,7 +468,27 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_bwd_kernel(RbBwdLaunch L) {
   const int K0p = rb_k_pad(K0, true);
   const int D = bo[0];
   if (J.pro == 0) {
-    rb_load(D, lda, J.dz_in, J.ld_dz_in, K0, K0p, row0, nrows);
+    if (J.dz_nslab <= 1) {
+      rb_load(D, lda, J.dz_in, J.ld_dz_in, K0, K0p, row0, nrows);
+    } else {
+      // split-K slabs of the producing GEMM (epilogue already applied per slab):
+      // every slab value of this thread's elements is requested before any is summed
+      const __amdgpu_buffer_rsrc_t rs = buf_rsrc(J.dz_in + (size_t)row0 * J.ld_dz_in);
+      for (int e = threadIdx.x; e < RB_ROWS * K0p; e += blockDim.x) {
+        const int rr = e / K0p, c = e - rr * K0p;
+        const bool ok = rr < nrows && c < K0;
+        const unsigned o0 = (unsigned)(rr * J.ld_dz_in + c);
+        float part[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          part[q] = bld1(rs, (ok && q < J.dz_nslab) ? (o0 + (unsigned)(q * J.dz_stride)) * 4u : kOOB);
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc += part[q];
+        rbs[D + rr * lda + c] = acc;
+        if (ok && J.dz_out) J.dz_out[(size_t)(row0 + rr) * J.ld_dz_in + c] = acc;
+      }
+    }
   } else if (J.pro == 1 || J.pro == 2) {
     // per row: dP of an encoder sampling layer (pro 1) or a decoder prior head (pro 2).
     // Thread t: row t/32, column quad t%32; all of its loads are issued first.

@@ -33,7 +33,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KSCALE>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const int by, const int bz) {
   constexpr int NTH = WM * WN * 64;
-  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = (TM == 1 && TN == 1) ? 32 : 16;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = (TM == 1 && TN == 1) ? 64 : 16;
   // k-major LDS images.  Transposed (scalar) writes want a row stride = 2 mod 32
   // floats (conflict-free, see header); float4 writes want a multiple of 4.
   constexpr int LDSA = BM + (TA ? 4 : 2);

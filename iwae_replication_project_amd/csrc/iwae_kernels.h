@@ -109,7 +109,7 @@ struct GemmArgs {
   const float* A; const float* B; float* C;
   int lda, ldb, ldc;
   int M, N, K;
-  int kchunk;                 // K range per blockIdx.z (multiple of 16)
+  int kchunk;                 // K range per blockIdx.z (multiple of 64)
   long long c_split_stride;   // C offset per blockIdx.z (split-K slabs)
   const float* aux; int ldaux;  // TANH_GRAD: Y (tanh output); BERN: x_in
   const float* rowscale;      // STORE/TANH_GRAD: C[m][:] *= rowscale[m]
@@ -278,7 +278,9 @@ struct RbFwdLaunch {
 struct RbBwdJob {
   int rows, rpb;
   int pro;                   // 0 load dZ; 1 encoder sampling bwd; 2 decoder prior bwd; 3 encoder layer 0 (per image)
-  const float* dz_in; int ld_dz_in;
+  const float* dz_in; int ld_dz_in;          // pro 0: dZ = sum of dz_nslab slabs dz_stride floats apart
+  int dz_nslab; long long dz_stride;
+  float* dz_out;                                 // slab mode: the summed dZ is also stored here (weight grads)
   const float* P; int ldP; int d;
   const float* H; int ldH; const float* eps; int ld_eps; const float* dlw;
   const float* src[4]; int ldsrc[4]; int nsrc;

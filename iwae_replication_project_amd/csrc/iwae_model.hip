@@ -115,6 +115,8 @@ struct iwae_handle {
   float* slabs = nullptr;
   float* fslab = nullptr;            // split-K partials of the first encoder layer (fused path)
   int fslab_S = 0;
+  float* oslab = nullptr;            // split-K slabs of the output layer's dX (fused path)
+  int oslab_S = 0;
   int path = 0;                      // 0 auto, 1 layer-wise kernels, 2 fused row-block kernels
   // graphs
   bool use_graphs = false;
@@ -259,6 +261,12 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
   vec(h->contrib, Bimg); vec(h->run_m, Bimg); vec(h->run_s, Bimg);
   h->fslab_S = (int)std::min<long long>(16, cdiv(h->xdim + 1, 64));
   vec(h->fslab, (size_t)h->fslab_S * Bimg * r4(h->enc[0].H + 1));
+  if (train && rows <= 65536) {
+    h->oslab_S = 4;
+    vec(h->oslab, (size_t)h->oslab_S * rows * r4(Hd));
+  } else {
+    h->oslab_S = 0;
+  }
   size_t slab_total = 0;
   if (train) {
     for (auto& d : h->dense) {
@@ -373,7 +381,7 @@ static int gemm_bwd_weight(iwae_handle* h, const Mat& X, const Mat& dZ, int rows
   a.C = h->slabs + d.slab_off; a.ldc = d.ldw;
   a.M = d.fin + 1; a.N = d.fout; a.K = rows;
   long long S = std::min<long long>(d.max_splits, std::max(1LL, cdiv(rows, 64)));
-  int kchunk = (int)(cdiv(cdiv(rows, S), 16) * 16);
+  int kchunk = (int)(cdiv(cdiv(rows, S), 64) * 64);
   S = cdiv(rows, kchunk);
   d.splits = (int)S;
   a.kchunk = kchunk;
@@ -720,7 +728,7 @@ static int fused_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool tr
     a.B = h->params + d.off; a.ldb = d.ldw;
     a.C = h->fslab; a.ldc = h->eb[0].y1.ld;
     a.M = P.Bimg; a.N = d.fout; a.K = d.fin + 1;
-    a.kchunk = (int)(cdiv(cdiv(a.K, h->fslab_S), 16) * 16);
+    a.kchunk = (int)(cdiv(cdiv(a.K, h->fslab_S), 64) * 64);
     const int S = (int)cdiv(a.K, a.kchunk);
     a.c_split_stride = (long long)P.Bimg * a.ldc;
     CHK(prof_begin(h, GEMM_FWD, EPI_STORE, 2.0 * P.Bimg * d.fout * d.fin));
@@ -845,14 +853,45 @@ static int fused_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool tr
 static int fused_decoder_bwd(iwae_handle* h, const Plan& P, const float* dlw, const float* dpx, bool need_dh) {
   const int L = h->L, M = P.Bimg * P.kS;
   if (L > kRbMaxJobs) return fail(h, IWAE_EINVAL, "fused path supports up to 4 stochastic layers");
-  CHK(gemm_bwd_data(h, h->ob.P, M, h->dense[h->o3], h->ob.dY2, &h->ob.y2, dpx));
+  // output layer dX = (dpx * g) W3^T (1 - y2^2), split over K = 784 into slabs
+  // that the row-block prologue sums (the epilogue is linear: applied per slab)
+  int oS = 1;
+  {
+    const DenseL& d = h->dense[h->o3];
+    GemmArgs a{};
+    a.A = h->ob.P.p; a.lda = h->ob.P.ld;
+    a.B = h->params + d.off; a.ldb = d.ldw;
+    a.M = M; a.N = d.fin; a.K = d.fout;
+    a.rowscale = dpx; a.aux = h->ob.y2.p; a.ldaux = h->ob.y2.ld;
+    const long long tiles = cdiv(M, 64) * cdiv(d.fin, 64);
+    if (h->oslab && h->oslab_S > 1 && tiles < 256) {
+      oS = (int)std::min<long long>(h->oslab_S, cdiv(256, tiles));
+      a.kchunk = (int)(cdiv(cdiv(a.K, oS), 64) * 64);
+      oS = (int)cdiv(a.K, a.kchunk);
+    }
+    if (oS > 1) {
+      a.C = h->oslab; a.ldc = h->ob.dY2.ld;
+      a.c_split_stride = (long long)M * a.ldc;
+    } else {
+      a.kchunk = a.K;
+      a.C = h->ob.dY2.p; a.ldc = h->ob.dY2.ld;
+    }
+    CHK(prof_begin(h, GEMM_BWD_DATA, EPI_TANH_GRAD, 2.0 * M * d.fout * d.fin));
+    HIPCHK(launch_gemm(h->stream, GEMM_BWD_DATA, EPI_TANH_GRAD, 0, oS, false, a));
+    CHK(prof_end(h, GEMM_BWD_DATA, EPI_TANH_GRAD));
+  }
   RbBwdLaunch Lb{};
   Lb.ld_lds = rb_ld(h, true);
   int nj = 0;
   {
     RbBwdJob& J = Lb.job[nj++];
     J.rows = M; J.rpb = 16; J.pro = 0;
-    J.dz_in = h->ob.dY2.p; J.ld_dz_in = h->ob.dY2.ld;
+    if (oS > 1) {
+      J.dz_in = h->oslab; J.ld_dz_in = h->ob.dY2.ld; J.dz_nslab = oS; J.dz_stride = (long long)M * h->ob.dY2.ld;
+      J.dz_out = h->ob.dY2.p;
+    } else {
+      J.dz_in = h->ob.dY2.p; J.ld_dz_in = h->ob.dY2.ld; J.dz_nslab = 1;
+    }
     J.nst = need_dh ? 2 : 1;
     J.st[0] = rb_bwd_stage(h, h->o2, &h->ob.y1, &h->ob.dY1);
     if (need_dh) J.st[1] = rb_bwd_stage(h, h->o1, nullptr, &h->dh_out[0]);
@@ -948,7 +987,7 @@ static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const
       a.C = h->slabs + d.slab_off; a.ldc = d.ldw;
       a.M = d.fin + 1; a.N = d.fout; a.K = w.rows;
       long long S = std::min<long long>(d.max_splits, std::max(1LL, cdiv(w.rows, 64)));
-      const int kchunk = (int)(cdiv(cdiv(w.rows, S), 16) * 16);
+      const int kchunk = (int)(cdiv(cdiv(w.rows, S), 64) * 64);
       S = cdiv(w.rows, kchunk);
       d.splits = (int)S;
       a.kchunk = kchunk;
