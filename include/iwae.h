@@ -95,6 +95,11 @@ int iwae_synchronize(iwae_handle* h);
 int iwae_set_seed(iwae_handle* h, unsigned long long seed);
 /* 1 = capture the Philox train step in a hipGraph per shape and replay it. */
 int iwae_set_graphs(iwae_handle* h, int enable);
+/* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --
+ * a.b = a_hi b_hi + a_hi b_lo + a_lo b_hi with hi = bf16(x), lo = bf16(x - hi),
+ * f32 accumulate on v_mfma_f32_32x32x16_bf16 (~2^-16 relative per product,
+ * 5.3x the f32-MFMA rate); 0 exact f32 on v_mfma_f32_32x32x2_f32. */
+int iwae_set_precision(iwae_handle* h, int mode);
 /* Kernel path: 0 auto (fused row-block kernels up to 65536 sample rows, then
  * layer-wise GEMMs), 1 layer-wise only, 2 fused whenever the widths allow. */
 int iwae_set_path(iwae_handle* h, int path);

@@ -53,6 +53,7 @@ SIGNATURES = {
     "iwae_set_seed": (c_int, [H, c_ulonglong]),
     "iwae_set_graphs": (c_int, [H, c_int]),
     "iwae_set_path": (c_int, [H, c_int]),
+    "iwae_set_precision": (c_int, [H, c_int]),
     "iwae_num_params": (c_longlong, [H]),
     "iwae_set_params": (c_int, [H, FP, c_longlong]),
     "iwae_get_params": (c_int, [H, FP, c_longlong]),

@@ -589,6 +589,22 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
       *reinterpret_cast<float4*>(a.m + pidx) = make_float4(mm[0], mm[1], mm[2], mm[3]);
       *reinterpret_cast<float4*>(a.v + pidx) = make_float4(vv[0], vv[1], vv[2], vv[3]);
       *reinterpret_cast<float4*>(a.param + pidx) = make_float4(pp[0], pp[1], pp[2], pp[3]);
+      if (a.whi) {
+        // refresh the split copies of these 4 weights (row r, columns c..c+3 of W_aug)
+        const int r = (int)((4 * i) / sg.ldw), c = (int)(4 * i - (long long)r * sg.ldw);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (c + q >= sg.fout) break;
+          const __bf16 hb = (__bf16)pp[q];
+          const __bf16 lb = (__bf16)(pp[q] - (float)hb);
+          const long long fi = sg.f_off + (long long)(c + q) * sg.ldF + r;
+          a.whi[fi] = hb; a.wlo[fi] = lb;
+          if (r < sg.fin) {
+            const long long gi = sg.g_off + (long long)r * sg.ldG + c + q;
+            a.whi[gi] = hb; a.wlo[gi] = lb;
+          }
+        }
+      }
     }
   }
 }
@@ -602,6 +618,35 @@ hipError_t launch_adam(hipStream_t st, const AdamArgs& a, long long max_seg_n) {
   if (bx > 64) bx = 64;
   if (bx < 1) bx = 1;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)bx, a.nseg), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------ split weights
+__global__ __launch_bounds__(256) void wsplit_kernel(WSplitArgs a) {
+  const WSplitSeg sg = a.seg[blockIdx.y];
+  const long long n = (long long)(sg.fin + 1) * sg.fout;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int i = (int)(e / sg.fout), j = (int)(e - (long long)i * sg.fout);
+    const float w = a.param[sg.off + (long long)i * sg.ldw + j];
+    const __bf16 h = (__bf16)w;
+    const __bf16 l = (__bf16)(w - (float)h);
+    const long long fi = sg.f_off + (long long)j * sg.ldF + i;
+    a.hi[fi] = h;
+    a.lo[fi] = l;
+    if (i < sg.fin) {
+      const long long gi = sg.g_off + (long long)i * sg.ldG + j;
+      a.hi[gi] = h;
+      a.lo[gi] = l;
+    }
+  }
+}
+
+hipError_t launch_wsplit(hipStream_t st, const WSplitArgs& a, long long max_seg_elems) {
+  if (a.nseg <= 0) return hipSuccess;
+  long long bx = (max_seg_elems + 255) / 256;
+  if (bx > 128) bx = 128;
+  if (bx < 1) bx = 1;
+  hipLaunchKernelGGL(wsplit_kernel, dim3((unsigned)bx, a.nseg), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

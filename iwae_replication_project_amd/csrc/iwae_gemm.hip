@@ -30,10 +30,25 @@ namespace iwae {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KSCALE>
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// f32 -> (hi, lo) bf16 pair of 4 values
+__device__ __forceinline__ void split4(const float4& v, bf16x4& hi, bf16x4& lo) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const __bf16 h = (__bf16)x[j];
+    hi[j] = h;
+    lo[j] = (__bf16)(x[j] - (float)h);
+  }
+}
+
+template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KSCALE, bool X3>
 __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const int by, const int bz) {
   constexpr int NTH = WM * WN * 64;
-  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = (TM == 1 && TN == 1) ? 64 : 16;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int BK = X3 ? 32 : ((TM == 1 && TN == 1) ? 64 : 16);
   // k-major LDS images.  Transposed (scalar) writes want a row stride = 2 mod 32
   // floats (conflict-free, see header); float4 writes want a multiple of 4.
   constexpr int LDSA = BM + (TA ? 4 : 2);
@@ -42,8 +57,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
   constexpr int B_F4 = (BN * BK / 4) / NTH;
   static_assert(A_F4 * NTH * 4 == BM * BK, "A tile must split evenly");
   static_assert(B_F4 * NTH * 4 == BN * BK, "B tile must split evenly");
-  constexpr int SMEM = 2 * BK * LDSA + 2 * BK * LDSB;
-  static_assert(SMEM >= WM * WN * 32 * 33, "epilogue scratch must fit");
+  // bf16x3 images: [buf][hi, lo][A rows (BM) | B rows (BN)][LDK] bf16, k contiguous
+  constexpr int LDK = BK + 8;
+  constexpr int SMEM_F32 = 2 * BK * LDSA + 2 * BK * LDSB;
+  constexpr int SMEM_X3 = 2 * 2 * (BM + BN) * LDK / 2;
+  constexpr int SMEM0 = X3 ? SMEM_X3 : SMEM_F32;
+  constexpr int SMEM = SMEM0 > WM * WN * 32 * 33 ? SMEM0 : WM * WN * 32 * 33;
   __shared__ __attribute__((aligned(16))) float smem[SMEM];
   float* As = smem;
   float* Bs = smem + 2 * BK * LDSA;
@@ -56,6 +75,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
   const int M = a.M, N = a.N;
 
   float4 ra[A_F4], rb[B_F4];
+  // x3 with pre-split B (the weights' F / G copies): [n][ldbx] bf16 rows copied as is
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int B_X = X3 ? (BN * BK * 2 / 16) / NTH : 1;     // 16-byte chunks per thread (hi; lo alike)
+  static_assert(!X3 || B_X * NTH * 16 == BN * BK * 2, "pre-split B tile must split evenly");
+  u32x4 rbh[B_X], rbl[B_X];
+  const bool preB = X3 && a.Bhi != nullptr;
   // block-relative buffer bases (uniform); out-of-tile lanes read 0 via kOOB
   const __amdgpu_buffer_rsrc_t rsA =
       buf_rsrc(TA ? a.A + (size_t)kbeg * a.lda + m0 : a.A + (size_t)m0 * a.lda + kbeg);
@@ -63,7 +88,20 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
       buf_rsrc(TB ? a.B + (size_t)n0 * a.ldb + kbeg : a.B + (size_t)kbeg * a.ldb + n0);
   const int klen = kend - kbeg;
 
+  const __amdgpu_buffer_rsrc_t rsBh = buf_rsrc(preB ? a.Bhi + (size_t)n0 * a.ldbx + kbeg : nullptr);
+  const __amdgpu_buffer_rsrc_t rsBl = buf_rsrc(preB ? a.Blo + (size_t)n0 * a.ldbx + kbeg : nullptr);
   auto gload = [&](int k0) {      // k0 relative to kbeg
+    if (preB) {
+#pragma unroll
+      for (int i = 0; i < B_X; ++i) {
+        const int c = tid + i * NTH;
+        const int nr = c / (BK / 8), kq = c % (BK / 8);
+        const int gk = k0 + 8 * kq;
+        const unsigned off = (n0 + nr < N && gk < klen) ? (unsigned)(nr * a.ldbx + gk) * 2u : kOOB;
+        rbh[i] = __builtin_amdgcn_raw_buffer_load_b128(rsBh, off, 0, 0);
+        rbl[i] = __builtin_amdgcn_raw_buffer_load_b128(rsBl, off, 0, 0);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < A_F4; ++i) {
       const int f = tid + i * NTH;
@@ -73,7 +111,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
         const int gk = k0 + 4 * kq;
         off = (m0 + mr < M && gk < klen) ? (unsigned)(mr * a.lda + gk) * 4u : kOOB;
       } else {
-        const int kr = f / (BM / 4), mq = f % (BM / 4);
+        // x3 walks k across lanes (its LDS image is [m][k]: conflict-free 2-byte writes)
+        const int kr = X3 ? f % BK : f / (BM / 4), mq = X3 ? f / BK : f % (BM / 4);
         const int gk = k0 + kr;
         off = (gk < klen && m0 + 4 * mq < M) ? (unsigned)(gk * a.lda + 4 * mq) * 4u : kOOB;
       }
@@ -81,9 +120,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
     }
 #pragma unroll
     for (int i = 0; i < B_F4; ++i) {
+      if (preB) break;
       const int f = tid + i * NTH;
       if (!TB) {
-        const int kr = f / (BN / 4), nq = f % (BN / 4);
+        const int kr = X3 ? f % BK : f / (BN / 4), nq = X3 ? f / BK : f % (BN / 4);
         const int gk = k0 + kr;
         const bool ok = gk < klen && n0 + 4 * nq < N;
         float4 v = bld4(rsB, ok ? (unsigned)(gk * a.ldb + 4 * nq) * 4u : kOOB);
@@ -100,7 +140,62 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
     }
   };
 
+  __bf16* const XL = reinterpret_cast<__bf16*>(smem);
+  auto ximg = [&](int buf, int lohi) { return XL + (size_t)((buf * 2 + lohi) * (BM + BN)) * LDK; };
+  // bf16x3: split while writing, A row m / B row n hold k contiguous
+  auto xstore = [&](int buf) {
+    __bf16* Hh = ximg(buf, 0);
+    __bf16* Hl = ximg(buf, 1);
+#pragma unroll
+    for (int i = 0; i < A_F4; ++i) {
+      const int f = tid + i * NTH;
+      bf16x4 hi, lo;
+      split4(ra[i], hi, lo);
+      if (!TA) {
+        const int mr = f / (BK / 4), kq = f % (BK / 4);
+        *reinterpret_cast<bf16x4*>(Hh + mr * LDK + 4 * kq) = hi;
+        *reinterpret_cast<bf16x4*>(Hl + mr * LDK + 4 * kq) = lo;
+      } else {
+        const int kr = f % BK, mq = f / BK;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          Hh[(4 * mq + c) * LDK + kr] = hi[c];
+          Hl[(4 * mq + c) * LDK + kr] = lo[c];
+        }
+      }
+    }
+    if (preB) {
+#pragma unroll
+      for (int i = 0; i < B_X; ++i) {
+        const int c = tid + i * NTH;
+        const int nr = c / (BK / 8), kq = c % (BK / 8);
+        *reinterpret_cast<u32x4*>(Hh + (BM + nr) * LDK + 8 * kq) = rbh[i];
+        *reinterpret_cast<u32x4*>(Hl + (BM + nr) * LDK + 8 * kq) = rbl[i];
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < B_F4; ++i) {
+      const int f = tid + i * NTH;
+      bf16x4 hi, lo;
+      split4(rb[i], hi, lo);
+      if (!TB) {
+        const int kr = f % BK, nq = f / BK;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          Hh[(BM + 4 * nq + c) * LDK + kr] = hi[c];
+          Hl[(BM + 4 * nq + c) * LDK + kr] = lo[c];
+        }
+      } else {
+        const int nr = f / (BK / 4), kq = f % (BK / 4);
+        *reinterpret_cast<bf16x4*>(Hh + (BM + nr) * LDK + 4 * kq) = hi;
+        *reinterpret_cast<bf16x4*>(Hl + (BM + nr) * LDK + 4 * kq) = lo;
+      }
+    }
+  };
+
   auto sstore = [&](int buf) {
+    if constexpr (X3) { xstore(buf); return; }
     float* Ab = As + buf * BK * LDSA;
     float* Bb = Bs + buf * BK * LDSB;
 #pragma unroll
@@ -153,6 +248,39 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
   for (int t = 0; t < nk; ++t) {
     const int cur = t & 1;
     if (t + 1 < nk) gload((t + 1) * BK);
+    if constexpr (X3) {
+      // bf16x3 on v_mfma_f32_32x32x16_bf16: lane l holds row l&31, k = 8(l>>5)..+7
+      const __bf16* Hh = ximg(cur, 0);
+      const __bf16* Hl = ximg(cur, 1);
+      const int fr = lane & 31, fk = 8 * (lane >> 5);
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wm * TM * 32 + i * 32 + fr;
+          ah[i] = *reinterpret_cast<const bf16x8*>(Hh + row * LDK + ks * 16 + fk);
+          al[i] = *reinterpret_cast<const bf16x8*>(Hl + row * LDK + ks * 16 + fk);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int row = BM + wn * TN * 32 + j * 32 + fr;
+          bh[j] = *reinterpret_cast<const bf16x8*>(Hh + row * LDK + ks * 16 + fk);
+          bl[j] = *reinterpret_cast<const bf16x8*>(Hl + row * LDK + ks * 16 + fk);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          }
+      }
+      if (t + 1 < nk) sstore(cur ^ 1);
+      __syncthreads();
+      continue;
+    }
     const float* Ab = As + cur * BK * LDSA;
     const float* Bb = Bs + cur * BK * LDSB;
 #pragma unroll
@@ -311,21 +439,21 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
   }
 }
 
-template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KSCALE>
+template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KSCALE, bool X3>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs a) {
-  gemm_body<WM, WN, TM, TN, TA, TB, EPI, KSCALE>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+  gemm_body<WM, WN, TM, TN, TA, TB, EPI, KSCALE, X3>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // Several independent GEMMs of one kind in ONE launch (the weight gradients of
 // every Dense layer): workgroup b runs tile (b - start[i]) of GEMM i.
-template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KSCALE>
+template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KSCALE, bool X3>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_group_kernel(GemmGroup gg) {
   const int b = blockIdx.x;
   int i = 0;
   while (i + 1 < gg.n && b >= gg.start[i + 1]) ++i;
   const int local = b - gg.start[i];
   const int tx = gg.tiles_x[i], ty = gg.tiles_y[i];
-  gemm_body<WM, WN, TM, TN, TA, TB, EPI, KSCALE>(gg.g[i], local % tx, (local / tx) % ty, local / (tx * ty));
+  gemm_body<WM, WN, TM, TN, TA, TB, EPI, KSCALE, X3>(gg.g[i], local % tx, (local / tx) % ty, local / (tx * ty));
 }
 
 hipError_t launch_gemm_group_bwd_weight(hipStream_t st, GemmGroup& gg) {
@@ -339,7 +467,10 @@ hipError_t launch_gemm_group_bwd_weight(hipStream_t st, GemmGroup& gg) {
     tot += gg.tiles_x[i] * gg.tiles_y[i] * gg.splits[i];
   }
   gg.start[gg.n] = tot;
-  hipLaunchKernelGGL((gemm_group_kernel<2, 2, 1, 1, true, false, EPI_STORE, true>), dim3(tot), dim3(256), 0, st, gg);
+  if (gg.g[0].x3)
+    hipLaunchKernelGGL((gemm_group_kernel<2, 2, 1, 1, true, false, EPI_STORE, true, true>), dim3(tot), dim3(256), 0, st, gg);
+  else
+    hipLaunchKernelGGL((gemm_group_kernel<2, 2, 1, 1, true, false, EPI_STORE, true, false>), dim3(tot), dim3(256), 0, st, gg);
   return hipGetLastError();
 }
 
@@ -347,8 +478,10 @@ template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KS>
 static hipError_t launch_t(hipStream_t st, int splits, const GemmArgs& a) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, splits);
-  hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, TA, TB, EPI, KS>), grid, dim3(WM * WN * 64), 0,
-                     st, a);
+  if (a.x3)
+    hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, TA, TB, EPI, KS, true>), grid, dim3(WM * WN * 64), 0, st, a);
+  else
+    hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, TA, TB, EPI, KS, false>), grid, dim3(WM * WN * 64), 0, st, a);
   return hipGetLastError();
 }
 

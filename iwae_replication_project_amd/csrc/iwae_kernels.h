@@ -119,6 +119,8 @@ struct GemmArgs {
   float wa, wb;               // BERN: g = (wa*dTFP + wb*dBCE) * dp/dlogit
   int store_g;                // BERN: write g into C
   int need_bce;               // BERN: write Keras-BCE partials into part2
+  int x3;                     // 1: bf16x3 products on v_mfma_f32_32x32x16_bf16 (else exact f32 MFMA)
+  const __bf16* Bhi; const __bf16* Blo; int ldbx;   // x3: pre-split B as [n][ldbx] (k contiguous), else null
 };
 
 // tile: 0 = 64x64 (4 waves), 1 = 128x128 (4 waves, 2x2 MFMA tiles each)
@@ -211,6 +213,9 @@ struct AdamSeg {
   long long off, n;        // parameter range in the flat internal buffer
   long long slab_off;      // offset of this segment's slabs in the slab arena
   int splits;              // number of slabs (0 = read grad buffer)
+  int fin, fout, ldw;      // the Dense layer (W_aug [fin+1][ldw])
+  long long f_off, g_off;  // its split copies F / G (see WSplitSeg)
+  int ldF, ldG;
 };
 struct AdamState {         // device resident (graph-replay safe)
   float lr, b1, b2, eps;
@@ -220,6 +225,7 @@ struct AdamState {         // device resident (graph-replay safe)
 constexpr int kMaxSegs = 64;
 struct AdamArgs {
   float* param; float* m; float* v; float* grad; const float* slabs;
+  __bf16* whi; __bf16* wlo;    // split weight copies refreshed with every update
   AdamSeg seg[kMaxSegs]; int nseg;
   int write_grad, do_adam, read_slabs;
   AdamState* state; unsigned* ticket;
@@ -227,6 +233,25 @@ struct AdamArgs {
   int tick;                    // advance state->t in a tick kernel first (else the bound kernel did)
 };
 hipError_t launch_adam(hipStream_t st, const AdamArgs& a, long long max_seg_n);
+
+// ------------------------------------------------------ split weights ----
+// bf16x3 products a.b ~ a_hi b_hi + a_hi b_lo + a_lo b_hi (hi = bf16(x),
+// lo = bf16(x - hi), f32 accumulate).  Every Dense layer keeps two split
+// copies of W_aug, both k-contiguous so an MFMA B operand row is a straight
+// copy into LDS (no transposition, no conversion):
+//   F [fout][ldF]  F[j][i] = W_aug[i][j]   forward   (k = fin+1 incl. the bias row)
+//   G [fin][ldG]   G[i][j] = W[i][j]       backward  (dX = dZ W^T, k = fout)
+// ldF / ldG are multiples of 32; the padding stays zero.  The Adam kernel
+// rewrites them with every update; wsplit_kernel after iwae_set_params.
+struct WSplitSeg {
+  long long off; int fin, fout, ldw;
+  long long f_off, g_off; int ldF, ldG;
+};
+struct WSplitArgs {
+  const float* param; __bf16* hi; __bf16* lo;
+  WSplitSeg seg[kMaxSegs]; int nseg;
+};
+hipError_t launch_wsplit(hipStream_t st, const WSplitArgs& a, long long max_seg_elems);
 
 // ------------------------------------------------- fused row-block kernels ----
 struct RbNoise {             // where a sampling layer's eps comes from (see eps_at)

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <map>
 #include <string>
 #include <tuple>
@@ -29,6 +30,8 @@ inline long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
 struct DenseL {
   int fin = 0, fout = 0, ldw = 0;
   long long off = 0;           // into the internal parameter buffer
+  long long f_off = 0, g_off = 0;  // split copies F [fout][ldF], G [fin][ldG] (bf16 hi / lo)
+  int ldF = 0, ldG = 0;
   long long size() const { return (long long)(fin + 1) * ldw; }
   int max_splits = 1, splits = 1;
   long long slab_off = 0;
@@ -97,6 +100,11 @@ struct iwae_handle {
   float* adam_v = nullptr;
   float* grad_own = nullptr;
   float* grad = nullptr;
+  __bf16* wsplit_hi = nullptr;       // split weight copies (WSplitSeg); lo = hi + wsplit_elems
+  __bf16* wsplit_lo = nullptr;
+  long long wsplit_elems = 0;
+  long long params_version = 1, wsplit_version = 0;   // split copies current iff equal
+  bool in_train_step = false;        // weight-operand GEMMs of a train step stay exact f32
   DevState* ds = nullptr;
   uint64_t seed = 0x5eed5eedULL;
   // workspace
@@ -118,6 +126,7 @@ struct iwae_handle {
   float* oslab = nullptr;            // split-K slabs of the output layer's dX (fused path)
   int oslab_S = 0;
   int path = 0;                      // 0 auto, 1 layer-wise kernels, 2 fused row-block kernels
+  int x3 = 1;                        // tiled GEMMs: 1 bf16x3 products (default), 0 exact f32 MFMA
   // graphs
   bool use_graphs = false;
   std::map<std::vector<long long>, hipGraphExec_t> graphs;
@@ -154,6 +163,13 @@ static int add_dense(iwae_handle* h, int fin, int fout, int rows_kind) {
   DenseL d;
   d.fin = fin; d.fout = fout; d.ldw = r4(fout); d.off = h->nparam_int; d.rows_kind = rows_kind;
   h->nparam_int += d.size();
+  d.ldF = (fin + 1 + 31) & ~31;
+  d.ldG = (fout + 31) & ~31;
+  d.f_off = h->wsplit_elems;
+  h->wsplit_elems += (long long)fout * d.ldF;
+  d.g_off = h->wsplit_elems;
+  h->wsplit_elems += (long long)fin * d.ldG;
+  h->wsplit_elems = (h->wsplit_elems + 63) & ~63LL;
   h->dense.push_back(d);
   return (int)h->dense.size() - 1;
 }
@@ -310,6 +326,9 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
 }
 
 // --------------------------------------------------------------- GEMMs
+// pre-split B operand (weights) for a bf16x3 GEMM: only outside the train step
+static bool use_split_b(const iwae_handle* h) { return h->x3 && !h->in_train_step; }
+
 static int choose_tile(long long M, long long N, int splits) {
   return (cdiv(M, 128) * cdiv(N, 128) * splits >= 512) ? 1 : 0;
 }
@@ -342,12 +361,14 @@ static int prof_end(iwae_handle* h, GemmKind kind, GemmEpi epi) {
 static int gemm_fwd(iwae_handle* h, GemmEpi epi, const Mat& X, int rows, const DenseL& d, Mat& Y,
                     GemmArgs extra = GemmArgs{}) {
   GemmArgs a = extra;
+  a.x3 = h->in_train_step ? 0 : h->x3;     // weight operand: exact f32 inside the train step
   a.A = X.p; a.lda = X.ld;
   a.B = h->params + d.off; a.ldb = d.ldw;
   a.C = Y.p; a.ldc = Y.ld;
   a.M = rows; a.N = d.fout; a.K = d.fin + 1;
   a.kchunk = a.K;
   a.c_split_stride = 0;
+  if (use_split_b(h)) { a.Bhi = h->wsplit_hi + d.f_off; a.Blo = h->wsplit_lo + d.f_off; a.ldbx = d.ldF; }
   CHK(prof_begin(h, GEMM_FWD, epi, 2.0 * rows * d.fout * d.fin));
   HIPCHK(launch_gemm(h->stream, GEMM_FWD, epi, choose_tile(a.M, a.N, 1), 1, false, a));
   CHK(prof_end(h, GEMM_FWD, epi));
@@ -358,12 +379,14 @@ static int gemm_fwd(iwae_handle* h, GemmEpi epi, const Mat& X, int rows, const D
 static int gemm_bwd_data(iwae_handle* h, const Mat& dZ, int rows, const DenseL& d, Mat& dX,
                          const Mat* Y, const float* rowscale) {
   GemmArgs a{};
+  a.x3 = h->in_train_step ? 0 : h->x3;     // weight operand: exact f32 inside the train step
   a.A = dZ.p; a.lda = dZ.ld;
   a.B = h->params + d.off; a.ldb = d.ldw;
   a.C = dX.p; a.ldc = dX.ld;
   a.M = rows; a.N = d.fin; a.K = d.fout;
   a.kchunk = a.K;
   a.rowscale = rowscale;
+  if (use_split_b(h)) { a.Bhi = h->wsplit_hi + d.g_off; a.Blo = h->wsplit_lo + d.g_off; a.ldbx = d.ldG; }
   GemmEpi epi = EPI_STORE;
   if (Y) { a.aux = Y->p; a.ldaux = Y->ld; epi = EPI_TANH_GRAD; }
   CHK(prof_begin(h, GEMM_BWD_DATA, epi, 2.0 * rows * d.fout * d.fin));
@@ -376,6 +399,7 @@ static int gemm_bwd_data(iwae_handle* h, const Mat& dZ, int rows, const DenseL& 
 static int gemm_bwd_weight(iwae_handle* h, const Mat& X, const Mat& dZ, int rows, DenseL& d,
                            const float* kscale) {
   GemmArgs a{};
+  a.x3 = h->x3;
   a.A = X.p; a.lda = X.ld;
   a.B = dZ.p; a.ldb = dZ.ld;
   a.C = h->slabs + d.slab_off; a.ldc = d.ldw;
@@ -628,15 +652,44 @@ static int encoder_bwd(iwae_handle* h, const Plan& P, const float* dlw) {
   return IWAE_OK;
 }
 
+// refresh the split (bf16 hi / lo) weight copies from the f32 parameters
+static int run_wsplit(iwae_handle* h) {
+  WSplitArgs a{};
+  a.param = h->params; a.hi = h->wsplit_hi; a.lo = h->wsplit_lo;
+  long long mx = 0;
+  for (size_t i = 0; i < h->dense.size(); ++i) {
+    const DenseL& d = h->dense[i];
+    WSplitSeg& g = a.seg[i];
+    g.off = d.off; g.fin = d.fin; g.fout = d.fout; g.ldw = d.ldw;
+    g.f_off = d.f_off; g.g_off = d.g_off; g.ldF = d.ldF; g.ldG = d.ldG;
+    mx = std::max(mx, (long long)(d.fin + 1) * d.fout);
+  }
+  a.nseg = (int)h->dense.size();
+  HIPCHK(launch_wsplit(h->stream, a, mx));
+  return IWAE_OK;
+}
+
+static int ensure_wsplit(iwae_handle* h) {
+  if (h->wsplit_version == h->params_version) return IWAE_OK;
+  CHK(run_wsplit(h));
+  h->wsplit_version = h->params_version;
+  return IWAE_OK;
+}
+
+
 static int run_adam(iwae_handle* h, bool read_slabs, bool write_grad, bool do_adam, float scale_override,
                     bool tick) {
   AdamArgs a{};
   a.param = h->params; a.m = h->adam_m; a.v = h->adam_v; a.grad = h->grad; a.slabs = h->slabs;
+  a.whi = nullptr; a.wlo = nullptr;          // split copies are refreshed lazily (ensure_wsplit)
+  if (do_adam) h->params_version++;
   long long mx = 0;
   for (size_t i = 0; i < h->dense.size(); ++i) {
     const DenseL& d = h->dense[i];
     a.seg[i].off = d.off; a.seg[i].n = d.size(); a.seg[i].slab_off = d.slab_off;
     a.seg[i].splits = read_slabs ? d.splits : 0;
+    a.seg[i].fin = d.fin; a.seg[i].fout = d.fout; a.seg[i].ldw = d.ldw;
+    a.seg[i].f_off = d.f_off; a.seg[i].g_off = d.g_off; a.seg[i].ldF = d.ldF; a.seg[i].ldG = d.ldG;
     mx = std::max(mx, d.size());
   }
   a.nseg = (int)h->dense.size();
@@ -724,10 +777,12 @@ static int fused_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool tr
   {
     const DenseL& d = h->dense[h->enc[0].l1];
     GemmArgs a{};
+    a.x3 = h->in_train_step ? 0 : h->x3;
     a.A = h->x_in.p; a.lda = h->x_in.ld;
     a.B = h->params + d.off; a.ldb = d.ldw;
     a.C = h->fslab; a.ldc = h->eb[0].y1.ld;
     a.M = P.Bimg; a.N = d.fout; a.K = d.fin + 1;
+    if (use_split_b(h)) { a.Bhi = h->wsplit_hi + d.f_off; a.Blo = h->wsplit_lo + d.f_off; a.ldbx = d.ldF; }
     a.kchunk = (int)(cdiv(cdiv(a.K, h->fslab_S), 64) * 64);
     const int S = (int)cdiv(a.K, a.kchunk);
     a.c_split_stride = (long long)P.Bimg * a.ldc;
@@ -859,10 +914,12 @@ static int fused_decoder_bwd(iwae_handle* h, const Plan& P, const float* dlw, co
   {
     const DenseL& d = h->dense[h->o3];
     GemmArgs a{};
+    a.x3 = h->in_train_step ? 0 : h->x3;
     a.A = h->ob.P.p; a.lda = h->ob.P.ld;
     a.B = h->params + d.off; a.ldb = d.ldw;
     a.M = M; a.N = d.fin; a.K = d.fout;
     a.rowscale = dpx; a.aux = h->ob.y2.p; a.ldaux = h->ob.y2.ld;
+    if (use_split_b(h)) { a.Bhi = h->wsplit_hi + d.g_off; a.Blo = h->wsplit_lo + d.g_off; a.ldbx = d.ldG; }
     const long long tiles = cdiv(M, 64) * cdiv(d.fin, 64);
     if (h->oslab && h->oslab_S > 1 && tiles < 256) {
       oS = (int)std::min<long long>(h->oslab_S, cdiv(256, tiles));
@@ -982,6 +1039,7 @@ static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const
       const WJ& w = js[q];
       DenseL& d = h->dense[w.di];
       GemmArgs& a = gg.g[gg.n];
+      a.x3 = h->x3;
       a.A = w.A->p; a.lda = w.A->ld;
       a.B = w.dZ->p; a.ldb = w.dZ->ld;
       a.C = h->slabs + d.slab_off; a.ldc = d.ldw;
@@ -1049,6 +1107,8 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
   CHK(copy_x(h, P, x));
   const bool philox = (E.a[0] == nullptr);
   h->loss_out = loss_dev;
+  h->in_train_step = true;
+  struct Reset { iwae_handle* h; ~Reset() { h->in_train_step = false; } } reset_flag{h};
   if (h->use_graphs && philox && h->prof_kind < 0) {
     std::vector<long long> key = {adam ? 1 : 0, lc->loss, B, lc->k, lc->k1, lc->k2, (long long)(uintptr_t)loss_dev};
     float fk[3] = {lc->p, lc->alpha, lc->beta};
@@ -1138,6 +1198,8 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (e == hipSuccess) e = hipMalloc(&h->adam_v, pb);
   if (e == hipSuccess) e = hipMalloc(&h->grad_own, pb);
   if (e == hipSuccess) e = hipMalloc(&h->ds, sizeof(DevState));
+  if (e == hipSuccess) e = hipMalloc(&h->wsplit_hi, (size_t)(2 * h->wsplit_elems) * sizeof(__bf16));
+  if (e == hipSuccess) e = hipMemset(h->wsplit_hi, 0, (size_t)(2 * h->wsplit_elems) * sizeof(__bf16));
   if (e == hipSuccess) e = hipMemset(h->params, 0, h->params_bytes);
   if (e == hipSuccess) e = hipMemset(h->adam_m, 0, pb);
   if (e == hipSuccess) e = hipMemset(h->adam_v, 0, pb);
@@ -1154,6 +1216,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
     return nullptr;
   }
   h->grad = h->grad_own;
+  h->wsplit_lo = h->wsplit_hi + h->wsplit_elems;
   e = rb_setup_attributes();
   if (e != hipSuccess) {
     g_create_error = std::string("hipFuncSetAttribute failed: ") + hipGetErrorString(e);
@@ -1176,6 +1239,7 @@ void iwae_destroy(iwae_handle* h) {
   if (h->adam_v) (void)hipFree(h->adam_v);
   if (h->grad_own) (void)hipFree(h->grad_own);
   if (h->ds) (void)hipFree(h->ds);
+  if (h->wsplit_hi) (void)hipFree(h->wsplit_hi);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
   delete h;
 }
@@ -1209,6 +1273,15 @@ int iwae_set_path(iwae_handle* h, int path) {
   if (!h) return IWAE_EINVAL;
   if (path < 0 || path > 2) return fail(h, IWAE_EINVAL, "path must be 0 (auto), 1 (layer-wise) or 2 (fused)");
   h->path = path;
+  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+  h->graphs.clear();
+  return IWAE_OK;
+}
+
+int iwae_set_precision(iwae_handle* h, int mode) {
+  if (!h) return IWAE_EINVAL;
+  if (mode != 0 && mode != 1) return fail(h, IWAE_EINVAL, "precision must be 0 (f32 MFMA) or 1 (bf16x3)");
+  h->x3 = mode;
   for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
   h->graphs.clear();
   return IWAE_OK;
@@ -1270,7 +1343,9 @@ static int download(iwae_handle* h, const float* dev, float* host) {
 
 int iwae_set_params(iwae_handle* h, const float* host, long long n) {
   CHK(check_n(h, n, host));
-  return upload(h, h->params, host);
+  CHK(upload(h, h->params, host));
+  h->params_version++;
+  return IWAE_OK;
 }
 
 int iwae_get_params(iwae_handle* h, float* host, long long n) {
@@ -1354,6 +1429,7 @@ int iwae_apply_adam(iwae_handle* h, float grad_scale) {
 static int eval_forward(iwae_handle* h, const Plan& P, const float* x, const float* const* eps, int n_eps,
                         EpsSet& E) {
   if (!x) return fail(h, IWAE_EINVAL, "x is NULL");
+  if (h->x3) CHK(ensure_wsplit(h));
   CHK(parse_eps(h, P, eps, n_eps, E));
   CHK(ensure_capacity(h, P.Bimg, P.Bimg * P.kS, false));
   CHK(copy_x(h, P, x));
@@ -1406,11 +1482,15 @@ static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, flo
   if (!h) return IWAE_EINVAL;
   if (!x) return fail(h, IWAE_EINVAL, "x is NULL");
   if (N <= 0 || k <= 0) return fail(h, IWAE_EINVAL, "N and k must be positive");
-  const long long target_rows = std::max<long long>(1 << 20, k);
+  // 2^20 sample rows per chunk (measured fastest: 2^17-2^20 within 10 %, smaller slower)
+  long long nll_rows = 1LL << 20;
+  if (const char* e = std::getenv("IWAE_NLL_ROWS")) nll_rows = std::max(1LL, std::atoll(e));   // tuning knob
+  const long long target_rows = std::max<long long>(nll_rows, k);
   int imgs = chunk > 0 ? chunk : (int)std::max<long long>(1, target_rows / k);
   imgs = std::min(imgs, N);
   const int kS = (int)std::min<long long>(k, std::max<long long>(1, target_rows / imgs));
   CHK(ensure_capacity(h, imgs, imgs * kS, false));
+  if (h->x3) CHK(ensure_wsplit(h));
   const size_t wbytes = (size_t)h->xdim * sizeof(float);
   for (int i0 = 0; i0 < N; i0 += imgs) {
     const int n = std::min(imgs, N - i0);
@@ -1472,6 +1552,7 @@ int iwae_debug_gemm(iwae_handle* h, const float* A, int lda, const float* B, int
   if ((lda | ldb | ldc) & 3) return fail(h, IWAE_EINVAL, "leading dims must be multiples of 4");
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return fail(h, IWAE_EINVAL, "pointers must be 16B aligned");
   GemmArgs a{};
+  a.x3 = h->x3;
   a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = C; a.ldc = ldc; a.M = M; a.N = N; a.K = K; a.kchunk = K;
   HIPCHK(launch_gemm(h->stream, GEMM_FWD, EPI_STORE, choose_tile(M, N, 1), 1, false, a));
   return IWAE_OK;

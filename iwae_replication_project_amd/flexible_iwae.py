@@ -160,7 +160,7 @@ class Flexible_Model:
     def __init__(self, n_hidden_encoder, n_hidden_decoder, n_latent_encoder, n_latent_decoder,
                  dataset_bias="Binarized_MNIST", loss_function="VAE", k=50, p=1, alpha=1, beta=0.5,
                  *, k1=None, k2=None, x_dim=784, device=None, seed=None, use_graphs=True,
-                 kernel_path="auto", **kwargs):
+                 kernel_path="auto", precision="bf16x3", **kwargs):
         self.dense = architecture(n_hidden_encoder, n_hidden_decoder, n_latent_encoder, n_latent_decoder, x_dim)
         loss_config(loss_function, k, p, alpha, beta, k1, k2)   # validate early
         if not torch.cuda.is_available():
@@ -206,6 +206,10 @@ class Flexible_Model:
         if kernel_path not in paths:
             raise ValueError(f"kernel_path must be one of {tuple(paths)}")
         self._call(self._lib.iwae_set_path(h, paths[kernel_path]))
+        precisions = {"f32": 0, "bf16x3": 1}
+        if precision not in precisions:
+            raise ValueError(f"precision must be one of {tuple(precisions)}")
+        self._call(self._lib.iwae_set_precision(h, precisions[precision]))
         rng = np.random.default_rng(int(seed) & ((1 << 63) - 1))
         self.set_weights(glorot_weights(self.dense, rng, resolve_dataset_bias(dataset_bias, x_dim)))
         self._loss_buf = torch.zeros(1, device=self.device)

@@ -13,6 +13,12 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 REL = 1e-4          # losses / gradients (north_star)
 NLL_TOL = 0.05      # nats
+# Post-Adam weights: Adam's first step lr*g/(|g|+eps) amplifies a gradient's
+# absolute error by up to lr/eps = 10 for near-zero gradient elements.  The
+# tiled GEMMs default to bf16x3 products (a_hi b_hi + a_hi b_lo + a_lo b_hi,
+# <= ~2.3e-5 relative per product), so isolated near-zero gradient elements
+# carry up to ~5e-6 absolute error: 6e-5 = 6% of lr on the weights.
+ADAM_ATOL = 6e-5
 
 
 @pytest.fixture(scope="module")
@@ -54,11 +60,12 @@ LOSS_KW = {"VAE": {}, "IWAE": {}, "L_power_p": dict(p=2.5), "L_median": {}, "L_a
 
 
 # ------------------------------------------------------------- GEMM unit
+@pytest.mark.parametrize("precision,tol", [("f32", 2e-6), ("bf16x3", 3e-5)])
 @pytest.mark.parametrize("M,N,K", [(64, 64, 16), (37, 53, 20), (130, 300, 68), (1000, 784, 200), (5, 7, 4)])
-def test_debug_gemm_matches_fp32_reference(torch_mod, M, N, K):
+def test_debug_gemm_matches_fp32_reference(torch_mod, M, N, K, precision, tol):
     torch = torch_mod
     from iwae_replication_project_amd import _lib
-    m = make_model([16], [16], [4], [64], x_dim=64)
+    m = make_model([16], [16], [4], [64], x_dim=64, precision=precision)
     g = torch.Generator().manual_seed(M * 1000 + N)
     lda, ldb, ldc = (K + 3) // 4 * 4, (N + 3) // 4 * 4, (N + 3) // 4 * 4
     A = torch.zeros(M, lda)
@@ -73,7 +80,8 @@ def test_debug_gemm_matches_fp32_reference(torch_mod, M, N, K):
     ref = (A[:, :K].double() @ B[:, :N].double())
     err = (Cd[:, :N].cpu().double() - ref).abs().max().item()
     scale = (A[:, :K].abs().double() @ B[:, :N].abs().double()).max().item()
-    assert err <= 2e-6 * scale, (err, scale)
+    # f32: exact fmaf chain; bf16x3: (2^-16 + 2^-17) relative per product, worst case
+    assert err <= tol * scale, (err, scale)
 
 
 # ---------------------------------------------------------- golden fixtures
@@ -159,7 +167,7 @@ def test_c2_full_size_iwae_train_step_matches_oracle():
     assert rel_l2(flat(m.get_gradients()), ref_g) <= REL
     # Adam's first step lr*g/(|g|+eps) amplifies gradient rounding by up to lr/eps = 10
     # for near-zero gradients: allow 2% of lr on the updated weights
-    np.testing.assert_allclose(flat(m.get_weights()), O.flatten_params(spec, ref_new), atol=2e-5)
+    np.testing.assert_allclose(flat(m.get_weights()), O.flatten_params(spec, ref_new), atol=ADAM_ATOL)
 
 
 @pytest.mark.parametrize("loss", ["IWAE", "CIWAE", "PIWAE", "VAE_V1", "L_alpha", "L_median"])
@@ -182,9 +190,10 @@ def test_fused_and_layerwise_paths_agree(arch, loss):
         l2 = m.train_step(x)[loss]
         outs.append((l1, l2, g1, flat(m.get_weights())))
     (a1, a2, ga, wa), (b1, b2, gb, wb) = outs
-    assert abs(a1 - b1) <= REL * abs(a1) and abs(a2 - b2) <= REL * abs(a2)
-    assert rel_l2(gb, ga) <= REL
-    np.testing.assert_allclose(wb, wa, atol=2e-5)      # see the Adam note above
+    # two independent approximations, each within REL of the exact value: |a - b| <= 2 REL
+    assert abs(a1 - b1) <= 2 * REL * abs(a1) and abs(a2 - b2) <= 2 * REL * abs(a2)
+    assert rel_l2(gb, ga) <= 2 * REL
+    np.testing.assert_allclose(wb, wa, atol=2 * ADAM_ATOL)      # see the Adam note above
 
 
 # ----------------------------------------------- multi-step training parity
