@@ -360,11 +360,36 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
         // pixels of all 16 elements requested before the first store (clamped,
         // unconditional; out-of-tile elements are masked below)
         const int nc = min(n, N - 1);
+        // image of each row: the 32-row tile crosses at most one image boundary
+        // when x_row_div >= 32 (one division per tile instead of one per element)
+        const int mt = m0 + wm * TM * 32 + i * 32;
+        const int div = a.x_row_div;
+        const int i0 = min(mt, M - 1) / div, b1 = (i0 + 1) * div;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + rowq;
-          xs[r] = a.aux[(size_t)(min(m, M - 1) / a.x_row_div) * a.ldaux + nc];
+          const int m = min(mt + (r & 3) + 8 * (r >> 2) + rowq, M - 1);
+          const int img = div >= 32 ? i0 + (m >= b1 ? 1 : 0) : m / div;
+          xs[r] = a.aux[(size_t)img * a.ldaux + nc];
         }
+        if (!a.store_g && !a.need_bce) {
+          // log-probability only (NLL / bounds without a backward pass)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int ml = (r & 3) + 8 * (r >> 2) + rowq;
+            const bool ok = (mt + ml < M && n < N);
+            const float xv = xs[r];
+            const float sg = __fdividef(1.f, 1.f + __expf(-t[r]));
+            const float p = __fadd_rn(__fmul_rn(sg, kProbScale), kProbShift);
+            float val;
+            if (__all((xv == 0.f) || (xv == 1.f))) {
+              val = __logf(xv != 0.f ? p : 1.f - p);
+            } else {
+              val = __fadd_rn(__fmul_rn(log1pf(-p), 1.f - xv), __fmul_rn(logf(p), xv));
+            }
+            S[ml * 33 + (lane & 31)] = ok ? val : 0.f;
+            vb[r] = 0.f;
+          }
+        } else
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int ml = (r & 3) + 8 * (r >> 2) + rowq;
@@ -439,9 +464,22 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
   }
 }
 
+// XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs
+// (b % 8 shares an XCD; speed only, never correctness), so consecutive tile
+// indices -- the column tiles that re-read one A row panel -- are given to one
+// XCD and hit its L2 instead of being fetched once per XCD.  A bijection on
+// [0, n) for any n.
+__device__ __forceinline__ int xcd_tile(int b, int n) {
+  const int q = n >> 3, r = n & 7, x = b & 7, i = b >> 3;
+  return x * q + min(x, r) + i;
+}
+
 template <int WM, int WN, int TM, int TN, bool TA, bool TB, int EPI, bool KSCALE, bool X3>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs a) {
-  gemm_body<WM, WN, TM, TN, TA, TB, EPI, KSCALE, X3>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+  const int ntx = gridDim.x, nty = gridDim.y;
+  const int n = ntx * nty * gridDim.z;
+  const int L = xcd_tile(blockIdx.x + ntx * (blockIdx.y + nty * blockIdx.z), n);
+  gemm_body<WM, WN, TM, TN, TA, TB, EPI, KSCALE, X3>(a, L % ntx, (L / ntx) % nty, L / (ntx * nty));
 }
 
 // Several independent GEMMs of one kind in ONE launch (the weight gradients of
