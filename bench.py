@@ -34,6 +34,9 @@ TRAIN_FLOP_PER_ROW = 1_712_944
 NLL_FLOP_PER_IMAGE = 2.818e9
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec peak
 HBM_PEAK_GBS = 8000.0
+# algorithmic HBM bytes of one train-step Bernoulli GEMM launch (1000 rows):
+# read y2 [1000 x 201] + W3_aug [201 x 784] + x [20 x 784]; write g [1000 x 784] + partials [1000 x 25]
+ALGO_MB_BERN = (1000 * 201 + 201 * 784 + 20 * 784 + 1000 * 784 + 1000 * 25) * 4 / 1e6
 
 
 def pixel_profile():
@@ -153,21 +156,34 @@ def main():
     value = rows / el
     ms_per_step = 1e3 * el / args.steps
 
-    # ---- dominant kernel live timing: HIP events on the library stream around
-    # every launch of the decoder output GEMM (200 -> 784, fused Bernoulli
-    # epilogue) over K eager steps of the same workload
+    # ---- dominant kernel live timing: the decoder output GEMM (200 -> 784,
+    # fused Bernoulli epilogue) of this workload, recorded from one eager step,
+    # re-launched K times back to back between two HIP events on the library's
+    # stream (the stream it runs on); avg = elapsed / K
     model._call(model._lib.iwae_profile_gemm(model._h, 0, 2))
-    run(args.steps, args.warmup + args.steps)
+    run(1, args.warmup + args.steps)
     import ctypes
-    ms, fl, nl = ctypes.c_double(), ctypes.c_double(), ctypes.c_longlong()
-    model._call(model._lib.iwae_profile_read(model._h, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(nl)))
+    ms, fl = ctypes.c_double(), ctypes.c_double()
+    model._call(model._lib.iwae_profile_replay(model._h, args.steps, ctypes.byref(ms), ctypes.byref(fl)))
     model._call(model._lib.iwae_profile_gemm(model._h, -1, -1))
+    nl = ctypes.c_longlong(args.steps)
     avg_ms = ms.value / max(1, nl.value)
     flop_per_launch = fl.value / max(1, nl.value)
     achieved = flop_per_launch / (avg_ms * 1e-3) / 1e12
+    # HBM traffic of the same kernel: committed rocprofv3 PMC record (tools/pmc_passes.sh +
+    # tools/pmc_to_json.py; FETCH_SIZE x2 per the gfx950 correction, WRITE_SIZE as is)
+    traffic, traffic_src = None, None
+    pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            rec = json.load(f)
+        traffic = round(rec["traffic_bytes"] / 1e6, 3)
+        traffic_src = f"profiles/r01_pmc_traffic.json (MB per launch: fetch {rec['fetch_bytes'] / 1e6:.2f} + " \
+                      f"write {rec['write_bytes'] / 1e6:.2f}; algorithmic {ALGO_MB_BERN:.2f})"
     roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
-                    frac=round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), traffic=None,
-                    kernel="gemm_kernel<FWD, EPI_BERN> (decoder 200->784 + Bernoulli log-prob)",
+                    frac=round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), traffic=traffic, traffic_unit="MB/launch",
+                    traffic_source=traffic_src,
+                    kernel="gemm_kernel<FWD, EPI_BERN> f32 MFMA (decoder 200->784 + Bernoulli log-prob + dlogit)",
                     avg_us=round(avg_ms * 1e3, 3), flop_per_launch=flop_per_launch, launches=int(nl.value),
                     step_tflops=round(TRAIN_FLOP_PER_ROW * rows / el / 1e12, 3))
 
@@ -193,7 +209,8 @@ def main():
             dist.all_reduce(tot)
         nll = dict(value=round(args.nll_images / el2, 2), unit="images/s", images=args.nll_images, k=args.nll_k,
                    seconds=round(el2, 4), nll=round(float(-(tot[0] / tot[1]).item()), 4), shard="image",
-                   tflops=round(NLL_FLOP_PER_IMAGE * (args.nll_k / 5000) * args.nll_images / el2 / 1e12, 3))
+                   tflops=round(NLL_FLOP_PER_IMAGE * (args.nll_k / 5000) * args.nll_images / el2 / 1e12, 3),
+                   precision="bf16x3")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -212,6 +229,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
+            "precision": "train step: exact-f32 MFMA for weight products, bf16x3 (hi/lo split, f32 accumulate) "
+                         "for weight-gradient GEMMs; NLL: bf16x3 GEMMs",
             "data": "synthetic",
             "config": {"workload": "IWAE train step (fwd+bound+bwd+Adam), k=50, 2 stochastic layers "
                                    "784-200-200-100-100-50, batch 20 per GPU (BASELINE configs[1])",

@@ -179,6 +179,10 @@ double iwae_workspace_bytes(const iwae_handle* h);
  * launches (2*rows*fan_in*fan_out each) and the launch count. */
 int iwae_profile_gemm(iwae_handle* h, int kind, int epi);
 int iwae_profile_read(iwae_handle* h, double* total_ms, double* total_flop, long long* launches);
+/* Re-launch the last recorded launch of the profiled GEMM class n times back to
+ * back between two HIP events on the handle's stream (steady-state kernel time,
+ * comparable with rocprofv3's per-dispatch duration); synchronous. */
+int iwae_profile_replay(iwae_handle* h, int n, double* total_ms, double* total_flop);
 
 #ifdef __cplusplus
 }

@@ -76,6 +76,7 @@ SIGNATURES = {
     "iwae_workspace_bytes": (c_double, [H]),
     "iwae_profile_gemm": (c_int, [H, c_int, c_int]),
     "iwae_profile_read": (c_int, [H, POINTER(c_double), POINTER(c_double), POINTER(c_longlong)]),
+    "iwae_profile_replay": (c_int, [H, c_int, POINTER(c_double), POINTER(c_double)]),
 }
 
 _lib = None

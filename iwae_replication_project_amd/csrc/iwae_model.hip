@@ -136,6 +136,12 @@ struct iwae_handle {
   std::vector<hipEvent_t> prof_ev;
   size_t prof_used = 0;
   double prof_flop = 0.0;
+  // last launch of the profiled GEMM class (replayed back to back by iwae_profile_replay)
+  bool prof_have = false;
+  GemmArgs prof_args{};
+  GemmKind prof_k = GEMM_FWD; GemmEpi prof_e = EPI_STORE;
+  int prof_tile = 0, prof_splits = 1; bool prof_ks = false;
+  double prof_flop1 = 0.0;
 };
 
 #define HIPCHK(expr)                                                           \
@@ -337,6 +343,13 @@ static bool prof_match(iwae_handle* h, GemmKind kind, GemmEpi epi) {
   return h->prof_kind == (int)kind && h->prof_epi == (int)epi;
 }
 
+static void prof_note(iwae_handle* h, GemmKind kind, GemmEpi epi, int tile, int splits, bool ks, const GemmArgs& a,
+                      double flop) {
+  if (!prof_match(h, kind, epi)) return;
+  h->prof_have = true; h->prof_args = a; h->prof_k = kind; h->prof_e = epi;
+  h->prof_tile = tile; h->prof_splits = splits; h->prof_ks = ks; h->prof_flop1 = flop;
+}
+
 static int prof_begin(iwae_handle* h, GemmKind kind, GemmEpi epi, double flop) {
   if (!prof_match(h, kind, epi)) return IWAE_OK;
   if (h->prof_used + 2 > h->prof_ev.size()) {
@@ -370,6 +383,7 @@ static int gemm_fwd(iwae_handle* h, GemmEpi epi, const Mat& X, int rows, const D
   a.c_split_stride = 0;
   if (use_split_b(h)) { a.Bhi = h->wsplit_hi + d.f_off; a.Blo = h->wsplit_lo + d.f_off; a.ldbx = d.ldF; }
   CHK(prof_begin(h, GEMM_FWD, epi, 2.0 * rows * d.fout * d.fin));
+  prof_note(h, GEMM_FWD, epi, choose_tile(a.M, a.N, 1), 1, false, a, 2.0 * rows * d.fout * d.fin);
   HIPCHK(launch_gemm(h->stream, GEMM_FWD, epi, choose_tile(a.M, a.N, 1), 1, false, a));
   CHK(prof_end(h, GEMM_FWD, epi));
   return IWAE_OK;
@@ -1567,6 +1581,28 @@ int iwae_profile_gemm(iwae_handle* h, int kind, int epi) {
   h->prof_epi = epi;
   h->prof_used = 0;
   h->prof_flop = 0.0;
+  h->prof_have = false;
+  return IWAE_OK;
+}
+
+int iwae_profile_replay(iwae_handle* h, int n, double* total_ms, double* total_flop) {
+  if (!h || !total_ms || !total_flop || n <= 0) return IWAE_EINVAL;
+  if (!h->prof_have) return fail(h, IWAE_EINVAL, "no launch of the profiled GEMM class was recorded");
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipEventRecord(e0, h->stream));
+  for (int i = 0; i < n; ++i)
+    HIPCHK(launch_gemm(h->stream, h->prof_k, h->prof_e, h->prof_tile, h->prof_splits, h->prof_ks, h->prof_args));
+  HIPCHK(hipEventRecord(e1, h->stream));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  *total_ms = ms;
+  *total_flop = h->prof_flop1 * n;
   return IWAE_OK;
 }
 
