@@ -472,7 +472,8 @@ __global__ __launch_bounds__(256) void lse_kernel(LseArgs a) {
     float m = -INFINITY, s = 0.f;
     for (int q = lane; q < a.kS; q += 64) {
       const int r = row0 + q;
-      const float v = __fsub_rn(__fadd_rn(a.logp[r], row_sum_parts(a.part, a.ldpart, a.npart, r)), a.logq[r]);
+      const float v = a.lw ? a.lw[r]
+                           : __fsub_rn(__fadd_rn(a.logp[r], row_sum_parts(a.part, a.ldpart, a.npart, r)), a.logq[r]);
       if (v > m) { s = s * fexp(m - v) + 1.f; m = v; }
       else s += fexp(v - m);
     }

@@ -197,6 +197,7 @@ hipError_t launch_bound(hipStream_t st, const BoundArgs& a);
 // per-image LSE over this chunk's rows merged into running (m, s)
 struct LseArgs {
   const float* part; int ldpart, npart; const float* logp; const float* logq;
+  const float* lw;             // if set: log w per row directly (fused forward), part/logp/logq unused
   int kS, Bimg;
   float* run_m; float* run_s; int init;
   unsigned* ticket; uint64_t* rng_base;
@@ -321,6 +322,40 @@ struct RbBwdLaunch {
 hipError_t launch_rb_fwd(hipStream_t st, RbFwdLaunch& L);
 hipError_t launch_rb_bwd(hipStream_t st, RbBwdLaunch& L);
 hipError_t rb_setup_attributes();
+
+// ------------------------------------------- fused k-sample forward (NLL) ----
+// One workgroup owns MG_ROWS(RT) = 16*RT sample rows and runs the whole model
+// after the first encoder layer on them, activations resident in LDS: sample
+// h1 from the image's (mu, scale), every later stochastic layer, the decoder
+// prior, the output MLP and the Bernoulli log-likelihood; it writes only the
+// log weight of each row.  Matrix products: bf16x3 on v_mfma_f32_16x16x32_bf16
+// with the layers' pre-split F copies streamed from L2 into registers.
+constexpr int kMgMaxStages = 24;
+constexpr int kMgMaxBufs = 12;
+enum MgAct { MG_NONE = 0, MG_TANH = 1, MG_BERN = 2 };
+enum MgPost { MGP_NONE = 0, MGP_SAMPLE = 1, MGP_PRIOR = 2 };
+struct MgStage {
+  const __bf16* Whi; const __bf16* Wlo; unsigned W_bytes;
+  int ldk, K, N;             // F [N][ldk]; K = fin + 1 (input ones column at K - 1)
+  int in_buf, out_buf;       // LDS buffer ids
+  int act;                   // MgAct
+  int post, post_buf, d;     // MgPost on the output (mu | zs): SAMPLE -> post_buf, PRIOR target post_buf
+  int layer, stdnormal;      // SAMPLE: Philox layer; add log N(h; 0, 1) to log p
+  int next_k;                // padded K of the next reader of out_buf (ones column + zero pad); N if none
+  int post_next_k;           // SAMPLE: padded K of the reader of post_buf
+};
+struct MgLaunch {
+  MgStage st[kMgMaxStages]; int nst;
+  int buf_off[kMgMaxBufs], buf_ld[kMgMaxBufs];   // float offsets / row strides in LDS
+  int acc_off;                                    // LDS: logq, logp, logpx [rows] + reduction scratch
+  int rows, kS;                                   // sample rows in this chunk, samples per image
+  const float* P0; int ldP0; int d0; int h0_buf; int h0_next_k; int h0_stdnormal;   // prologue sampling
+  const float* x; int ldx;                        // pixels [images][ldx]
+  uint64_t seed; const uint64_t* rng_base;
+  float* lw;                                      // out: log w per row
+};
+hipError_t launch_mega_fwd(hipStream_t st, const MgLaunch& L, int rt, size_t lds_bytes);
+hipError_t mega_setup_attributes();
 
 hipError_t launch_fill_col(hipStream_t st, float* buf, int rows, int ld, int col, float v);
 hipError_t launch_transpose_lw(hipStream_t st, const float* lw_img, int Bimg, int kS, float* out);

@@ -127,6 +127,7 @@ struct iwae_handle {
   int oslab_S = 0;
   int path = 0;                      // 0 auto, 1 layer-wise kernels, 2 fused row-block kernels
   int x3 = 1;                        // tiled GEMMs: 1 bf16x3 products (default), 0 exact f32 MFMA
+  int nll_fused = 1;                 // NLL: fused k-sample forward (mega_fwd_kernel) when it fits
   // graphs
   bool use_graphs = false;
   std::map<std::vector<long long>, hipGraphExec_t> graphs;
@@ -1232,6 +1233,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   h->grad = h->grad_own;
   h->wsplit_lo = h->wsplit_hi + h->wsplit_elems;
   e = rb_setup_attributes();
+  if (e == hipSuccess) e = mega_setup_attributes();
   if (e != hipSuccess) {
     g_create_error = std::string("hipFuncSetAttribute failed: ") + hipGetErrorString(e);
     iwae_destroy(h);
@@ -1287,6 +1289,7 @@ int iwae_set_path(iwae_handle* h, int path) {
   if (!h) return IWAE_EINVAL;
   if (path < 0 || path > 2) return fail(h, IWAE_EINVAL, "path must be 0 (auto), 1 (layer-wise) or 2 (fused)");
   h->path = path;
+  h->nll_fused = path != 1;             // layer-wise everywhere when asked for
   for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
   h->graphs.clear();
   return IWAE_OK;
@@ -1490,6 +1493,80 @@ int iwae_e_log_px(iwae_handle* h, const float* x, int B, int k, const float* con
   return IWAE_OK;
 }
 
+// ------------------------------------------------ fused k-sample forward
+// Plan of mega_fwd_kernel for this model (iwae_mega.hip): LDS buffers h_0 ..
+// h_{L-2} (kept), scratch P and Q (h_{L-1} lives in Q), the Dense stages after
+// the first encoder layer with their post ops.  False if it does not fit.
+static bool mega_plan(iwae_handle* h, MgLaunch& M, int& rt, size_t& lds) {
+  const int L = h->L;
+  std::memset(&M, 0, sizeof(M));
+  auto r32 = [](int x) { return (x + 31) & ~31; };
+  const int bP = L - 1, bQ = L;                 // scratch buffer ids
+  auto hbuf = [&](int i) { return i == L - 1 ? bQ : i; };
+  int nb = L + 1;
+  if (nb > kMgMaxBufs) return false;
+  int sw = 0;                                   // scratch width
+  std::vector<MgStage> st;
+  auto stage = [&](int di, int in, int out, int act, int next_k) {
+    const DenseL& d = h->dense[di];
+    MgStage S{};
+    S.Whi = h->wsplit_hi + d.f_off; S.Wlo = h->wsplit_lo + d.f_off;
+    S.W_bytes = (unsigned)((h->wsplit_elems - d.f_off) * (long long)sizeof(__bf16));
+    S.ldk = d.ldF; S.K = d.fin + 1; S.N = d.fout;
+    S.in_buf = in; S.out_buf = out; S.act = act; S.next_k = next_k;
+    if (in == bP || in == bQ) sw = std::max(sw, S.ldk);
+    if (out == bP || out == bQ) sw = std::max(sw, std::max(S.N, next_k));
+    st.push_back(S);
+    return (int)st.size() - 1;
+  };
+  for (int i = 1; i < L; ++i) {
+    const StochL& E = h->enc[i];
+    stage(E.l1, hbuf(i - 1), bP, MG_TANH, h->dense[E.l2].ldF);
+    stage(E.l2, bP, bQ, MG_TANH, h->dense[E.head].ldF);
+    const int s = stage(E.head, bQ, bP, MG_NONE, h->dense[E.head].fout);
+    st[s].post = MGP_SAMPLE; st[s].post_buf = hbuf(i); st[s].d = E.d; st[s].layer = i;
+    st[s].stdnormal = i == L - 1; st[s].post_next_k = r32(E.d + 1);
+    if (hbuf(i) == bQ) sw = std::max(sw, r32(E.d + 1));
+  }
+  for (int j = 0; j < L - 1; ++j) {
+    const StochL& D = h->dec[j];
+    stage(D.l1, hbuf(L - 1 - j), bP, MG_TANH, h->dense[D.l2].ldF);
+    stage(D.l2, bP, bQ, MG_TANH, h->dense[D.head].ldF);
+    const int s = stage(D.head, bQ, bP, MG_NONE, h->dense[D.head].fout);
+    st[s].post = MGP_PRIOR; st[s].post_buf = hbuf(L - 2 - j); st[s].d = D.d;
+  }
+  const int h0 = hbuf(0);
+  const int o1out = h0 == bQ ? bP : bQ, o2out = o1out == bP ? bQ : bP;
+  stage(h->o1, h0, o1out, MG_TANH, h->dense[h->o2].ldF);
+  stage(h->o2, o1out, o2out, MG_TANH, h->dense[h->o3].ldF);
+  stage(h->o3, o2out, -1, MG_BERN, 0);
+  if ((int)st.size() > kMgMaxStages) return false;
+  if (h0 == bQ) sw = std::max(sw, r32(h->enc[0].d + 1));
+  // LDS layout (floats): row strides = width + 4 (rows start 4 banks apart)
+  int off = 0;
+  for (int b = 0; b < nb; ++b) {
+    const int w = (b == bP || b == bQ) ? sw : r32(h->enc[b].d + 1);
+    M.buf_ld[b] = w + 4;
+    M.buf_off[b] = off;
+  }
+  for (int c : {4, 2, 1}) {
+    const int R = 16 * c;
+    off = 0;
+    for (int b = 0; b < nb; ++b) { M.buf_off[b] = off; off += R * M.buf_ld[b]; }
+    M.acc_off = off;
+    const size_t bytes = (size_t)(off + 3 * R + 8 * R) * sizeof(float);
+    if (bytes <= 160 * 1024) {
+      rt = c;
+      lds = bytes;
+      for (size_t i = 0; i < st.size(); ++i) M.st[i] = st[i];
+      M.nst = (int)st.size();
+      M.h0_buf = h0; M.d0 = h->enc[0].d; M.h0_next_k = r32(h->enc[0].d + 1); M.h0_stdnormal = L == 1;
+      return true;
+    }
+  }
+  return false;
+}
+
 // chunked k-sample NLL over N images; accumulates per-image (m, s)
 static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, float* out_m, float* out_s,
                     float* out_logpx) {
@@ -1505,6 +1582,10 @@ static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, flo
   const int kS = (int)std::min<long long>(k, std::max<long long>(1, target_rows / imgs));
   CHK(ensure_capacity(h, imgs, imgs * kS, false));
   if (h->x3) CHK(ensure_wsplit(h));
+  MgLaunch MG;
+  int mg_rt = 0;
+  size_t mg_lds = 0;
+  const bool mega = h->x3 && h->nll_fused && mega_plan(h, MG, mg_rt, mg_lds);
   const size_t wbytes = (size_t)h->xdim * sizeof(float);
   for (int i0 = 0; i0 < N; i0 += imgs) {
     const int n = std::min(imgs, N - i0);
@@ -1515,8 +1596,20 @@ static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, flo
       P.B = n; P.Bimg = n; P.Bsplit = n; P.kS = std::min(kS, k - s0);
       EpsSet E;
       std::memset(&E, 0, sizeof(E));
-      CHK(forward_core(h, P, E, false));
       LseArgs a{};
+      if (mega) {
+        // first encoder layer on the chunk's images, then everything else fused
+        CHK(stoch_fwd(h, h->enc[0], h->x_in, n, h->eb[0]));
+        MG.rows = n * P.kS; MG.kS = P.kS;
+        MG.P0 = h->eb[0].P.p; MG.ldP0 = h->eb[0].P.ld;
+        MG.x = h->x_in.p; MG.ldx = h->x_in.ld;
+        MG.seed = h->seed; MG.rng_base = &h->ds->rng[0];
+        MG.lw = h->lw;
+        HIPCHK(launch_mega_fwd(h->stream, MG, mg_rt, mg_lds));
+        a.lw = h->lw;
+      } else {
+        CHK(forward_core(h, P, E, false));
+      }
       a.part = h->part; a.ldpart = h->ldpart; a.npart = h->npart; a.logp = h->logp; a.logq = h->logq;
       a.kS = P.kS; a.Bimg = n; a.run_m = h->run_m; a.run_s = h->run_s; a.init = s0 == 0;
       a.ticket = &h->ds->tickets[1]; a.rng_base = &h->ds->rng[0];
