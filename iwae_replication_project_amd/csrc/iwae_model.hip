@@ -1542,19 +1542,19 @@ static bool mega_plan(iwae_handle* h, MgLaunch& M, int& rt, size_t& lds) {
   stage(h->o3, o2out, -1, MG_BERN, 0);
   if ((int)st.size() > kMgMaxStages) return false;
   if (h0 == bQ) sw = std::max(sw, r32(h->enc[0].d + 1));
-  // LDS layout (floats): row strides = width + 4 (rows start 4 banks apart)
-  int off = 0;
+  // LDS layout: each buffer = hi and lo bf16 planes [R][ld]; ld = width + 8
+  // (16-byte aligned rows that start 4 banks apart); then logq, logp [R] and
+  // the [8][R] reduction scratch as floats
   for (int b = 0; b < nb; ++b) {
     const int w = (b == bP || b == bQ) ? sw : r32(h->enc[b].d + 1);
-    M.buf_ld[b] = w + 4;
-    M.buf_off[b] = off;
+    M.buf_ld[b] = w + 8;
   }
   for (int c : {4, 2, 1}) {
     const int R = 16 * c;
-    off = 0;
-    for (int b = 0; b < nb; ++b) { M.buf_off[b] = off; off += R * M.buf_ld[b]; }
-    M.acc_off = off;
-    const size_t bytes = (size_t)(off + 3 * R + 8 * R) * sizeof(float);
+    int off = 0;                                // bf16 units
+    for (int b = 0; b < nb; ++b) { M.buf_off[b] = off; off += 2 * R * M.buf_ld[b]; }
+    M.acc_off = (off + 3) / 2 & ~1;             // floats
+    const size_t bytes = (size_t)(M.acc_off + 2 * R + 8 * R) * sizeof(float);
     if (bytes <= 160 * 1024) {
       rt = c;
       lds = bytes;
