@@ -547,6 +547,115 @@ static hipError_t dispatch_tile(hipStream_t st, GemmKind kind, GemmEpi epi, int 
   return hipErrorInvalidValue;
 }
 
+// ------------------------------------------------------------ few-row Dense
+// The [M][K] activations are staged once into LDS with coalesced 16-byte loads
+// (fragment-shaped loads straight from global touch 16 cache lines per
+// instruction and saturate the CU's address path); each wave then owns a
+// 16-aligned k range: lane (r, g) holds k = 16u + 4g + j (j = 0..3), so a
+// 16-byte LDS read feeds 4 MFMAs and, for bt = 1, one 16-byte weight load does.
+constexpr int SM_WAVES = 8;
+constexpr int SM_MAXU = 8;          // 16-deep k groups per wave (K <= 8 * 16 * 8 = 1024)
+
+__global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int t = blockIdx.x;
+  const int n = t * 16 + r;
+  const int Kp = (a.K + 15) & ~15, lds_ld = Kp + 4;
+  float* As = sm_lds;                                  // [32][lds_ld]
+  float* part = sm_lds + 32 * lds_ld;                  // [wave][rt][i][lane]
+  const int kc = (((a.K + SM_WAVES - 1) / SM_WAVES) + 15) & ~15;
+  const int kb = wave * kc;
+  const int nu = min(SM_MAXU, max(0, (min(kc, Kp - kb) + 15) >> 4));
+  // weights of this wave's k range, requested first (they do not depend on A)
+  const __amdgpu_buffer_rsrc_t rW = buf_rsrc(a.W);
+  float4 bq[SM_MAXU];
+#pragma unroll
+  for (int u = 0; u < SM_MAXU; ++u) {
+    const int k0 = kb + 16 * u + 4 * g;
+    const bool ok = u < nu && n < a.N;
+    if (a.bt) {
+      // W[n][k0..k0+3]: one 16-byte load (k beyond K reads the row's zero padding or 0)
+      bq[u] = bld4(rW, (ok && k0 < a.K) ? (unsigned)(n * a.ldw + k0) * 4u : kOOB);
+    } else {
+      float e[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        e[j] = bld1(rW, (ok && k0 + j < a.K) ? (unsigned)((k0 + j) * a.ldw + n) * 4u : kOOB);
+      bq[u] = make_float4(e[0], e[1], e[2], e[3]);
+    }
+  }
+  // activations -> LDS (rows >= M and k >= K zero)
+  const __amdgpu_buffer_rsrc_t rA = buf_rsrc(a.A);
+  const int q4 = Kp >> 2;
+  for (int e = threadIdx.x; e < 32 * q4; e += blockDim.x) {
+    const int row = e / q4, kq = e - row * q4;
+    const int k = 4 * kq;
+    float4 v = bld4(rA, (row < a.M && k < a.K) ? (unsigned)(row * a.lda + k) * 4u : kOOB);
+    if (k + 3 >= a.K) {          // zero the part of the last quad past K (the row's padding may hold the ones column)
+      if (k + 1 >= a.K) v.y = 0.f;
+      if (k + 2 >= a.K) v.z = 0.f;
+      if (k + 3 >= a.K) v.w = 0.f;
+    }
+    *reinterpret_cast<float4*>(&As[row * lds_ld + k]) = v;
+  }
+  __syncthreads();
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  f4v c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+  const bool two = a.M > 16;
+#pragma unroll
+  for (int u = 0; u < SM_MAXU; ++u) {
+    if (u >= nu) break;
+    const int k0 = kb + 16 * u + 4 * g;
+    const float4 a0 = *reinterpret_cast<const float4*>(&As[r * lds_ld + k0]);
+    const float4 a1 = *reinterpret_cast<const float4*>(&As[(16 + r) * lds_ld + k0]);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, bq[u].x, c0, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, bq[u].y, c0, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, bq[u].z, c0, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, bq[u].w, c0, 0, 0, 0);
+    if (two) {
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, bq[u].x, c1, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, bq[u].y, c1, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, bq[u].z, c1, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, bq[u].w, c1, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    part[((wave * 2 + 0) * 4 + i) * 64 + lane] = c0[i];
+    part[((wave * 2 + 1) * 4 + i) * 64 + lane] = c1[i];
+  }
+  __syncthreads();
+  // 512 threads: (row tile, i, lane) = 2 * 4 * 64 elements, fixed-order sum over the waves
+  const int e = threadIdx.x, rt = e >> 8, i = (e >> 6) & 3, l = e & 63;
+  float v = 0.f;
+#pragma unroll
+  for (int w = 0; w < SM_WAVES; ++w) v += part[((w * 2 + rt) * 4 + i) * 64 + l];
+  const int row = rt * 16 + 4 * (l >> 4) + i, col = t * 16 + (l & 15);
+  if (row < a.M && col < a.N) {
+    if (a.act == 1) v = ftanh(v);
+    else if (a.act == 2) {
+      const float y = a.Y[(size_t)row * a.ldy + col];
+      v = v * (1.f - y * y);
+    }
+    a.C[(size_t)row * a.ldc + col] = v;
+  }
+}
+
+hipError_t launch_smallm(hipStream_t st, const SmArgs& a) {
+  if (a.M <= 0 || a.N <= 0) return hipSuccess;
+  if (a.M > 32 || a.K > SM_WAVES * 16 * SM_MAXU) return hipErrorInvalidValue;
+  const int Kp = (a.K + 15) & ~15;
+  const size_t lds = (size_t)(32 * (Kp + 4) + SM_WAVES * 2 * 4 * 64) * sizeof(float);
+  hipLaunchKernelGGL(smallm_kernel, dim3((a.N + 15) / 16), dim3(SM_WAVES * 64), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t smallm_setup_attributes() {
+  return hipFuncSetAttribute((const void*)smallm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
 hipError_t launch_gemm(hipStream_t st, GemmKind kind, GemmEpi epi, int tile, int splits, bool ks,
                        const GemmArgs& a) {
   if (a.M <= 0 || a.N <= 0) return hipSuccess;

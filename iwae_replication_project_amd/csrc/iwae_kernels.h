@@ -127,6 +127,23 @@ struct GemmArgs {
 hipError_t launch_gemm(hipStream_t st, GemmKind kind, GemmEpi epi, int tile, int splits,
                        bool kscale, const GemmArgs& a);
 
+// Few-row Dense layer (M <= 32 rows: the per-image first encoder layer of a
+// small batch): C[M][N] = act(A[M][K] . B).  One workgroup per 16-column tile
+// (N-split, so the K x N weights are streamed once over many CUs), its 8 waves
+// split K, partial tiles summed through LDS; exact f32 MFMA.
+//   bt = 0: B(k,n) = W[k*ldw + n]  (forward, W_aug = [W; b], K = fin + 1)
+//   bt = 1: B(k,n) = W[n*ldw + k]  (backward dX = dZ W^T, K = fout, N = fin)
+//   act: 0 store, 1 tanh, 2 times (1 - Y^2)
+struct SmArgs {
+  const float* A; int lda;
+  const float* W; int ldw; int bt;
+  float* C; int ldc;
+  int M, N, K;
+  int act; const float* Y; int ldy;
+};
+hipError_t launch_smallm(hipStream_t st, const SmArgs& a);
+hipError_t smallm_setup_attributes();
+
 // grouped backward-weight GEMMs (64x64 tiles, split over K = rows)
 constexpr int kMaxGroup = 16;
 struct GemmGroup {

@@ -786,8 +786,34 @@ static RbNoise rb_noise(iwae_handle* h, const Plan& P, const EpsSet& E, int laye
   return n;
 }
 
+// few-row Dense layer (per-image first encoder layer of a small batch)
+static int smallm(iwae_handle* h, const Mat& A, int rows, const DenseL& d, bool bwd, int act, const Mat* Y, Mat& C) {
+  SmArgs a{};
+  a.A = A.p; a.lda = A.ld;
+  a.W = h->params + d.off; a.ldw = d.ldw; a.bt = bwd ? 1 : 0;
+  a.C = C.p; a.ldc = C.ld;
+  a.M = rows; a.N = bwd ? d.fin : d.fout; a.K = bwd ? d.fout : d.fin + 1;
+  a.act = act;
+  if (Y) { a.Y = Y->p; a.ldy = Y->ld; }
+  HIPCHK(launch_smallm(h->stream, a));
+  return IWAE_OK;
+}
+static bool smallm_ok(const iwae_handle* h, int rows) {
+  if (rows > 32) return false;
+  for (int di : {h->enc[0].l1, h->enc[0].l2, h->enc[0].head})
+    if (h->dense[di].fin + 1 > 1024 || h->dense[di].fout > 1024) return false;
+  return true;
+}
+
 static int fused_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool train) {
   const int L = h->L, kS = P.kS, M = P.Bimg * kS;
+  if (smallm_ok(h, P.Bimg)) {
+    // (1') first encoder layer on the images: three N-split few-row launches
+    const StochL& S0 = h->enc[0];
+    CHK(smallm(h, h->x_in, P.Bimg, h->dense[S0.l1], false, 1, nullptr, h->eb[0].y1));
+    CHK(smallm(h, h->eb[0].y1, P.Bimg, h->dense[S0.l2], false, 1, nullptr, h->eb[0].y2));
+    CHK(smallm(h, h->eb[0].y2, P.Bimg, h->dense[S0.head], false, 0, nullptr, h->eb[0].P));
+  } else
   // (1) first encoder Dense (K = 785) as a split-K GEMM into partial slabs
   {
     const DenseL& d = h->dense[h->enc[0].l1];
@@ -1013,12 +1039,20 @@ static int fused_encoder_bwd(iwae_handle* h, const Plan& P, const float* dlw) {
     J.std_normal = i == L - 1;
     if (P.kl && i == L - 1) { J.kl_coef = 1.f; J.kl_rows = (L == 1) ? P.Bimg : M; }
     J.dP_out = h->eb[i].dP.p; J.ld_dP = h->eb[i].dP.ld;
-    J.nst = i == 0 ? 2 : 3;
-    J.st[0] = rb_bwd_stage(h, S.head, &h->eb[i].y2, &h->eb[i].dY2);
-    J.st[1] = rb_bwd_stage(h, S.l2, &h->eb[i].y1, &h->eb[i].dY1);
+    const bool sm0 = i == 0 && smallm_ok(h, P.Bimg);
+    J.nst = i == 0 ? (sm0 ? 0 : 2) : 3;
+    if (!sm0) {
+      J.st[0] = rb_bwd_stage(h, S.head, &h->eb[i].y2, &h->eb[i].dY2);
+      J.st[1] = rb_bwd_stage(h, S.l2, &h->eb[i].y1, &h->eb[i].dY1);
+    }
     if (i > 0) J.st[2] = rb_bwd_stage(h, S.l1, nullptr, &h->dh_enc[i - 1]);
     Lb.njobs = 1;
     HIPCHK(launch_rb_bwd(h->stream, Lb));
+    if (sm0) {
+      // first encoder layer's head and l2 backward as N-split few-row launches
+      CHK(smallm(h, h->eb[0].dP, P.Bimg, h->dense[S.head], true, 2, &h->eb[0].y2, h->eb[0].dY2));
+      CHK(smallm(h, h->eb[0].dY2, P.Bimg, h->dense[S.l2], true, 2, &h->eb[0].y1, h->eb[0].dY1));
+    }
   }
   return IWAE_OK;
 }
@@ -1234,6 +1268,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   h->wsplit_lo = h->wsplit_hi + h->wsplit_elems;
   e = rb_setup_attributes();
   if (e == hipSuccess) e = mega_setup_attributes();
+  if (e == hipSuccess) e = smallm_setup_attributes();
   if (e != hipSuccess) {
     g_create_error = std::string("hipFuncSetAttribute failed: ") + hipGetErrorString(e);
     iwae_destroy(h);
