@@ -248,9 +248,12 @@ __device__ __forceinline__ float row_sum_parts(const float* part, int ldpart, in
   // loads (no serialized latency chain), summed in column order.
   const float4* p = reinterpret_cast<const float4*>(part + (size_t)r * ldpart);
   const int n4 = (npart + 3) >> 2;
+  // buffer loads: the columns past n4 read 0 without a branch around the load
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(part);
+  const unsigned base = (unsigned)r * (unsigned)ldpart * 4u;
   float4 v[8];
 #pragma unroll
-  for (int t = 0; t < 8; ++t) v[t] = t < n4 ? p[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int t = 0; t < 8; ++t) v[t] = bld4(rs, t < n4 ? base + 16u * t : kOOB);
   float s = 0.f;
 #pragma unroll
   for (int t = 0; t < 8; ++t) s += ((v[t].x + v[t].y) + v[t].z) + v[t].w;
@@ -541,51 +544,61 @@ hipError_t launch_kl_v1(hipStream_t st, const float* P, int ldP, int d, int rows
 // Sums a layer's split-K weight-gradient slabs in fixed order (deterministic),
 // then TF ResourceApplyAdam: m += (g-m)(1-b1); v += (g^2-v)(1-b2);
 // p -= m * lr*sqrt(1-b2^t)/(1-b1^t) / (sqrt(v)+eps).
-__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
-  const AdamSeg sg = a.seg[blockIdx.y];
-  const AdamState st = *a.state;
-  const float scale = a.grad_scale_override > 0.f ? a.grad_scale_override : st.grad_scale;
-  // state->t was already advanced for this step (bound kernel / adam_tick_kernel)
-  const float t = (float)st.t;
-  const float b1p = powf(st.b1, t), b2p = powf(st.b2, t);
-  const float alpha = st.lr * sqrtf(1.f - b2p) / (1.f - b1p);
-  const float omb1 = 1.f - st.b1, omb2 = 1.f - st.b2;
-  const long long n4 = sg.n >> 2;    // segment sizes and offsets are multiples of 4 floats
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-       i += (long long)gridDim.x * blockDim.x) {
+// One float4 of one segment: slab sum, optional grad write-back, Adam update,
+// split-copy refresh.
+__device__ __forceinline__ void adam_one(const AdamArgs& a, const AdamSeg& sg, long long i) {
     const long long pidx = sg.off + 4 * i;
+    // Adam state first: its loads are in flight while the slabs are summed
+    float4 m = make_float4(0.f, 0.f, 0.f, 0.f), v = m, p = m;
+    if (a.do_adam) {
+      m = *reinterpret_cast<const float4*>(a.m + pidx);
+      v = *reinterpret_cast<const float4*>(a.v + pidx);
+      p = *reinterpret_cast<const float4*>(a.param + pidx);
+    }
     float4 g;
     if (a.read_slabs && sg.splits > 0) {
+      // every slab load in flight at once (buffer loads: slabs past `splits` read
+      // 0 without a branch), summed in slab order
       const float4* sl = reinterpret_cast<const float4*>(a.slabs + sg.slab_off) + i;
       const long long st4 = sg.n >> 2;
-      float4 acc0 = make_float4(0.f, 0.f, 0.f, 0.f), acc1 = acc0;
-      int s = 0;
-      for (; s + 4 <= sg.splits; s += 4) {
-        const float4 u0 = sl[(long long)s * st4], u1 = sl[(long long)(s + 1) * st4];
-        const float4 u2 = sl[(long long)(s + 2) * st4], u3 = sl[(long long)(s + 3) * st4];
-        acc0.x += u0.x + u1.x; acc0.y += u0.y + u1.y; acc0.z += u0.z + u1.z; acc0.w += u0.w + u1.w;
-        acc1.x += u2.x + u3.x; acc1.y += u2.y + u3.y; acc1.z += u2.z + u3.z; acc1.w += u2.w + u3.w;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (sg.splits <= 16 && st4 * 16 * 16 < 0x7FFFFFF0ll) {
+        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(a.slabs + sg.slab_off);
+        float4 u[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          u[q] = bld4(rs, q < sg.splits ? (unsigned)((q * st4 + i) * 16) : kOOB);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          acc.x += u[q].x; acc.y += u[q].y; acc.z += u[q].z; acc.w += u[q].w;
+        }
+      } else {
+        for (int q = 0; q < sg.splits; ++q) {
+          const float4 v4 = sl[(long long)q * st4];
+          acc.x += v4.x; acc.y += v4.y; acc.z += v4.z; acc.w += v4.w;
+        }
       }
-      for (; s < sg.splits; ++s) {
-        const float4 u = sl[(long long)s * st4];
-        acc0.x += u.x; acc0.y += u.y; acc0.z += u.z; acc0.w += u.w;
-      }
-      g = make_float4(acc0.x + acc1.x, acc0.y + acc1.y, acc0.z + acc1.z, acc0.w + acc1.w);
+      g = acc;
     } else {
       g = *reinterpret_cast<const float4*>(a.grad + pidx);
     }
     if (a.write_grad) *reinterpret_cast<float4*>(a.grad + pidx) = g;
     if (a.do_adam) {
-      float4 m = *reinterpret_cast<const float4*>(a.m + pidx);
-      float4 v = *reinterpret_cast<const float4*>(a.v + pidx);
-      float4 p = *reinterpret_cast<const float4*>(a.param + pidx);
+      // the step's Adam constants (state->t was already advanced for this step by
+      // the bound kernel / adam_tick_kernel); read after the data loads are issued
+      const AdamState st = *a.state;
+      const float scale = a.grad_scale_override > 0.f ? a.grad_scale_override : st.grad_scale;
+      const float t = (float)st.t;
+      const float b1p = powf(st.b1, t), b2p = powf(st.b2, t);
+      const float alpha = st.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+      const float omb1 = 1.f - st.b1, omb2 = 1.f - st.b2, eps = st.eps;
       float gg[4] = {g.x * scale, g.y * scale, g.z * scale, g.w * scale};
       float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w}, pp[4] = {p.x, p.y, p.z, p.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         mm[q] = mm[q] + (gg[q] - mm[q]) * omb1;
         vv[q] = vv[q] + (gg[q] * gg[q] - vv[q]) * omb2;
-        pp[q] = pp[q] - (mm[q] * alpha) / (sqrtf(vv[q]) + st.eps);
+        pp[q] = pp[q] - (mm[q] * alpha) / (sqrtf(vv[q]) + eps);
       }
       *reinterpret_cast<float4*>(a.m + pidx) = make_float4(mm[0], mm[1], mm[2], mm[3]);
       *reinterpret_cast<float4*>(a.v + pidx) = make_float4(vv[0], vv[1], vv[2], vv[3]);
@@ -607,6 +620,23 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
         }
       }
     }
+}
+
+// Flat grid over every segment's float4s (one float4 per thread): each wave
+// walks the segment table with uniform scalar loads and updates the
+// float4s of the segments it overlaps -- no per-thread loop, so every load of
+// the update is in flight at once.
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+  const long long gi = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long g0 = gi - (threadIdx.x & 63);
+  long long c = 0;
+  for (int s = 0; s < a.nseg; ++s) {
+    const long long n4 = a.seg[s].n >> 2;     // segment sizes and offsets are multiples of 4 floats
+    if (g0 + 64 > c && g0 < c + n4) {
+      const long long i = gi - c;
+      if (i >= 0 && i < n4) adam_one(a, a.seg[s], i);
+    }
+    c += n4;
   }
 }
 
@@ -615,10 +645,12 @@ __global__ void adam_tick_kernel(AdamState* s) { s->t += 1; }
 hipError_t launch_adam(hipStream_t st, const AdamArgs& a, long long max_seg_n) {
   if (a.nseg <= 0) return hipSuccess;
   if (a.do_adam && a.tick) hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(1), 0, st, a.state);
-  long long bx = (max_seg_n / 4 + 255) / 256;
-  if (bx > 64) bx = 64;
-  if (bx < 1) bx = 1;
-  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)bx, a.nseg), dim3(256), 0, st, a);
+  (void)max_seg_n;
+  long long n4 = 0;
+  for (int s = 0; s < a.nseg; ++s) n4 += a.seg[s].n >> 2;
+  const long long bx = (n4 + 255) / 256;
+  if (bx < 1) return hipSuccess;
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)bx), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

@@ -28,6 +28,26 @@
 
 namespace iwae {
 
+#ifdef IWAE_GEMM_TRACE
+// Debug build only (-DIWAE_GEMM_TRACE): 100 MHz timestamps of every workgroup
+// of the Bernoulli-epilogue GEMM at its phase boundaries.
+__device__ unsigned long long g_gemm_trace[32768];
+__device__ unsigned g_gemm_trace_n;
+#define GT_OPEN()                                                               \
+  int gt_ = -1;                                                                \
+  if (EPI == EPI_BERN && threadIdx.x == 0) {                                   \
+    const unsigned long long t_ = wall_clock64();                              \
+    gt_ = (int)atomicAdd(&g_gemm_trace_n, 8u);                                 \
+    if (gt_ + 8 > 32768) gt_ = -1;                                             \
+    else { g_gemm_trace[gt_] = (unsigned long long)(by * 4096 + bx); g_gemm_trace[gt_ + 1] = t_; } \
+  }
+#define GT(slot) \
+  if (gt_ >= 0) g_gemm_trace[gt_ + (slot)] = wall_clock64();
+#else
+#define GT_OPEN()
+#define GT(slot)
+#endif
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -67,6 +87,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
   float* As = smem;
   float* Bs = smem + 2 * BK * LDSA;
 
+  GT_OPEN()
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int m0 = by * BM, n0 = bx * BN;
@@ -74,7 +95,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
   const int kend = min(a.K, kbeg + a.kchunk);
   const int M = a.M, N = a.N;
 
-  float4 ra[A_F4], rb[B_F4];
+  // f32 64x64 tiles keep D K-slices in flight (the train-step GEMMs have K <= 4 slices:
+  // every load is issued before the first MFMA instead of one latency per slice)
+  constexpr int D = (!X3 && TM == 1 && TN == 1) ? 4 : 1;
+  float4 ra[D][A_F4], rb[D][B_F4];
   // x3 with pre-split B (the weights' F / G copies): [n][ldbx] bf16 rows copied as is
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   constexpr int B_X = X3 ? (BN * BK * 2 / 16) / NTH : 1;     // 16-byte chunks per thread (hi; lo alike)
@@ -90,7 +114,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
 
   const __amdgpu_buffer_rsrc_t rsBh = buf_rsrc(preB ? a.Bhi + (size_t)n0 * a.ldbx + kbeg : nullptr);
   const __amdgpu_buffer_rsrc_t rsBl = buf_rsrc(preB ? a.Blo + (size_t)n0 * a.ldbx + kbeg : nullptr);
-  auto gload = [&](int k0) {      // k0 relative to kbeg
+  auto gload = [&](int k0, int sl) {      // k0 relative to kbeg; sl: register slot
     if (preB) {
 #pragma unroll
       for (int i = 0; i < B_X; ++i) {
@@ -116,7 +140,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
         const int gk = k0 + kr;
         off = (gk < klen && m0 + 4 * mq < M) ? (unsigned)(gk * a.lda + 4 * mq) * 4u : kOOB;
       }
-      ra[i] = bld4(rsA, off);
+      ra[sl][i] = bld4(rsA, off);
     }
 #pragma unroll
     for (int i = 0; i < B_F4; ++i) {
@@ -131,11 +155,11 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
           const float s = a.kscale[kbeg + min(gk, klen - 1)];
           v.x *= s; v.y *= s; v.z *= s; v.w *= s;
         }
-        rb[i] = v;
+        rb[sl][i] = v;
       } else {
         const int nr = f / (BK / 4), kq = f % (BK / 4);
         const int gk = k0 + 4 * kq;
-        rb[i] = bld4(rsB, (n0 + nr < N && gk < klen) ? (unsigned)(nr * a.ldb + gk) * 4u : kOOB);
+        rb[sl][i] = bld4(rsB, (n0 + nr < N && gk < klen) ? (unsigned)(nr * a.ldb + gk) * 4u : kOOB);
       }
     }
   };
@@ -150,7 +174,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
     for (int i = 0; i < A_F4; ++i) {
       const int f = tid + i * NTH;
       bf16x4 hi, lo;
-      split4(ra[i], hi, lo);
+      split4(ra[0][i], hi, lo);
       if (!TA) {
         const int mr = f / (BK / 4), kq = f % (BK / 4);
         *reinterpret_cast<bf16x4*>(Hh + mr * LDK + 4 * kq) = hi;
@@ -178,7 +202,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
     for (int i = 0; i < B_F4; ++i) {
       const int f = tid + i * NTH;
       bf16x4 hi, lo;
-      split4(rb[i], hi, lo);
+      split4(rb[0][i], hi, lo);
       if (!TB) {
         const int kr = f % BK, nq = f / BK;
 #pragma unroll
@@ -194,7 +218,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
     }
   };
 
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, int sl) {
     if constexpr (X3) { xstore(buf); return; }
     float* Ab = As + buf * BK * LDSA;
     float* Bb = Bs + buf * BK * LDSB;
@@ -203,13 +227,13 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
       const int f = tid + i * NTH;
       if (!TA) {
         const int mr = f / (BK / 4), kq = f % (BK / 4);
-        Ab[(4 * kq + 0) * LDSA + mr] = ra[i].x;
-        Ab[(4 * kq + 1) * LDSA + mr] = ra[i].y;
-        Ab[(4 * kq + 2) * LDSA + mr] = ra[i].z;
-        Ab[(4 * kq + 3) * LDSA + mr] = ra[i].w;
+        Ab[(4 * kq + 0) * LDSA + mr] = ra[sl][i].x;
+        Ab[(4 * kq + 1) * LDSA + mr] = ra[sl][i].y;
+        Ab[(4 * kq + 2) * LDSA + mr] = ra[sl][i].z;
+        Ab[(4 * kq + 3) * LDSA + mr] = ra[sl][i].w;
       } else {
         const int kr = f / (BM / 4), mq = f % (BM / 4);
-        *reinterpret_cast<float4*>(Ab + kr * LDSA + 4 * mq) = ra[i];
+        *reinterpret_cast<float4*>(Ab + kr * LDSA + 4 * mq) = ra[sl][i];
       }
     }
 #pragma unroll
@@ -217,13 +241,13 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
       const int f = tid + i * NTH;
       if (!TB) {
         const int kr = f / (BN / 4), nq = f % (BN / 4);
-        *reinterpret_cast<float4*>(Bb + kr * LDSB + 4 * nq) = rb[i];
+        *reinterpret_cast<float4*>(Bb + kr * LDSB + 4 * nq) = rb[sl][i];
       } else {
         const int nr = f / (BK / 4), kq = f % (BK / 4);
-        Bb[(4 * kq + 0) * LDSB + nr] = rb[i].x;
-        Bb[(4 * kq + 1) * LDSB + nr] = rb[i].y;
-        Bb[(4 * kq + 2) * LDSB + nr] = rb[i].z;
-        Bb[(4 * kq + 3) * LDSB + nr] = rb[i].w;
+        Bb[(4 * kq + 0) * LDSB + nr] = rb[sl][i].x;
+        Bb[(4 * kq + 1) * LDSB + nr] = rb[sl][i].y;
+        Bb[(4 * kq + 2) * LDSB + nr] = rb[sl][i].z;
+        Bb[(4 * kq + 3) * LDSB + nr] = rb[sl][i].w;
       }
     }
   };
@@ -238,16 +262,25 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
 
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   if (nk > 0) {
-    gload(0);
-    sstore(0);
+#pragma unroll
+    for (int d = 0; d + 1 < D; ++d)
+      if (d < nk) gload(d * BK, d);
+    if (D == 1) gload(0, 0);
+    sstore(0, 0);
   }
   __syncthreads();
+  GT(2)
   const int arow = wm * TM * 32 + (lane & 31);
   const int brow = wn * TN * 32 + (lane & 31);
   const int khalf = lane >> 5;
-  for (int t = 0; t < nk; ++t) {
+  constexpr int PF = D > 1 ? D - 1 : 1;      // prefetch distance in slices
+  for (int t0 = 0; t0 < nk; t0 += D) {
+#pragma unroll
+   for (int d = 0; d < D; ++d) {
+    const int t = t0 + d;
+    if (t >= nk) break;
     const int cur = t & 1;
-    if (t + 1 < nk) gload((t + 1) * BK);
+    if (t + PF < nk) gload((t + PF) * BK, (d + PF) % D);
     if constexpr (X3) {
       // bf16x3 on v_mfma_f32_32x32x16_bf16: lane l holds row l&31, k = 8(l>>5)..+7
       const __bf16* Hh = ximg(cur, 0);
@@ -277,7 +310,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
           }
       }
-      if (t + 1 < nk) sstore(cur ^ 1);
+      if (t + 1 < nk) sstore(cur ^ 1, 0);
       __syncthreads();
       continue;
     }
@@ -297,10 +330,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < nk) sstore(cur ^ 1);
+    if (t + 1 < nk) sstore(cur ^ 1, (d + 1) % D);
     __syncthreads();
+   }
   }
 
+  GT(3)
   // ---------------------------------------------------------------- epilogue
   float* C = a.C + (size_t)bz * a.c_split_stride;
   const int rowq = 4 * (lane >> 5);
@@ -365,13 +400,44 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
         const int mt = m0 + wm * TM * 32 + i * 32;
         const int div = a.x_row_div;
         const int i0 = min(mt, M - 1) / div, b1 = (i0 + 1) * div;
+        if (div >= 32) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = min(mt + (r & 3) + 8 * (r >> 2) + rowq, M - 1);
-          const int img = div >= 32 ? i0 + (m >= b1 ? 1 : 0) : m / div;
-          xs[r] = a.aux[(size_t)img * a.ldaux + nc];
+          for (int r = 0; r < 16; ++r) {
+            const int m = min(mt + (r & 3) + 8 * (r >> 2) + rowq, M - 1);
+            xs[r] = a.aux[(size_t)(i0 + (m >= b1 ? 1 : 0)) * a.ldaux + nc];
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = min(mt + (r & 3) + 8 * (r >> 2) + rowq, M - 1);
+            xs[r] = a.aux[(size_t)(m / div) * a.ldaux + nc];
+          }
         }
-        if (!a.store_g && !a.need_bce) {
+        // binarised pixels (every image of the hot path), decided once per wave tile
+        bool bin = true;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bin = bin && (xs[r] == 0.f || xs[r] == 1.f);
+        bin = __all(bin);
+        if (bin && !a.need_bce && a.wb == 0.f) {
+          // p = sigmoid(l)*(1-1e-6)+1e-7 >= 1e-7, so the raw v_log / v_rcp are exact
+          // to an ulp here; log(1-p) stands in for log1p(-p) (< 1e-7 absolute apart).
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int ml = (r & 3) + 8 * (r >> 2) + rowq;
+            const int m = mt + ml;
+            const bool ok = (m < M && n < N);
+            const float s = frcp(1.f + fexp(-t[r]));
+            const float p = __fadd_rn(__fmul_rn(s, kProbScale), kProbShift);
+            const bool one = xs[r] != 0.f;
+            const float sel = one ? p : 1.f - p;
+            S[ml * 33 + (lane & 31)] = ok ? kLn2 * __builtin_amdgcn_logf(sel) : 0.f;
+            if (a.store_g && ok) {
+              const float g = one ? frcp(sel) : -frcp(sel);
+              C[(size_t)m * a.ldc + n] = (a.wa * g) * (kProbScale * (s * (1.f - s)));
+            }
+            vb[r] = 0.f;
+          }
+        } else if (!a.store_g && !a.need_bce) {
           // log-probability only (NLL / bounds without a backward pass)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -462,6 +528,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
     if constexpr (TM > 1 && TN > 1) bern_tile(acc[TM - 1][TN - 1], TM - 1, TN - 1);
     static_assert(TM <= 2 && TN <= 2, "bern_tile dispatch covers up to 2x2 tiles");
   }
+  GT(4)
 }
 
 // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs
@@ -664,3 +731,18 @@ hipError_t launch_gemm(hipStream_t st, GemmKind kind, GemmEpi epi, int tile, int
 }
 
 }  // namespace iwae
+
+#ifdef IWAE_GEMM_TRACE
+extern "C" int iwae_gemm_trace_dump(unsigned long long* out, int cap) {
+  unsigned n = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(iwae::g_gemm_trace_n), sizeof(n)) != hipSuccess) return -1;
+  n = n > 32768u ? 32768u : n;
+  const int m = (int)n < cap ? (int)n : cap;
+  if (m > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(iwae::g_gemm_trace), m * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  unsigned zero = 0;
+  hipMemcpyToSymbol(HIP_SYMBOL(iwae::g_gemm_trace_n), &zero, sizeof(zero));
+  return m;
+}
+#endif

@@ -17,6 +17,7 @@
 namespace iwae {
 
 constexpr float kProbScale = 0.999999f;      // F:126  (1-10**(-6)) as float32
+constexpr float kLn2 = 0.693147180559945309f;
 constexpr float kProbShift = 1e-7f;          // F:126  10**(-7)
 constexpr float kScaleEps = 1e-6f;           // F:37
 constexpr float kKerasEps = 1e-7f;           // keras.backend.epsilon()

@@ -295,7 +295,11 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
     for (auto& d : h->dense) {
       const long long R = d.rows_kind == 0 ? Bimg : rows;
       const long long tiles = cdiv(d.fin + 1, 64) * cdiv(d.fout, 64);
-      long long S = std::max(1LL, cdiv(768, tiles));
+      static const long long kSlabTarget = [] {      // tuning knob: split-K target workgroups per layer
+        const char* e = std::getenv("IWAE_DW_TARGET");
+        return e ? std::max(1LL, std::atoll(e)) : 768LL;
+      }();
+      long long S = std::max(1LL, cdiv(kSlabTarget, tiles));
       S = std::min(S, std::max(1LL, cdiv(R, 64)));
       d.max_splits = (int)S;
       d.slab_off = (long long)slab_total;
