@@ -68,6 +68,25 @@ __device__ __forceinline__ float4 philox_normal4(uint64_t seed, uint64_t base, u
   return make_float4(r0 * __builtin_amdgcn_cosf(u1), r0 * __builtin_amdgcn_sinf(u1),
                      r1 * __builtin_amdgcn_cosf(u3), r1 * __builtin_amdgcn_sinf(u3));
 }
+// Normals 2*half and 2*half+1 of philox_normal4(...) (bitwise the same values):
+// one Box-Muller pair, for a lane that owns two of the four columns.
+__device__ __forceinline__ float2 philox_normal2(uint64_t seed, uint64_t base, unsigned row, unsigned layer,
+                                                 unsigned grp, bool half) {
+  unsigned c0 = row, c1 = (layer << 20) | grp, c2 = (unsigned)base, c3 = (unsigned)(base >> 32);
+  unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const unsigned lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const unsigned lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  constexpr float k2m32 = 2.3283064365386963e-10f;
+  const unsigned ca = half ? c2 : c0, cb = half ? c3 : c1;
+  const float ua = ((float)ca + 0.5f) * k2m32, ub = ((float)cb + 0.5f) * k2m32;
+  const float r = __builtin_amdgcn_sqrtf(-1.38629436f * __builtin_amdgcn_logf(ua));
+  return make_float2(r * __builtin_amdgcn_cosf(ub), r * __builtin_amdgcn_sinf(ub));
+}
 __device__ __forceinline__ float f4_at(const float4& v, int q) {
   return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
 }
@@ -350,17 +369,20 @@ hipError_t rb_setup_attributes();
 // with the layers' pre-split F copies streamed from L2 into registers.
 constexpr int kMgMaxStages = 24;
 constexpr int kMgMaxBufs = 12;
-enum MgAct { MG_NONE = 0, MG_TANH = 1, MG_BERN = 2 };
-enum MgPost { MGP_NONE = 0, MGP_SAMPLE = 1, MGP_PRIOR = 2 };
+// Stage kinds.  A head stage (SAMPLE / PRIOR) computes the (mu | zs) outputs
+// of a stochastic layer with its weight rows permuted into groups of 8 --
+// [mu 4q..4q+3 | zs 4q..4q+3] -- so the lanes holding mu_j and zs_j are 16
+// apart and the sampling / prior density runs in the MFMA epilogue.
+enum MgAct { MG_NONE = 0, MG_TANH = 1, MG_BERN = 2, MG_SAMPLE = 3, MG_PRIOR = 4 };
 struct MgStage {
   const __bf16* Whi; const __bf16* Wlo; unsigned W_bytes;
-  int ldk, K, N;             // F [N][ldk]; K = fin + 1 (input ones column at K - 1)
-  int in_buf, out_buf;       // LDS buffer ids
+  int ldk, K, N;             // F [rows][ldk]; K = fin + 1 (input ones column at K - 1);
+                             // N = output features (head stages: 8 * ceil(d / 4) permuted)
+  int in_buf, out_buf;       // LDS buffer ids; out_buf: TANH output, SAMPLE destination h_i,
+                             // PRIOR target h_t (read)
   int act;                   // MgAct
-  int post, post_buf, d;     // MgPost on the output (mu | zs): SAMPLE -> post_buf, PRIOR target post_buf
-  int layer, stdnormal;      // SAMPLE: Philox layer; add log N(h; 0, 1) to log p
-  int next_k;                // padded K of the next reader of out_buf (ones column + zero pad); N if none
-  int post_next_k;           // SAMPLE: padded K of the reader of post_buf
+  int d, layer, stdnormal;   // head stages: latent width, Philox layer, add log N(h; 0, 1)
+  int next_k;                // TANH / SAMPLE: padded K of the reader of out_buf (ones column + zero pad)
 };
 struct MgLaunch {
   MgStage st[kMgMaxStages]; int nst;

@@ -1533,18 +1533,22 @@ int iwae_e_log_px(iwae_handle* h, const float* x, int B, int k, const float* con
 }
 
 // ------------------------------------------------ fused k-sample forward
-// Plan of mega_fwd_kernel for this model (iwae_mega.hip): LDS buffers h_0 ..
-// h_{L-2} (kept), scratch P and Q (h_{L-1} lives in Q), the Dense stages after
-// the first encoder layer with their post ops.  False if it does not fit.
+// Plan of mega_fwd_kernel for this model (iwae_mega.hip).  LDS buffers: h_0 ..
+// h_{L-2} kept (ids 0 .. L-2), scratch P (id L-1, also holds h_{L-1}) and Q
+// (id L).  Stages after the first encoder layer:
+//   encoder i = 1..L-1:  h_{i-1} -> P (tanh) -> Q (tanh) -> head: sample h_i
+//   decoder prior j:     h_{L-1-j} -> Q -> P -> head: log p(h_{L-2-j} | .)
+//   output MLP:          h_0 -> Q -> P -> Dense(784) + Bernoulli
+// False if it does not fit the LDS.
 static bool mega_plan(iwae_handle* h, MgLaunch& M, int& rt, size_t& lds) {
   const int L = h->L;
   std::memset(&M, 0, sizeof(M));
   auto r32 = [](int x) { return (x + 31) & ~31; };
-  const int bP = L - 1, bQ = L;                 // scratch buffer ids
-  auto hbuf = [&](int i) { return i == L - 1 ? bQ : i; };
-  int nb = L + 1;
+  const int bP = L - 1, bQ = L;
+  auto hbuf = [&](int i) { return i == L - 1 ? bP : i; };
+  const int nb = L + 1;
   if (nb > kMgMaxBufs) return false;
-  int sw = 0;                                   // scratch width
+  std::vector<int> width(nb, 0);
   std::vector<MgStage> st;
   auto stage = [&](int di, int in, int out, int act, int next_k) {
     const DenseL& d = h->dense[di];
@@ -1553,54 +1557,61 @@ static bool mega_plan(iwae_handle* h, MgLaunch& M, int& rt, size_t& lds) {
     S.W_bytes = (unsigned)((h->wsplit_elems - d.f_off) * (long long)sizeof(__bf16));
     S.ldk = d.ldF; S.K = d.fin + 1; S.N = d.fout;
     S.in_buf = in; S.out_buf = out; S.act = act; S.next_k = next_k;
-    if (in == bP || in == bQ) sw = std::max(sw, S.ldk);
-    if (out == bP || out == bQ) sw = std::max(sw, std::max(S.N, next_k));
+    width[in] = std::max(width[in], S.ldk);
+    if (act == MG_TANH) width[out] = std::max(width[out], std::max(S.N, next_k));
     st.push_back(S);
     return (int)st.size() - 1;
+  };
+  auto head = [&](int di, int in, int out, int act, int dd, int layer, int stdnormal) {
+    const int s = stage(di, in, out, act, r32(dd + 1));
+    st[s].N = 8 * ((dd + 3) / 4);
+    st[s].d = dd; st[s].layer = layer; st[s].stdnormal = stdnormal;
+    width[out] = std::max(width[out], r32(dd + 1));
   };
   for (int i = 1; i < L; ++i) {
     const StochL& E = h->enc[i];
     stage(E.l1, hbuf(i - 1), bP, MG_TANH, h->dense[E.l2].ldF);
     stage(E.l2, bP, bQ, MG_TANH, h->dense[E.head].ldF);
-    const int s = stage(E.head, bQ, bP, MG_NONE, h->dense[E.head].fout);
-    st[s].post = MGP_SAMPLE; st[s].post_buf = hbuf(i); st[s].d = E.d; st[s].layer = i;
-    st[s].stdnormal = i == L - 1; st[s].post_next_k = r32(E.d + 1);
-    if (hbuf(i) == bQ) sw = std::max(sw, r32(E.d + 1));
+    head(E.head, bQ, hbuf(i), MG_SAMPLE, E.d, i, i == L - 1);
   }
   for (int j = 0; j < L - 1; ++j) {
     const StochL& D = h->dec[j];
-    stage(D.l1, hbuf(L - 1 - j), bP, MG_TANH, h->dense[D.l2].ldF);
-    stage(D.l2, bP, bQ, MG_TANH, h->dense[D.head].ldF);
-    const int s = stage(D.head, bQ, bP, MG_NONE, h->dense[D.head].fout);
-    st[s].post = MGP_PRIOR; st[s].post_buf = hbuf(L - 2 - j); st[s].d = D.d;
+    stage(D.l1, hbuf(L - 1 - j), bQ, MG_TANH, h->dense[D.l2].ldF);
+    stage(D.l2, bQ, bP, MG_TANH, h->dense[D.head].ldF);
+    head(D.head, bP, hbuf(L - 2 - j), MG_PRIOR, D.d, 0, 0);
   }
   const int h0 = hbuf(0);
-  const int o1out = h0 == bQ ? bP : bQ, o2out = o1out == bP ? bQ : bP;
-  stage(h->o1, h0, o1out, MG_TANH, h->dense[h->o2].ldF);
-  stage(h->o2, o1out, o2out, MG_TANH, h->dense[h->o3].ldF);
-  stage(h->o3, o2out, -1, MG_BERN, 0);
+  stage(h->o1, h0, bQ, MG_TANH, h->dense[h->o2].ldF);
+  stage(h->o2, bQ, bP, MG_TANH, h->dense[h->o3].ldF);
+  stage(h->o3, bP, -1, MG_BERN, 0);
   if ((int)st.size() > kMgMaxStages) return false;
-  if (h0 == bQ) sw = std::max(sw, r32(h->enc[0].d + 1));
-  // LDS layout: each buffer = hi and lo bf16 planes [R][ld]; ld = width + 8
-  // (16-byte aligned rows that start 4 banks apart); then logq, logp [R] and
-  // the [8][R] reduction scratch as floats
-  for (int b = 0; b < nb; ++b) {
-    const int w = (b == bP || b == bQ) ? sw : r32(h->enc[b].d + 1);
-    M.buf_ld[b] = w + 8;
-  }
+  width[h0] = std::max(width[h0], r32(h->enc[0].d + 1));
+  // LDS layout: each buffer = hi and lo bf16 planes [R][ld], then logq, logp [R]
+  // and the [8][R] reduction scratch as floats.  Row stride s dwords (ld = 2s):
+  // s = 8 mod 16 makes the fragment reads (ds_read_b128) conflict-free; s = 4
+  // mod 8 (2-way) is the fallback when that does not fit.
   for (int c : {4, 2, 1}) {
     const int R = 16 * c;
-    int off = 0;                                // bf16 units
-    for (int b = 0; b < nb; ++b) { M.buf_off[b] = off; off += 2 * R * M.buf_ld[b]; }
-    M.acc_off = (off + 3) / 2 & ~1;             // floats
-    const size_t bytes = (size_t)(M.acc_off + 2 * R + 8 * R) * sizeof(float);
-    if (bytes <= 160 * 1024) {
-      rt = c;
-      lds = bytes;
-      for (size_t i = 0; i < st.size(); ++i) M.st[i] = st[i];
-      M.nst = (int)st.size();
-      M.h0_buf = h0; M.d0 = h->enc[0].d; M.h0_next_k = r32(h->enc[0].d + 1); M.h0_stdnormal = L == 1;
-      return true;
+    for (int pass = 0; pass < 2; ++pass) {
+      int off = 0;                              // bf16 units
+      for (int b = 0; b < nb; ++b) {
+        int sdw = (std::max(width[b], 32) + 1) / 2;
+        if (pass == 0) while (sdw % 16 != 8) ++sdw;
+        else while (sdw % 8 != 4) ++sdw;
+        M.buf_ld[b] = 2 * sdw;
+        M.buf_off[b] = off;
+        off += 2 * R * M.buf_ld[b];
+      }
+      M.acc_off = (off + 3) / 2 & ~1;           // floats
+      const size_t bytes = (size_t)(M.acc_off + 2 * R + 8 * R) * sizeof(float);
+      if (bytes <= 160 * 1024) {
+        rt = c;
+        lds = bytes;
+        for (size_t i = 0; i < st.size(); ++i) M.st[i] = st[i];
+        M.nst = (int)st.size();
+        M.h0_buf = h0; M.d0 = h->enc[0].d; M.h0_next_k = r32(h->enc[0].d + 1); M.h0_stdnormal = L == 1;
+        return true;
+      }
     }
   }
   return false;

@@ -300,6 +300,34 @@ def test_nll_k5000_matches_oracle_within_0p05_nats(layers):
     assert abs(nll_gpu - ref) <= 5e-3, (nll_gpu, ref)
 
 
+@pytest.mark.parametrize("arch", [([64], [64], [16], [784]), ([40], [40], [6], [784]),
+                                  ([64, 32], [32, 64], [32, 16], [32, 784]),
+                                  ([48, 32, 24], [24, 32, 48], [20, 12, 8], [12, 20, 784]),
+                                  ([200, 100], [100, 200], [100, 50], [100, 784])])
+@pytest.mark.parametrize("pixels", ["binary", "fractional"])
+def test_fused_nll_kernel_matches_layerwise_path(arch, pixels):
+    """The fused k-sample kernel (activations in LDS, sampling and prior density
+    in the MFMA epilogue, product-of-probabilities Bernoulli sum) and the
+    layer-wise GEMM path give the same per-image log p(x) on the same Philox
+    noise; fractional pixels take the two-log Bernoulli form."""
+    he, hd, le, ld = arch
+    rng = np.random.default_rng(23)
+    x = rng.random((5, 784)).astype(np.float32)
+    if pixels == "binary":
+        x = (x < 0.25).astype(np.float32)
+    out = {}
+    for path in ("layerwise", "fused"):
+        m = make_model(he, hd, le, ld, seed=41, kernel_path=path)
+        if path == "layerwise":
+            w0 = m.get_weights()
+        else:
+            m.set_weights(w0)
+        out[path] = m.log_px(x, 700).cpu().numpy().astype(np.float64)
+    a, b = out["layerwise"], out["fused"]
+    assert np.all(np.isfinite(b))
+    np.testing.assert_allclose(b, a, rtol=2e-5, atol=2e-3)
+
+
 def test_nll_chunking_and_sample_split_are_consistent():
     O, spec, params, m, x, rng = _concentrated_model(4, (64, 32), (32, 16))
     a = m.log_px(x, 3000, chunk=6).cpu().numpy()
