@@ -260,6 +260,35 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  // Bernoulli epilogue pixels x[image(row)][n] of one 32x32 accumulator tile
+  // (clamped, unconditional buffer loads).  The image of each row: the 32-row
+  // tile crosses at most one image boundary when x_row_div >= 32.
+  const int rowq_ = 4 * (lane >> 5);
+  auto load_x = [&](const int i, const int j, float (&xs)[16]) {
+    const __amdgpu_buffer_rsrc_t rsx = buf_rsrc(a.aux);
+    const int n = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+    const int nc = min(n, N - 1);
+    const int mt = m0 + wm * TM * 32 + i * 32;
+    const int div = a.x_row_div;
+    const int i0 = min(mt, M - 1) / div, b1 = (i0 + 1) * div;
+    if (div >= 32) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = min(mt + (r & 3) + 8 * (r >> 2) + rowq_, M - 1);
+        xs[r] = bld1(rsx, (unsigned)((i0 + (m >= b1 ? 1 : 0)) * a.ldaux + nc) * 4u);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = min(mt + (r & 3) + 8 * (r >> 2) + rowq_, M - 1);
+        xs[r] = bld1(rsx, (unsigned)((m / div) * a.ldaux + nc) * 4u);
+      }
+    }
+  };
+  // one tile per wave: its pixels are requested now, in flight during the K loop
+  float xs_pre[16];
+  if constexpr (EPI == EPI_BERN && TM == 1 && TN == 1) load_x(0, 0, xs_pre);
+
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   if (nk > 0) {
 #pragma unroll
@@ -392,26 +421,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
         const int ncol0 = n0 + wn * TN * 32 + j * 32;
         const int n = ncol0 + (lane & 31);
         float vb[16], xs[16];
-        // pixels of all 16 elements requested before the first store (clamped,
-        // unconditional; out-of-tile elements are masked below)
-        const int nc = min(n, N - 1);
-        // image of each row: the 32-row tile crosses at most one image boundary
-        // when x_row_div >= 32 (one division per tile instead of one per element)
         const int mt = m0 + wm * TM * 32 + i * 32;
-        const int div = a.x_row_div;
-        const int i0 = min(mt, M - 1) / div, b1 = (i0 + 1) * div;
-        if (div >= 32) {
+        if constexpr (TM == 1 && TN == 1) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int m = min(mt + (r & 3) + 8 * (r >> 2) + rowq, M - 1);
-            xs[r] = a.aux[(size_t)(i0 + (m >= b1 ? 1 : 0)) * a.ldaux + nc];
-          }
+          for (int r = 0; r < 16; ++r) xs[r] = xs_pre[r];
         } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int m = min(mt + (r & 3) + 8 * (r >> 2) + rowq, M - 1);
-            xs[r] = a.aux[(size_t)(m / div) * a.ldaux + nc];
-          }
+          load_x(i, j, xs);
         }
         // binarised pixels (every image of the hot path), decided once per wave tile
         bool bin = true;
@@ -622,17 +637,22 @@ static hipError_t dispatch_tile(hipStream_t st, GemmKind kind, GemmEpi epi, int 
 // 16-byte LDS read feeds 4 MFMAs and, for bt = 1, one 16-byte weight load does.
 constexpr int SM_WAVES = 8;
 constexpr int SM_MAXU = 8;          // 16-deep k groups per wave (K <= 8 * 16 * 8 = 1024)
+constexpr int SM_MAX_ASLABS = 4;    // partial slabs a reader sums while staging A
 
 __global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm_lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int t = blockIdx.x;
+  const int t = blockIdx.x, ks = blockIdx.y;
   const int n = t * 16 + r;
-  const int Kp = (a.K + 15) & ~15, lds_ld = Kp + 4;
+  // this workgroup's K range [kb0, kb0 + Kb)
+  const int KC = a.kslabs > 1 ? (((a.K + a.kslabs - 1) / a.kslabs) + 15) & ~15 : a.K;
+  const int kb0 = ks * KC;
+  const int Kb = max(0, min(KC, a.K - kb0));
+  const int Kp = (Kb + 15) & ~15, lds_ld = Kp + 4;
   float* As = sm_lds;                                  // [32][lds_ld]
   float* part = sm_lds + 32 * lds_ld;                  // [wave][rt][i][lane]
-  const int kc = (((a.K + SM_WAVES - 1) / SM_WAVES) + 15) & ~15;
+  const int kc = (((Kb + SM_WAVES - 1) / SM_WAVES) + 15) & ~15;
   const int kb = wave * kc;
   const int nu = min(SM_MAXU, max(0, (min(kc, Kp - kb) + 15) >> 4));
   // weights of this wave's k range, requested first (they do not depend on A)
@@ -644,26 +664,52 @@ __global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
     const bool ok = u < nu && n < a.N;
     if (a.bt) {
       // W[n][k0..k0+3]: one 16-byte load (k beyond K reads the row's zero padding or 0)
-      bq[u] = bld4(rW, (ok && k0 < a.K) ? (unsigned)(n * a.ldw + k0) * 4u : kOOB);
+      bq[u] = bld4(rW, (ok && k0 < Kb) ? (unsigned)(n * a.ldw + kb0 + k0) * 4u : kOOB);
     } else {
       float e[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        e[j] = bld1(rW, (ok && k0 + j < a.K) ? (unsigned)((k0 + j) * a.ldw + n) * 4u : kOOB);
+        e[j] = bld1(rW, (ok && k0 + j < Kb) ? (unsigned)((kb0 + k0 + j) * a.ldw + n) * 4u : kOOB);
       bq[u] = make_float4(e[0], e[1], e[2], e[3]);
     }
   }
   // activations -> LDS (rows >= M and k >= K zero)
   const __amdgpu_buffer_rsrc_t rA = buf_rsrc(a.A);
   const int q4 = Kp >> 2;
+  const bool write_a = a.a_out != nullptr && blockIdx.x == 0 && ks == 0;
   for (int e = threadIdx.x; e < 32 * q4; e += blockDim.x) {
     const int row = e / q4, kq = e - row * q4;
-    const int k = 4 * kq;
-    float4 v = bld4(rA, (row < a.M && k < a.K) ? (unsigned)(row * a.lda + k) * 4u : kOOB);
-    if (k + 3 >= a.K) {          // zero the part of the last quad past K (the row's padding may hold the ones column)
-      if (k + 1 >= a.K) v.y = 0.f;
-      if (k + 2 >= a.K) v.z = 0.f;
-      if (k + 3 >= a.K) v.w = 0.f;
+    const int k = 4 * kq, gk = kb0 + k;
+    float4 v;
+    if (a.a_slabs > 0) {
+      // sum of the producer's partial slabs, activation, ones column at K - 1
+      // (all slab loads in flight at once: up to SM_MAX_ASLABS, slabs past a_slabs read 0)
+      float4 w[SM_MAX_ASLABS];
+#pragma unroll
+      for (int sl = 0; sl < SM_MAX_ASLABS; ++sl)
+        w[sl] = bld4(rA, (sl < a.a_slabs && row < a.M && k < Kb)
+                             ? (unsigned)(sl * a.a_slab + row * a.lda + gk) * 4u : kOOB);
+      float4 sacc = w[0];
+#pragma unroll
+      for (int sl = 1; sl < SM_MAX_ASLABS; ++sl) {
+        sacc.x += w[sl].x; sacc.y += w[sl].y; sacc.z += w[sl].z; sacc.w += w[sl].w;
+      }
+      float vv[4] = {sacc.x, sacc.y, sacc.z, sacc.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int col = gk + q;
+        float y = a.a_act ? ftanh(vv[q]) : vv[q];
+        if (write_a && row < a.M && col < a.K - 1) a.a_out[(size_t)row * a.a_ldo + col] = y;
+        vv[q] = (row < a.M && k + q < Kb) ? (col < a.K - 1 ? y : 1.f) : 0.f;
+      }
+      v = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    } else {
+      v = bld4(rA, (row < a.M && k < Kb) ? (unsigned)(row * a.lda + gk) * 4u : kOOB);
+      if (k + 3 >= Kb) {          // zero the part of the last quad past K (the row's padding may hold the ones column)
+        if (k + 1 >= Kb) v.y = 0.f;
+        if (k + 2 >= Kb) v.z = 0.f;
+        if (k + 3 >= Kb) v.w = 0.f;
+      }
     }
     *reinterpret_cast<float4*>(&As[row * lds_ld + k]) = v;
   }
@@ -701,6 +747,10 @@ __global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
   for (int w = 0; w < SM_WAVES; ++w) v += part[((w * 2 + rt) * 4 + i) * 64 + l];
   const int row = rt * 16 + 4 * (l >> 4) + i, col = t * 16 + (l & 15);
   if (row < a.M && col < a.N) {
+    if (a.kslabs > 1) {
+      a.C[(size_t)ks * a.c_slab + (size_t)row * a.ldc + col] = v;
+      return;
+    }
     if (a.act == 1) v = ftanh(v);
     else if (a.act == 2) {
       const float y = a.Y[(size_t)row * a.ldy + col];
@@ -712,10 +762,12 @@ __global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
 
 hipError_t launch_smallm(hipStream_t st, const SmArgs& a) {
   if (a.M <= 0 || a.N <= 0) return hipSuccess;
-  if (a.M > 32 || a.K > SM_WAVES * 16 * SM_MAXU) return hipErrorInvalidValue;
-  const int Kp = (a.K + 15) & ~15;
+  const int ksl = a.kslabs > 1 ? a.kslabs : 1;
+  const int KC = ksl > 1 ? (((a.K + ksl - 1) / ksl) + 15) & ~15 : a.K;
+  if (a.M > 32 || KC > SM_WAVES * 16 * SM_MAXU || a.a_slabs > SM_MAX_ASLABS) return hipErrorInvalidValue;
+  const int Kp = (KC + 15) & ~15;
   const size_t lds = (size_t)(32 * (Kp + 4) + SM_WAVES * 2 * 4 * 64) * sizeof(float);
-  hipLaunchKernelGGL(smallm_kernel, dim3((a.N + 15) / 16), dim3(SM_WAVES * 64), lds, st, a);
+  hipLaunchKernelGGL(smallm_kernel, dim3((a.N + 15) / 16, ksl), dim3(SM_WAVES * 64), lds, st, a);
   return hipGetLastError();
 }
 

@@ -160,6 +160,12 @@ struct SmArgs {
   float* C; int ldc;
   int M, N, K;
   int act; const float* Y; int ldy;
+  // split K over kslabs workgroup columns (blockIdx.y): partial sums into slabs
+  // C + ks * c_slab (no activation; the reader sums them)
+  int kslabs; long long c_slab;
+  // A given as a_slabs partial slabs of a pre-activation: staged as
+  // tanh(sum) (a_act) with the ones column at K - 1, and written once to a_out
+  int a_slabs; long long a_slab; int a_act; float* a_out; int a_ldo;
 };
 hipError_t launch_smallm(hipStream_t st, const SmArgs& a);
 hipError_t smallm_setup_attributes();

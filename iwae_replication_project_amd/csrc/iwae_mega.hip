@@ -154,31 +154,37 @@ __device__ __forceinline__ void mg_mma(const MgBuf& IN, int k0, int ns, MgFrag& 
                                        int pf_ns) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
+  // chunks of (k step u, row-tile pair p); the activation fragments of the next
+  // chunk are read from LDS while this chunk's MFMAs run (two register sets)
+  constexpr int RH = RT < 2 ? RT : 2;
+  constexpr int NP = RT / RH;
+  constexpr int NC = MG_KS * NP;
+  mg_bf16x8 ah[2][RH], al[2][RH];
+  auto rd = [&](int c, int b) {
+    const int u = c / NP, p = c % NP;
 #pragma unroll
-  for (int u = 0; u < MG_KS; ++u) {
-    if (u >= ns) break;
-    // row tiles in pairs: 16 fragment registers in flight instead of 8 * RT
-#pragma unroll
-    for (int r0 = 0; r0 < RT; r0 += 2) {
-      constexpr int RH = RT < 2 ? RT : 2;
-      mg_bf16x8 ah[RH], al[RH];
-#pragma unroll
-      for (int i = 0; i < RH; ++i) {
-        const int ao = ((r0 + i) * 16 + r) * IN.ld + k0 + 32 * u + 8 * g;
-        ah[i] = *reinterpret_cast<const mg_bf16x8*>(IN.hi + ao);
-        al[i] = *reinterpret_cast<const mg_bf16x8*>(IN.lo + ao);
-      }
-#pragma unroll
-      for (int i = 0; i < RH; ++i)
-        acc[r0 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.l[u], ah[i], acc[r0 + i], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < RH; ++i)
-        acc[r0 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], al[i], acc[r0 + i], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < RH; ++i)
-        acc[r0 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], ah[i], acc[r0 + i], 0, 0, 0);
+    for (int i = 0; i < RH; ++i) {
+      const int ao = ((p * RH + i) * 16 + r) * IN.ld + k0 + 32 * u + 8 * g;
+      ah[b][i] = *reinterpret_cast<const mg_bf16x8*>(IN.hi + ao);
+      al[b][i] = *reinterpret_cast<const mg_bf16x8*>(IN.lo + ao);
     }
-    if (u < MG_PF && pf) mg_fetch_step(rh, rl, pf_vb, u, pf_ns, f);
+  };
+  rd(0, 0);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int u = c / NP, p = c % NP, b = c & 1;
+    if (u >= ns) break;
+    if (c + 1 < NC && (c + 1) / NP < ns) rd(c + 1, b ^ 1);
+#pragma unroll
+    for (int i = 0; i < RH; ++i)
+      acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.l[u], ah[b][i], acc[p * RH + i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < RH; ++i)
+      acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], al[b][i], acc[p * RH + i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < RH; ++i)
+      acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], ah[b][i], acc[p * RH + i], 0, 0, 0);
+    if (p == NP - 1 && u < MG_PF && pf) mg_fetch_step(rh, rl, pf_vb, u, pf_ns, f);
   }
 }
 

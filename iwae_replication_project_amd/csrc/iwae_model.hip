@@ -814,8 +814,31 @@ static int fused_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool tr
   if (smallm_ok(h, P.Bimg)) {
     // (1') first encoder layer on the images: three N-split few-row launches
     const StochL& S0 = h->enc[0];
-    CHK(smallm(h, h->x_in, P.Bimg, h->dense[S0.l1], false, 1, nullptr, h->eb[0].y1));
-    CHK(smallm(h, h->eb[0].y1, P.Bimg, h->dense[S0.l2], false, 1, nullptr, h->eb[0].y2));
+    const DenseL& d1 = h->dense[S0.l1];
+    const int ksl = (int)std::min<long long>(std::min(4, h->fslab_S), cdiv(d1.fin + 1, 128));
+    if (ksl > 1) {
+      // the wide input layer split over K into partial slabs (more workgroups);
+      // the second layer sums them, applies tanh and stores y1 while staging
+      SmArgs a{};
+      a.A = h->x_in.p; a.lda = h->x_in.ld;
+      a.W = h->params + d1.off; a.ldw = d1.ldw;
+      a.C = h->fslab; a.ldc = h->eb[0].y1.ld;
+      a.M = P.Bimg; a.N = d1.fout; a.K = d1.fin + 1;
+      a.kslabs = ksl; a.c_slab = (long long)P.Bimg * a.ldc;
+      HIPCHK(launch_smallm(h->stream, a));
+      const DenseL& d2 = h->dense[S0.l2];
+      SmArgs b{};
+      b.A = h->fslab; b.lda = a.ldc;
+      b.a_slabs = ksl; b.a_slab = a.c_slab; b.a_act = 1; b.a_out = h->eb[0].y1.p; b.a_ldo = h->eb[0].y1.ld;
+      b.W = h->params + d2.off; b.ldw = d2.ldw;
+      b.C = h->eb[0].y2.p; b.ldc = h->eb[0].y2.ld;
+      b.M = P.Bimg; b.N = d2.fout; b.K = d2.fin + 1;
+      b.act = 1;
+      HIPCHK(launch_smallm(h->stream, b));
+    } else {
+      CHK(smallm(h, h->x_in, P.Bimg, h->dense[S0.l1], false, 1, nullptr, h->eb[0].y1));
+      CHK(smallm(h, h->eb[0].y1, P.Bimg, h->dense[S0.l2], false, 1, nullptr, h->eb[0].y2));
+    }
     CHK(smallm(h, h->eb[0].y2, P.Bimg, h->dense[S0.head], false, 0, nullptr, h->eb[0].P));
   } else
   // (1) first encoder Dense (K = 785) as a split-K GEMM into partial slabs
