@@ -42,3 +42,11 @@ for b in range(4):
         work = dn - ent
         print(f"  {nm:9s} enter {ent.min():7d}  work per wave min/max {work.min():6d}/{work.max():6d}  "
               f"barrier done {br.max():7d}  (stage {br.max() - ent.min():6d})")
+        f0, f1, f2 = a[b, :, 64 + 4 * s], a[b, :, 65 + 4 * s], a[b, :, 66 + 4 * s]
+        ok = (f0 > 0) & (f1 > 0) & (f2 > 0)
+        if ok.any():
+            fetch = (f0 - (a[b, :, 2 + 3 * s]))[ok]
+            mma = (f1 - f0)[ok]
+            epi = (f2 - f1)[ok]
+            print(f"            first tile: fetch-wait {int(np.median(fetch)):6d}  mfma-loop {int(np.median(mma)):6d}  "
+                  f"epilogue {int(np.median(epi)):6d}  (medians over waves)")
