@@ -674,7 +674,7 @@ __global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
     }
   }
   // activations -> LDS (rows >= M and k >= K zero)
-  const __amdgpu_buffer_rsrc_t rA = buf_rsrc(a.A);
+  const __amdgpu_buffer_rsrc_t rA = a.a_bytes ? buf_rsrc(a.A, a.a_bytes) : buf_rsrc(a.A);
   const int q4 = Kp >> 2;
   const bool write_a = a.a_out != nullptr && blockIdx.x == 0 && ks == 0;
   for (int e = threadIdx.x; e < 32 * q4; e += blockDim.x) {
@@ -705,10 +705,25 @@ __global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
       v = make_float4(vv[0], vv[1], vv[2], vv[3]);
     } else {
       v = bld4(rA, (row < a.M && k < Kb) ? (unsigned)(row * a.lda + gk) * 4u : kOOB);
+      if (a.a_ones > 0 && gk + 3 >= a.a_ones) {
+        // caller's rows end at a_ones: the ones column there, zeros after
+        float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (gk + q >= a.a_ones) vv[q] = (gk + q == a.a_ones && row < a.M) ? 1.f : 0.f;
+        v = make_float4(vv[0], vv[1], vv[2], vv[3]);
+      }
       if (k + 3 >= Kb) {          // zero the part of the last quad past K (the row's padding may hold the ones column)
         if (k + 1 >= Kb) v.y = 0.f;
         if (k + 2 >= Kb) v.z = 0.f;
         if (k + 3 >= Kb) v.w = 0.f;
+      }
+      if (a.a_copy && blockIdx.x == 0 && row < a.M && k < Kb) {
+        float* dst = a.a_copy + (size_t)row * a.a_copy_ld + gk;
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (k + q < Kb) dst[q] = vv[q];
       }
     }
     *reinterpret_cast<float4*>(&As[row * lds_ld + k]) = v;

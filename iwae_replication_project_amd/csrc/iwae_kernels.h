@@ -166,6 +166,11 @@ struct SmArgs {
   // A given as a_slabs partial slabs of a pre-activation: staged as
   // tanh(sum) (a_act) with the ones column at K - 1, and written once to a_out
   int a_slabs; long long a_slab; int a_act; float* a_out; int a_ldo;
+  // A read straight from the caller's rows (no ones column): column a_ones (> 0)
+  // reads 1, later ones 0 (0: off); a_bytes bounds the reads (0: unbounded);
+  // workgroups of column tile 0 also store the staged rows (ones column
+  // included) to a_copy for the later readers of A
+  int a_ones; unsigned a_bytes; float* a_copy; int a_copy_ld;
 };
 hipError_t launch_smallm(hipStream_t st, const SmArgs& a);
 hipError_t smallm_setup_attributes();

@@ -130,7 +130,20 @@ struct iwae_handle {
   int nll_fused = 1;                 // NLL: fused k-sample forward (mega_fwd_kernel) when it fits
   // graphs
   bool use_graphs = false;
-  std::map<std::vector<long long>, hipGraphExec_t> graphs;
+  // a captured train step; its first kernel reads the caller's x directly
+  // (x_node: that launch, re-pointed with hipGraphExecKernelNodeSetParams)
+  struct GraphRec {
+    hipGraphExec_t exec = nullptr;
+    hipGraph_t graph = nullptr;
+    hipGraphNode_t x_node = nullptr;
+    SmArgs x_args{};
+    const float* x_cap = nullptr;
+  };
+  std::map<std::vector<long long>, GraphRec> graphs;
+  const float* x_user = nullptr;       // train step: caller's x read directly by the first kernel
+  bool capturing = false;
+  hipGraphNode_t cap_x_node = nullptr;
+  SmArgs cap_x_args{};
   // live kernel timing (HIP events around every launch of one GEMM class)
   float* loss_out = nullptr;           // train-step loss destination (part of the graph key)
   int prof_kind = -1, prof_epi = -1;
@@ -192,9 +205,16 @@ static StochL add_stoch(iwae_handle* h, int fin, int H, int d, int rows_kind) {
   h->keras.push_back({s.head, d, d});
   return s;
 }
+static void destroy_graph(iwae_handle::GraphRec& g) {
+  if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  if (g.graph) (void)hipGraphDestroy(g.graph);
+  g.exec = nullptr;
+  g.graph = nullptr;
+}
+
 
 static void free_workspace(iwae_handle* h) {
-  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : h->graphs) destroy_graph(kv.second);
   h->graphs.clear();
   if (h->arena) (void)hipFree(h->arena);
   h->arena = nullptr;
@@ -816,16 +836,40 @@ static int fused_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool tr
     const StochL& S0 = h->enc[0];
     const DenseL& d1 = h->dense[S0.l1];
     const int ksl = (int)std::min<long long>(std::min(4, h->fslab_S), cdiv(d1.fin + 1, 128));
+    // input layer: from the caller's x when given (it also fills x_in for the
+    // later readers: Bernoulli epilogue, weight gradient), else from x_in
+    SmArgs a{};
+    if (h->x_user) {
+      a.A = h->x_user; a.lda = h->xdim;
+      a.a_ones = h->xdim; a.a_bytes = (unsigned)((size_t)P.Bimg * h->xdim * sizeof(float));
+      a.a_copy = h->x_in.p; a.a_copy_ld = h->x_in.ld;
+    } else {
+      a.A = h->x_in.p; a.lda = h->x_in.ld;
+    }
+    a.W = h->params + d1.off; a.ldw = d1.ldw;
+    a.M = P.Bimg; a.N = d1.fout; a.K = d1.fin + 1;
     if (ksl > 1) {
       // the wide input layer split over K into partial slabs (more workgroups);
       // the second layer sums them, applies tanh and stores y1 while staging
-      SmArgs a{};
-      a.A = h->x_in.p; a.lda = h->x_in.ld;
-      a.W = h->params + d1.off; a.ldw = d1.ldw;
       a.C = h->fslab; a.ldc = h->eb[0].y1.ld;
-      a.M = P.Bimg; a.N = d1.fout; a.K = d1.fin + 1;
       a.kslabs = ksl; a.c_slab = (long long)P.Bimg * a.ldc;
-      HIPCHK(launch_smallm(h->stream, a));
+    } else {
+      a.C = h->eb[0].y1.p; a.ldc = h->eb[0].y1.ld;
+      a.act = 1;
+    }
+    HIPCHK(launch_smallm(h->stream, a));
+    if (h->capturing && h->x_user) {
+      // remember this launch: replays re-point it at the caller's next x
+      hipStreamCaptureStatus cs;
+      unsigned long long cid;
+      hipGraph_t cg;
+      const hipGraphNode_t* deps = nullptr;
+      size_t nd = 0;
+      HIPCHK(hipStreamGetCaptureInfo_v2(h->stream, &cs, &cid, &cg, &deps, &nd));
+      h->cap_x_node = nd == 1 ? deps[0] : nullptr;
+      h->cap_x_args = a;
+    }
+    if (ksl > 1) {
       const DenseL& d2 = h->dense[S0.l2];
       SmArgs b{};
       b.A = h->fslab; b.lda = a.ldc;
@@ -836,7 +880,6 @@ static int fused_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool tr
       b.act = 1;
       HIPCHK(launch_smallm(h->stream, b));
     } else {
-      CHK(smallm(h, h->x_in, P.Bimg, h->dense[S0.l1], false, 1, nullptr, h->eb[0].y1));
       CHK(smallm(h, h->eb[0].y1, P.Bimg, h->dense[S0.l2], false, 1, nullptr, h->eb[0].y2));
     }
     CHK(smallm(h, h->eb[0].y2, P.Bimg, h->dense[S0.head], false, 0, nullptr, h->eb[0].P));
@@ -1180,13 +1223,21 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
   EpsSet E;
   CHK(parse_eps(h, P, eps, n_eps, E));
   CHK(ensure_capacity(h, P.Bimg, P.Bimg * P.kS, true));
-  CHK(copy_x(h, P, x));
+  // the fused step's first kernel reads the caller's x itself (and fills x_in);
+  // every other path stages x into x_in first
+  const bool direct = P.Bimg == P.B && use_fused(h, P) && smallm_ok(h, P.Bimg);
+  if (!direct) CHK(copy_x(h, P, x));
+  h->x_user = direct ? x : nullptr;
   const bool philox = (E.a[0] == nullptr);
   h->loss_out = loss_dev;
   h->in_train_step = true;
-  struct Reset { iwae_handle* h; ~Reset() { h->in_train_step = false; } } reset_flag{h};
+  struct Reset {
+    iwae_handle* h;
+    ~Reset() { h->in_train_step = false; h->x_user = nullptr; h->capturing = false; }
+  } reset_flag{h};
   if (h->use_graphs && philox && h->prof_kind < 0) {
-    std::vector<long long> key = {adam ? 1 : 0, lc->loss, B, lc->k, lc->k1, lc->k2, (long long)(uintptr_t)loss_dev};
+    std::vector<long long> key = {adam ? 1 : 0, lc->loss, B, lc->k, lc->k1, lc->k2, (long long)(uintptr_t)loss_dev,
+                                  direct ? 1 : 0};
     float fk[3] = {lc->p, lc->alpha, lc->beta};
     for (float f : fk) {
       int bits;
@@ -1196,17 +1247,42 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
     auto it = h->graphs.find(key);
     if (it == h->graphs.end()) {
       hipGraph_t graph;
+      h->capturing = true;
+      h->cap_x_node = nullptr;
       HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
       int rc = train_body(h, P, E, adam);
       hipError_t ec = hipStreamEndCapture(h->stream, &graph);
+      h->capturing = false;
       if (rc != IWAE_OK) return rc;
       HIPCHK(ec);
-      hipGraphExec_t exec;
-      HIPCHK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-      HIPCHK(hipGraphDestroy(graph));
-      it = h->graphs.emplace(key, exec).first;
+      iwae_handle::GraphRec g;
+      g.graph = graph;
+      HIPCHK(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
+      if (direct) {
+        if (!h->cap_x_node) {
+          destroy_graph(g);
+          return fail(h, IWAE_EHIP, "train-step capture: input-layer launch not found");
+        }
+        g.x_node = h->cap_x_node;
+        g.x_args = h->cap_x_args;
+        g.x_cap = x;
+      }
+      it = h->graphs.emplace(key, g).first;
     }
-    HIPCHK(hipGraphLaunch(it->second, h->stream));
+    iwae_handle::GraphRec& g = it->second;
+    if (g.x_node && g.x_cap != x) {
+      // re-point the input-layer launch at this call's x
+      hipKernelNodeParams kp;
+      HIPCHK(hipGraphKernelNodeGetParams(g.x_node, &kp));
+      SmArgs na = g.x_args;
+      na.A = x;
+      void* args[] = {&na};
+      kp.kernelParams = args;
+      kp.extra = nullptr;
+      HIPCHK(hipGraphExecKernelNodeSetParams(g.exec, g.x_node, &kp));
+      g.x_cap = x;
+    }
+    HIPCHK(hipGraphLaunch(g.exec, h->stream));
   } else {
     CHK(train_body(h, P, E, adam));
   }
@@ -1339,7 +1415,7 @@ int iwae_synchronize(iwae_handle* h) {
 int iwae_set_seed(iwae_handle* h, unsigned long long seed) {
   if (!h) return IWAE_EINVAL;
   h->seed = seed;
-  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);   // seed is a captured kernel argument
+  for (auto& kv : h->graphs) destroy_graph(kv.second);   // seed is a captured kernel argument
   h->graphs.clear();
   uint64_t z[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(h->ds->rng, z, sizeof(z), hipMemcpyHostToDevice, h->stream));
@@ -1352,7 +1428,7 @@ int iwae_set_path(iwae_handle* h, int path) {
   if (path < 0 || path > 2) return fail(h, IWAE_EINVAL, "path must be 0 (auto), 1 (layer-wise) or 2 (fused)");
   h->path = path;
   h->nll_fused = path != 1;             // layer-wise everywhere when asked for
-  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : h->graphs) destroy_graph(kv.second);
   h->graphs.clear();
   return IWAE_OK;
 }
@@ -1361,7 +1437,7 @@ int iwae_set_precision(iwae_handle* h, int mode) {
   if (!h) return IWAE_EINVAL;
   if (mode != 0 && mode != 1) return fail(h, IWAE_EINVAL, "precision must be 0 (f32 MFMA) or 1 (bf16x3)");
   h->x3 = mode;
-  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : h->graphs) destroy_graph(kv.second);
   h->graphs.clear();
   return IWAE_OK;
 }
@@ -1494,7 +1570,7 @@ int iwae_bind_grad_buffer(iwae_handle* h, float* g, long long n) {
   if (g && n != h->nparam_int)
     return fail(h, IWAE_EINVAL, "grad buffer must hold " + std::to_string(h->nparam_int) + " floats");
   h->grad = g ? g : h->grad_own;
-  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : h->graphs) destroy_graph(kv.second);
   h->graphs.clear();
   return IWAE_OK;
 }
