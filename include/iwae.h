@@ -135,6 +135,13 @@ int iwae_forward_backward(iwae_handle* h, const iwae_loss_config* lc, const floa
  * caller may bind its own buffer (e.g. a torch tensor used for RCCL). */
 int iwae_grad_buffer(iwae_handle* h, float** grad_dev, long long* n);
 int iwae_bind_grad_buffer(iwae_handle* h, float* grad_dev, long long n);
+/* Gradient signal-to-noise harness (the SNR of
+ * Rainforth et al. 2018 discussed at PDF p7): accumulates the current gradient
+ * buffer (after iwae_forward_backward) into sum_dev += g, sumsq_dev += g^2.
+ * Both are device buffers of iwae_grad_buffer's n floats, internal layout;
+ * iwae_export_internal converts such a buffer to the Keras weight order. */
+int iwae_grad_moments(iwae_handle* h, float* sum_dev, float* sumsq_dev);
+int iwae_export_internal(iwae_handle* h, const float* internal_dev, float* host, long long n);
 /* Adam over the gradient buffer times grad_scale (1/world_size under DP). */
 int iwae_apply_adam(iwae_handle* h, float grad_scale);
 

@@ -66,6 +66,8 @@ SIGNATURES = {
     "iwae_grad_buffer": (c_int, [H, POINTER(FP), POINTER(c_longlong)]),
     "iwae_bind_grad_buffer": (c_int, [H, FP, c_longlong]),
     "iwae_apply_adam": (c_int, [H, c_float]),
+    "iwae_grad_moments": (c_int, [H, FP, FP]),
+    "iwae_export_internal": (c_int, [H, FP, FP, c_longlong]),
     "iwae_log_weights": (c_int, [H, FP, c_int, c_int, FPP, c_int, FP]),
     "iwae_bound": (c_int, [H, POINTER(IwaeLossConfig), FP, c_int, FPP, c_int, FP]),
     "iwae_e_log_px": (c_int, [H, FP, c_int, c_int, FPP, c_int, FP]),

@@ -4,6 +4,8 @@
 // reductions by __shfl_xor butterflies -- HBM/latency-bound by design.
 #include "iwae_kernels.h"
 
+#include <algorithm>
+
 namespace iwae {
 
 // ----------------------------------------------------------------- helpers
@@ -651,6 +653,30 @@ hipError_t launch_adam(hipStream_t st, const AdamArgs& a, long long max_seg_n) {
   const long long bx = (n4 + 255) / 256;
   if (bx < 1) return hipSuccess;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)bx), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------ gradient moments
+// Gradient signal-to-noise harness (Rainforth et al. 2018 as
+// in PDF p7): sum += g, sumsq += g*g over the internal gradient layout (its
+// padding is zero and stays zero).  Fixed order per element: deterministic.
+__global__ __launch_bounds__(256) void grad_moments_kernel(const float4* g, float4* s, float4* s2, long long n4) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const float4 v = g[i];
+    float4 a = s[i], b = s2[i];
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    b.x += v.x * v.x; b.y += v.y * v.y; b.z += v.z * v.z; b.w += v.w * v.w;
+    s[i] = a;
+    s2[i] = b;
+  }
+}
+hipError_t launch_grad_moments(hipStream_t st, const float* g, float* s, float* s2, long long n) {
+  if (n <= 0) return hipSuccess;
+  const long long n4 = n >> 2;             // the internal layout is padded to float4 rows
+  const long long blocks = std::min<long long>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(grad_moments_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(s), reinterpret_cast<float4*>(s2),
+                     n4);
   return hipGetLastError();
 }
 

@@ -282,6 +282,7 @@ struct AdamArgs {
   int tick;                    // advance state->t in a tick kernel first (else the bound kernel did)
 };
 hipError_t launch_adam(hipStream_t st, const AdamArgs& a, long long max_seg_n);
+hipError_t launch_grad_moments(hipStream_t st, const float* g, float* s, float* s2, long long n);
 
 // ------------------------------------------------------ split weights ----
 // bf16x3 products a.b ~ a_hi b_hi + a_hi b_lo + a_lo b_hi (hi = bf16(x),

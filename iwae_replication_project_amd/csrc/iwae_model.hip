@@ -1565,6 +1565,20 @@ int iwae_grad_buffer(iwae_handle* h, float** g, long long* n) {
   return IWAE_OK;
 }
 
+int iwae_grad_moments(iwae_handle* h, float* sum_dev, float* sumsq_dev) {
+  if (!h) return IWAE_EINVAL;
+  if (!sum_dev || !sumsq_dev) return fail(h, IWAE_EINVAL, "NULL moment buffer");
+  if ((h->nparam_int & 3) != 0) return fail(h, IWAE_EINVAL, "internal gradient layout not float4-padded");
+  HIPCHK(launch_grad_moments(h->stream, h->grad, sum_dev, sumsq_dev, h->nparam_int));
+  return IWAE_OK;
+}
+
+int iwae_export_internal(iwae_handle* h, const float* internal_dev, float* host, long long n) {
+  CHK(check_n(h, n, host));
+  if (!internal_dev) return fail(h, IWAE_EINVAL, "internal_dev is NULL");
+  return download(h, internal_dev, host);
+}
+
 int iwae_bind_grad_buffer(iwae_handle* h, float* g, long long n) {
   if (!h) return IWAE_EINVAL;
   if (g && n != h->nparam_int)

@@ -493,6 +493,50 @@ class Flexible_Model:
         return res, {}
 
     # ------------------------------------------------------------ data parallel
+    def get_gradient_snr(self, x, k=None, R=1000, loss_function=None, p=None, alpha=None, beta=None, k1=None,
+                         k2=None, seed=None, group=None):
+        """Per-parameter gradient signal-to-noise ratio |E g| / std(g) over R
+        independent noise draws at fixed weights (the
+        estimator SNR of Rainforth et al. 2018, PDF p7).  Each draw is one
+        device forward+backward (Philox noise, no Adam step); the moments
+        sum g and sum g^2 accumulate on the device (iwae_grad_moments).  Under
+        torch.distributed the R draws are split over the ranks (noise stream
+        seed + rank) and the moments summed with one all-reduce each.
+        Returns (list of SNR arrays in Keras weight order, {'R': R})."""
+        from . import distributed as D
+        rank, w = D.world(group)
+        xd = self._x(x)
+        B = xd.shape[0]
+        lc = self._lc(loss_function, k, p, alpha, beta, k1, k2)
+        if seed is not None:
+            self._call(self._lib.iwae_set_seed(self._h, (int(seed) + rank) & ((1 << 64) - 1)))
+        import ctypes
+        g = _lib.FP()
+        n = ctypes.c_longlong(0)
+        self._call(self._lib.iwae_grad_buffer(self._h, ctypes.byref(g), ctypes.byref(n)))
+        with torch.cuda.stream(self._stream):
+            s1 = torch.zeros(int(n.value), device=self.device)
+            s2 = torch.zeros(int(n.value), device=self.device)
+        lo, hi = D.shard_range(int(R), rank, w)
+        for _ in range(hi - lo):
+            self._call(self._lib.iwae_forward_backward(self._h, lc, _lib.fptr(xd), B, None, 0,
+                                                       _lib.fptr(self._loss_buf)))
+            self._call(self._lib.iwae_grad_moments(self._h, _lib.fptr(s1), _lib.fptr(s2)))
+        if w > 1:
+            with torch.cuda.stream(self._stream):
+                torch.distributed.all_reduce(s1, group=group)
+                torch.distributed.all_reduce(s2, group=group)
+        self._stream.synchronize()
+        m1 = np.empty(self._nparams, np.float32)
+        m2 = np.empty(self._nparams, np.float32)
+        self._call(self._lib.iwae_export_internal(self._h, _lib.fptr(s1), m1.ctypes.data_as(_lib.FP), m1.size))
+        self._call(self._lib.iwae_export_internal(self._h, _lib.fptr(s2), m2.ctypes.data_as(_lib.FP), m2.size))
+        mean = m1.astype(np.float64) / R
+        var = np.maximum(m2.astype(np.float64) / R - mean * mean, 0.0)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            snr = np.where(var > 0, np.abs(mean) / np.sqrt(var), np.inf)
+        return _split(snr, weight_shapes(self.dense)), {"R": int(R)}
+
     def _forward_backward(self, lc, xd, B, arr, n):
         self._call(self._lib.iwae_forward_backward(self._h, lc, _lib.fptr(xd), B, arr, n,
                                                    _lib.fptr(self._loss_buf)))

@@ -261,6 +261,38 @@ def test_graph_replays_follow_the_callers_batch():
     np.testing.assert_array_equal(runs[0][1], runs[1][1])
 
 
+@pytest.mark.parametrize("loss", ["IWAE", "PIWAE"])
+def test_gradient_snr_harness_matches_per_draw_gradients(loss):
+    """get_gradient_snr (device moment accumulation over R Philox draws) equals
+    the SNR computed on the host from the same R draws' gradients, one
+    forward_backward + get_gradients at a time (same seed, same stream)."""
+    he, hd, le, ld = [64, 32], [32, 64], [32, 16], [32, 784]
+    rng = np.random.default_rng(41)
+    x = (rng.random((6, 784)) < 0.2).astype(np.float32)
+    kw = dict(k1=4, k2=2) if loss == "PIWAE" else {}
+    k = 8
+    R = 40
+    a = make_model(he, hd, le, ld, loss=loss, k=k, seed=5, **kw)
+    snr, info = a.get_gradient_snr(x, R=R, seed=123)
+    b = make_model(he, hd, le, ld, loss=loss, k=k, seed=5, **kw)
+    b.set_weights(a.get_weights())
+    b._call(b._lib.iwae_set_seed(b._h, 123))
+    xd = b._x(x)
+    lc = b._lc()
+    gs = []
+    for _ in range(R):
+        b._forward_backward(lc, xd, xd.shape[0], None, 0)
+        gs.append(flat(b.get_gradients()))
+    G = np.stack(gs)
+    mean = G.mean(0)
+    sd = np.sqrt(np.maximum((G * G).mean(0) - mean * mean, 0.0))
+    ref = np.where(sd > 0, np.abs(mean) / np.where(sd > 0, sd, 1.0), np.inf)
+    got = flat(snr)
+    fin = np.isfinite(ref) & (sd > 1e-6 * np.abs(mean).max())
+    assert info["R"] == R and np.isfinite(got[fin]).all()
+    np.testing.assert_allclose(got[fin], ref[fin], rtol=2e-3, atol=1e-4)
+
+
 def test_philox_noise_statistics_match_oracle_vae_bound():
     """The VAE bound mean_{s,b} lw depends on the whole noise distribution:
     estimate it with device Philox noise and with numpy noise in the oracle
