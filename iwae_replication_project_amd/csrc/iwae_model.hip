@@ -320,7 +320,9 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
         return e ? std::max(1LL, std::atoll(e)) : 768LL;
       }();
       long long S = std::max(1LL, cdiv(kSlabTarget, tiles));
-      S = std::min(S, std::max(1LL, cdiv(R, 64)));
+      // at most 16 slabs (the Adam kernel sums up to 16 with all loads in flight;
+      // more slabs only add write + read traffic at large batch)
+      S = std::min(S, std::min(16LL, std::max(1LL, cdiv(R, 64))));
       d.max_splits = (int)S;
       d.slab_off = (long long)slab_total;
       slab_total += (size_t)((d.size() * S + 63) & ~63LL);
