@@ -429,9 +429,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
           load_x(i, j, xs);
         }
         // binarised pixels (every image of the hot path), decided once per wave tile
+        // (bitwise, not short-circuit: no branch per pixel)
         bool bin = true;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) bin = bin && (xs[r] == 0.f || xs[r] == 1.f);
+        for (int r = 0; r < 16; ++r) bin = bin & ((xs[r] == 0.f) | (xs[r] == 1.f));
         bin = __all(bin);
         if (bin && !a.need_bce && a.wb == 0.f) {
           // p = sigmoid(l)*(1-1e-6)+1e-7 >= 1e-7, so the raw v_log / v_rcp are exact

@@ -32,7 +32,14 @@ st = (a[:, 1] - t0) / 100.0
 pro = (a[:, 2] - a[:, 1]) / 100.0
 loop = (a[:, 3] - a[:, 2]) / 100.0
 epi = (a[:, 4] - a[:, 3]) / 100.0
+ecomp = (a[:, 5] - a[:, 3]) / 100.0
+ered = (a[:, 6] - a[:, 5]) / 100.0
+etail = (a[:, 4] - a[:, 6]) / 100.0
 end = (a[:, 4] - t0) / 100.0
 print(f"workgroups {len(a)}; span {end.max():.2f} us (first start -> last end)")
-for name, v in (("start offset", st), ("prologue load", pro), ("main loop", loop), ("epilogue", epi), ("end", end)):
+rows = [("start offset", st), ("prologue load", pro), ("main loop", loop), ("epilogue", epi)]
+if (a[:, 5] > 0).all() and (a[:, 6] > 0).all():      # debug builds with the finer epilogue stamps
+    rows += [("  elementwise", ecomp), ("  row reduce", ered), ("  tail", etail)]
+rows.append(("end", end))
+for name, v in rows:
     print(f"  {name:14s} min {v.min():6.2f}  med {np.median(v):6.2f}  max {v.max():6.2f} us")
