@@ -7,6 +7,7 @@ Python API; see DESIGN.md.
 """
 from .flexible_iwae import (Adam, Flexible_Model, LOSSES, architecture, glorot_weights,  # noqa: F401
                             loss_config, output_bias, resolve_dataset_bias, weight_shapes)
+from . import data  # noqa: F401,E402  (local-file loaders, LR-stage driver)
 
 __all__ = ["Adam", "Flexible_Model", "LOSSES", "architecture", "glorot_weights", "loss_config",
            "output_bias", "resolve_dataset_bias", "weight_shapes"]

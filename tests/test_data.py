@@ -1,0 +1,65 @@
+"""Host-side data plumbing: local-file loaders,
+binarisation, bias initialiser and the learning-rate stage schedule (E:76-E:77)."""
+import gzip
+
+import numpy as np
+import pytest
+
+from iwae_replication_project_amd import data as D
+
+
+def test_stage_schedule_matches_experiment_example():
+    # E:76: optimizer.learning_rate = 1e-4*round(10.**(1-(i-1)/7.), 1); E:77: 3**(i-1) passes
+    lrs = [D.stage_learning_rate(i) for i in range(1, 9)]
+    assert lrs[0] == pytest.approx(1e-3) and lrs[-1] == pytest.approx(1e-4)
+    assert lrs == pytest.approx([1e-4 * round(10.0 ** (1 - (i - 1) / 7.0), 1) for i in range(1, 9)])
+    assert all(a > b for a, b in zip(lrs, lrs[1:]))
+    assert [D.stage_passes(i) for i in range(1, 9)] == [1, 3, 9, 27, 81, 243, 729, 2187]
+    assert sum(D.stage_passes(i) for i in range(1, 9)) == 3280          # PDF p8: 3280 passes
+
+
+def test_idx_and_amat_and_npz_loaders(tmp_path):
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 256, size=(5, 28, 28), dtype=np.uint8)
+    hdr = b"".join(int(v).to_bytes(4, "big") for v in (2051, 5, 28, 28))
+    p = tmp_path / "train-images-idx3-ubyte.gz"
+    with gzip.open(p, "wb") as f:
+        f.write(hdr + img.tobytes())
+    x = D.load_mnist_idx(p)
+    assert x.shape == (5, 784) and x.dtype == np.float32
+    np.testing.assert_allclose(x, img.reshape(5, 784) / 255.0, atol=1e-7)
+
+    b = (rng.random((4, 784)) < 0.3).astype(np.float32)
+    amat = tmp_path / "binarized_mnist_train.amat"
+    amat.write_text("\n".join(" ".join(str(int(v)) for v in row) for row in b) + "\n")
+    np.testing.assert_array_equal(D.load_binarized_mnist(amat), b)
+    npz = tmp_path / "bm.npz"
+    np.savez(npz, x=b.reshape(4, 28, 28))
+    np.testing.assert_array_equal(D.load_binarized_mnist(npz), b)
+    with pytest.raises(ValueError):
+        bad = tmp_path / "bad.npy"
+        np.save(bad, b[:, :100])
+        D.load_binarized_mnist(bad)
+
+
+def test_omniglot_chardata_layout(tmp_path):
+    import scipy.io as sio
+    rng = np.random.default_rng(1)
+    data = rng.random((784, 6)).astype(np.float32)            # chardata.mat stores [784, N]
+    p = tmp_path / "chardata.mat"
+    sio.savemat(p, {"data": data, "testdata": data[:, :2]})
+    x = D.load_omniglot_chardata(p)                            # F:164: transpose then reshape
+    assert x.shape == (6, 784)
+    np.testing.assert_allclose(x, data.T, rtol=0, atol=0)
+    assert D.load_omniglot_chardata(p, "testdata").shape == (2, 784)
+
+
+def test_stochastic_binarisation_and_bias():
+    rng = np.random.default_rng(2)
+    grey = np.full((2000, 784), 0.25, np.float32)
+    xb = D.stochastic_binarize(grey, rng)
+    assert set(np.unique(xb)) <= {0.0, 1.0}
+    assert abs(xb.mean() - 0.25) < 0.01
+    bias = D.bias_from_train(xb)
+    m = np.clip(xb.astype(np.float64).mean(0), 0.001, 0.999)
+    np.testing.assert_allclose(bias, -np.log(1.0 / m - 1.0))
