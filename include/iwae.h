@@ -171,6 +171,24 @@ int iwae_nll_partials(iwae_handle* h, const float* x, int N, int k_local, int ch
 int iwae_nll_eps(iwae_handle* h, const float* x, int N, int k, const float* const* eps,
                  int n_eps, float* out_logpx);
 
+/* --- evaluation statistics (get_training_statistics, F:496-F:526) --------- */
+/* get_levels_of_units_activity (F:264-F:281): out_means[i] [dev] [N][d_i] =
+ * mean over n samples of q(h|x) of h_i (one encoder pass per sample, as the
+ * reference's n calls of encoder(x, 1)).  eps (optional) is [n][N][d_i] per
+ * layer.  Variances and PCA eigenvalues of these means are host arithmetic. */
+int iwae_encoder_means(iwae_handle* h, const float* x, int N, int n, const float* const* eps,
+                       int n_eps, float* const* out_means, int n_out);
+/* reconstructed_x_probs + get_reconstruction_loss (F:249-F:262, generate_x
+ * F:106-F:119): probs [dev] [B][ld_probs] (or NULL), loss_dev [dev] one float
+ * = mean_B sum_784 Keras BCE (or NULL).  eps (optional): L encoder buffers
+ * [1][B][d_i], then L-1 prior buffers [1][B][d_{L-2-j}] in generation order. */
+int iwae_reconstruct(iwae_handle* h, const float* x, int B, const float* const* eps, int n_eps,
+                     float* probs, int ld_probs, float* loss_dev);
+/* get_NLL_without_inactive_units (F:466-F:494): like iwae_nll / iwae_nll_eps
+ * with every sampled h_i multiplied by masks[i] ([dev], d_i floats of 0/1). */
+int iwae_nll_masked(iwae_handle* h, const float* x, int N, int k, const float* const* eps,
+                    int n_eps, const float* const* masks, int n_masks, float* out_logpx);
+
 /* --- diagnostics ---------------------------------------------------------- */
 /* C[M][N] = A[M][K] @ B[K][N] (all [dev], row-major, leading dims given) via
  * the f32 MFMA GEMM used on the hot path (unit-test entry). */

@@ -74,6 +74,9 @@ SIGNATURES = {
     "iwae_nll": (c_int, [H, FP, c_int, c_int, c_int, FP]),
     "iwae_nll_partials": (c_int, [H, FP, c_int, c_int, c_int, FP, FP]),
     "iwae_nll_eps": (c_int, [H, FP, c_int, c_int, FPP, c_int, FP]),
+    "iwae_encoder_means": (c_int, [H, FP, c_int, c_int, FPP, c_int, FPP, c_int]),
+    "iwae_reconstruct": (c_int, [H, FP, c_int, FPP, c_int, FP, c_int, FP]),
+    "iwae_nll_masked": (c_int, [H, FP, c_int, c_int, FPP, c_int, FPP, c_int, FP]),
     "iwae_debug_gemm": (c_int, [H, FP, c_int, FP, c_int, FP, c_int, c_int, c_int, c_int]),
     "iwae_workspace_bytes": (c_double, [H]),
     "iwae_profile_gemm": (c_int, [H, c_int, c_int]),

@@ -103,6 +103,7 @@ __global__ __launch_bounds__(256) void gauss_fwd_kernel(GaussArgs a, int lpr) {
         if (MODE == 0) {
           const float e = f4_at(e4, q);
           h = e * sc + mu[q];
+          if (a.mask) h *= a.mask[j];
           a.H[(size_t)r * a.ldH + j] = h;
           if (a.eps_out) a.eps_out[(size_t)r * a.ld_eps_out + j] = e;
         } else {
@@ -731,6 +732,55 @@ hipError_t launch_transpose_lw(hipStream_t st, const float* lw, int Bimg, int kS
   const int n = Bimg * kS;
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(transpose_lw_kernel, dim3((n + 255) / 256), dim3(256), 0, st, lw, Bimg, kS, out);
+  return hipGetLastError();
+}
+
+
+// ------------------------------------------------ evaluation statistics
+// Mean of h over the n samples of each image (get_levels_of_units_activity,
+// F:264-F:281): one thread per (image, column), 4 sample rows in flight.
+__global__ __launch_bounds__(256) void group_mean_kernel(const float* __restrict__ H, int ldH, int n, int d, int N,
+                                                         float* out, int ldo, float scale, int accumulate,
+                                                         uint64_t* rng_base) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (rng_base && i == 0) { rng_base[1] = rng_base[0]; rng_base[0] += 1; }
+  if (i >= (long long)N * d) return;
+  const int b = (int)(i / d), j = (int)(i - (long long)b * d);
+  const float* p = H + (size_t)b * n * ldH + j;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = 0;
+  for (; s + 4 <= n; s += 4) {
+    a0 += p[(size_t)s * ldH];
+    a1 += p[(size_t)(s + 1) * ldH];
+    a2 += p[(size_t)(s + 2) * ldH];
+    a3 += p[(size_t)(s + 3) * ldH];
+  }
+  for (; s < n; ++s) a0 += p[(size_t)s * ldH];
+  const float v = ((a0 + a1) + (a2 + a3)) * scale;
+  float* o = out + (size_t)b * ldo + j;
+  *o = accumulate ? *o + v : v;
+}
+hipError_t launch_group_mean(hipStream_t st, const float* H, int ldH, int n, int d, int N, float* out, int ldo,
+                             float scale, int accumulate, uint64_t* rng_base) {
+  const long long t = (long long)N * d;
+  if (t <= 0) return hipSuccess;
+  hipLaunchKernelGGL(group_mean_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, H, ldH, n, d, N, out,
+                     ldo, scale, accumulate, rng_base);
+  return hipGetLastError();
+}
+
+// Decoder.call probabilities (F:101-F:102), exact expf (evaluation only).
+__global__ __launch_bounds__(256) void bern_probs_kernel(float* z, int rows, int cols, int ld) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)rows * cols) return;
+  const int r = (int)(i / cols), c = (int)(i - (long long)r * cols);
+  float* p = z + (size_t)r * ld + c;
+  *p = (1.f / (1.f + expf(-*p))) * kProbScale + kProbShift;
+}
+hipError_t launch_bern_probs(hipStream_t st, float* z, int rows, int cols, int ld) {
+  const long long t = (long long)rows * cols;
+  if (t <= 0) return hipSuccess;
+  hipLaunchKernelGGL(bern_probs_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, z, rows, cols, ld);
   return hipGetLastError();
 }
 

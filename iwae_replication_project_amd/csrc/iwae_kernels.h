@@ -197,6 +197,7 @@ struct GaussArgs {
   float* out; int accumulate;               // per-row log density (set or +=)
   float* eps_out; int ld_eps_out;           // mode 0: keep the noise for the backward pass
   int M;
+  const float* mask;                        // mode 0: h *= mask[j] before log q (F:501-F:511), or null
 };
 // mode 0: sample h = eps*scale+mu and log N(h; mu, scale)   (Encoder.call F:58-F:70)
 // mode 1: log N(h; mu, scale) of a given h                   (Decoder.get_log_ph F:139-F:140)
@@ -410,6 +411,12 @@ hipError_t launch_mega_fwd(hipStream_t st, const MgLaunch& L, int rt, size_t lds
 hipError_t mega_setup_attributes();
 
 hipError_t launch_fill_col(hipStream_t st, float* buf, int rows, int ld, int col, float v);
+// Evaluation statistics (F:249-F:302).  out[b][j] (+)= scale * sum_s H[b*n+s][j]
+// for b < N, j < d; block 0 advances the Philox base when rng_base is given.
+hipError_t launch_group_mean(hipStream_t st, const float* H, int ldH, int n, int d, int N, float* out, int ldo,
+                             float scale, int accumulate, uint64_t* rng_base);
+// probs = sigmoid(logit) * (1 - 1e-6) + 1e-7 in place over [rows][ld] (F:102)
+hipError_t launch_bern_probs(hipStream_t st, float* z, int rows, int cols, int ld);
 hipError_t launch_transpose_lw(hipStream_t st, const float* lw_img, int Bimg, int kS, float* out);
 
 }  // namespace iwae

@@ -128,6 +128,8 @@ struct iwae_handle {
   int path = 0;                      // 0 auto, 1 layer-wise kernels, 2 fused row-block kernels
   int x3 = 1;                        // tiled GEMMs: 1 bf16x3 products (default), 0 exact f32 MFMA
   int nll_fused = 1;                 // NLL: fused k-sample forward (mega_fwd_kernel) when it fits
+  bool masked = false;               // active-unit masks in force (iwae_nll_masked only)
+  const float* mask[IWAE_MAX_LAYERS] = {};
   // graphs
   bool use_graphs = false;
   // a captured train step; its first kernel reads the caller's x directly
@@ -555,10 +557,11 @@ static int parse_eps(iwae_handle* h, const Plan& P, const float* const* eps, int
 static bool use_fused(const iwae_handle* h, const Plan& P);
 static int fused_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool train);
 
-static int forward_core(iwae_handle* h, const Plan& P, const EpsSet& E, bool train) {
-  if (use_fused(h, P)) return fused_forward(h, P, E, train);
+// Layer-wise encoder (F:56-F:75): h[i] sampled, log q into h->logq.  With
+// active-unit masks set (get_NLL_without_inactive_units, F:466-F:483) each
+// sample is multiplied by its layer's mask before log q and the next layer.
+static int encoder_fwd(iwae_handle* h, const Plan& P, const EpsSet& E, bool train) {
   const int L = h->L, kS = P.kS, M = P.Bimg * kS;
-  // encoder (F:56-F:75)
   CHK(stoch_fwd(h, h->enc[0], h->x_in, P.Bimg, h->eb[0]));
   for (int i = 0; i < L; ++i) {
     if (i > 0) CHK(stoch_fwd(h, h->enc[i], h->h[i - 1], M, h->eb[i]));
@@ -570,8 +573,16 @@ static int forward_core(iwae_handle* h, const Plan& P, const EpsSet& E, bool tra
     g.seed = h->seed; g.rng_base = &h->ds->rng[0]; g.layer = i;
     g.out = h->logq; g.accumulate = i > 0; g.M = M;
     if (train) { g.eps_out = h->eps_st[i].p; g.ld_eps_out = h->eps_st[i].ld; }
+    g.mask = h->masked ? h->mask[i] : nullptr;
     HIPCHK(launch_gauss_fwd(h->stream, 0, g));
   }
+  return IWAE_OK;
+}
+
+static int forward_core(iwae_handle* h, const Plan& P, const EpsSet& E, bool train) {
+  if (use_fused(h, P)) return fused_forward(h, P, E, train);
+  const int L = h->L, kS = P.kS, M = P.Bimg * kS;
+  CHK(encoder_fwd(h, P, E, train));
   // prior log p(h) (F:134-F:142)
   {
     GaussArgs g{};
@@ -765,7 +776,7 @@ static int rb_width_ok(const iwae_handle* h) {
 }
 
 static bool use_fused(const iwae_handle* h, const Plan& P) {
-  if (h->path == 1 || h->L > kRbMaxJobs) return false;
+  if (h->path == 1 || h->L > kRbMaxJobs || h->masked) return false;
   if (!rb_width_ok(h)) return false;
   if (h->path == 2) return true;
   return (long long)P.Bimg * P.kS <= 65536;
@@ -1750,7 +1761,7 @@ static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, flo
   MgLaunch MG;
   int mg_rt = 0;
   size_t mg_lds = 0;
-  const bool mega = h->x3 && h->nll_fused && mega_plan(h, MG, mg_rt, mg_lds);
+  const bool mega = h->x3 && h->nll_fused && !h->masked && mega_plan(h, MG, mg_rt, mg_lds);
   const size_t wbytes = (size_t)h->xdim * sizeof(float);
   for (int i0 = 0; i0 < N; i0 += imgs) {
     const int n = std::min(imgs, N - i0);
@@ -1816,6 +1827,117 @@ int iwae_nll_eps(iwae_handle* h, const float* x, int N, int k, const float* cons
   HIPCHK(launch_lse(h->stream, a));
   HIPCHK(launch_lse_final(h->stream, h->run_m, h->run_s, N, logf((float)k), out_logpx));
   return IWAE_OK;
+}
+
+// ------------------------------------------------ evaluation statistics
+// get_levels_of_units_activity (F:264-F:281): mean of every h_i over n
+// samples per image.  Chunks of images keep chunk*n rows within 2^20.
+int iwae_encoder_means(iwae_handle* h, const float* x, int N, int n, const float* const* eps, int n_eps,
+                       float* const* out_means, int n_out) {
+  if (!h) return IWAE_EINVAL;
+  if (!x) return fail(h, IWAE_EINVAL, "x is NULL");
+  if (N <= 0 || n <= 0) return fail(h, IWAE_EINVAL, "N and n_samples must be positive");
+  if (!out_means || n_out != h->L) return fail(h, IWAE_EINVAL, "expected one output per stochastic layer");
+  for (int i = 0; i < h->L; ++i)
+    if (!out_means[i]) return fail(h, IWAE_EINVAL, "NULL output buffer");
+  const long long max_rows = 1LL << 20;
+  if (n > max_rows) return fail(h, IWAE_EINVAL, "n_samples above 2^20 per image is not supported");
+  const bool injected = eps && n_eps > 0;
+  int imgs = injected ? N : (int)std::max<long long>(1, max_rows / n);
+  imgs = std::min(imgs, N);
+  if (h->x3) CHK(ensure_wsplit(h));
+  CHK(ensure_capacity(h, imgs, imgs * n, false));
+  const size_t wbytes = (size_t)h->xdim * sizeof(float);
+  for (int i0 = 0; i0 < N; i0 += imgs) {
+    const int m = std::min(imgs, N - i0);
+    Plan P;
+    P.B = m; P.Bimg = m; P.Bsplit = m; P.kS = n;
+    EpsSet E;
+    CHK(parse_eps(h, P, eps, n_eps, E));
+    HIPCHK(hipMemcpy2DAsync(h->x_in.p, (size_t)h->x_in.ld * sizeof(float), x + (size_t)i0 * h->xdim, wbytes,
+                            wbytes, m, hipMemcpyDeviceToDevice, h->stream));
+    CHK(encoder_fwd(h, P, E, false));
+    for (int l = 0; l < h->L; ++l) {
+      const int d = h->enc[l].d;
+      HIPCHK(launch_group_mean(h->stream, h->h[l].p, h->h[l].ld, n, d, m, out_means[l] + (size_t)i0 * d, d,
+                               1.f / (float)n, 0, l == h->L - 1 ? &h->ds->rng[0] : nullptr));
+    }
+  }
+  return IWAE_OK;
+}
+
+// reconstructed_x_probs / get_reconstruction_loss (F:249-F:262): one encoder
+// sample, keep h_L, re-draw h_{L-1} .. h_1 from the decoder's prior layers
+// (Decoder.generate_x, F:106-F:119), then the output MLP.
+int iwae_reconstruct(iwae_handle* h, const float* x, int B, const float* const* eps, int n_eps, float* probs,
+                     int ld_probs, float* loss_dev) {
+  if (!h) return IWAE_EINVAL;
+  if (!x) return fail(h, IWAE_EINVAL, "x is NULL");
+  const int L = h->L;
+  const bool injected = eps && n_eps > 0;
+  if (injected && n_eps != 2 * L - 1)
+    return fail(h, IWAE_EINVAL, "expected " + std::to_string(2 * L - 1) + " eps buffers (encoder, then prior)");
+  if (probs && (ld_probs < h->xdim || (ld_probs & 3) || ((uintptr_t)probs & 15)))
+    return fail(h, IWAE_EINVAL, "probs needs ld >= x_dim, a multiple of 4, 16-byte aligned");
+  iwae_loss_config lc{IWAE_LOSS_VAE, 1, 1.f, 1.f, 0.5f, 0, 0};
+  Plan P;
+  CHK(make_plan(h, &lc, B, P));
+  P.mode_a = BM_NONE; P.w_a = 0.f; P.need_bce = 1; P.bce_w = 1.f;
+  EpsSet E;
+  CHK(parse_eps(h, P, eps, injected ? L : 0, E));
+  if (h->x3) CHK(ensure_wsplit(h));
+  CHK(ensure_capacity(h, B, B, false));
+  CHK(copy_x(h, P, x));
+  CHK(encoder_fwd(h, P, E, false));
+  for (int j = 0; j < L - 1; ++j) {
+    CHK(stoch_fwd(h, h->dec[j], h->h[L - 1 - j], B, h->db[j]));
+    GaussArgs g{};
+    g.P = h->db[j].P.p; g.ldP = h->db[j].P.ld; g.prow_div = 1; g.d = h->dec[j].d;
+    g.H = h->h[L - 2 - j].p; g.ldH = h->h[L - 2 - j].ld;
+    g.eps_a = injected ? eps[L + j] : nullptr;
+    if (injected && !g.eps_a) return fail(h, IWAE_EINVAL, "NULL eps buffer");
+    g.kS = 1; g.Bsplit = B; g.Bimg = B;
+    g.seed = h->seed; g.rng_base = &h->ds->rng[0]; g.layer = IWAE_MAX_LAYERS + j;   // own Philox stream
+    g.out = h->logp; g.accumulate = 0; g.M = B;
+    HIPCHK(launch_gauss_fwd(h->stream, 0, g));
+  }
+  CHK(gemm_fwd(h, EPI_TANH, h->h[0], B, h->dense[h->o1], h->ob.y1));
+  CHK(gemm_fwd(h, EPI_TANH, h->ob.y1, B, h->dense[h->o2], h->ob.y2));
+  if (probs) {
+    Mat pm;
+    pm.p = probs; pm.ld = ld_probs;
+    CHK(gemm_fwd(h, EPI_STORE, h->ob.y2, B, h->dense[h->o3], pm));
+    HIPCHK(launch_bern_probs(h->stream, probs, B, h->xdim, ld_probs));
+  }
+  // Keras BCE of x against those probabilities, summed over pixels, mean over
+  // the batch (F:257-F:261) = -(E_q log p(x|h) with the BCE form); this pass
+  // also advances the Philox base
+  GemmArgs ex{};
+  ex.aux = h->x_in.p; ex.ldaux = h->x_in.ld; ex.x_row_div = 1;
+  ex.part = h->part; ex.part2 = h->part2; ex.ldpart = h->ldpart;
+  ex.wa = P.wa; ex.wb = P.wb; ex.need_bce = 1;
+  Mat gm;
+  CHK(gemm_fwd(h, EPI_BERN, h->ob.y2, B, h->dense[h->o3], gm, ex));
+  CHK(run_bound(h, P, false, -1.f, loss_dev ? loss_dev : &h->ds->scalars[1]));
+  return IWAE_OK;
+}
+
+// get_NLL_without_inactive_units (F:466-F:494): k-sample log p(x) with every
+// sampled h_i multiplied by its 0/1 active-unit mask masks[i] ([dev], d_i).
+int iwae_nll_masked(iwae_handle* h, const float* x, int N, int k, const float* const* eps, int n_eps,
+                    const float* const* masks, int n_masks, float* out_logpx) {
+  if (!h) return IWAE_EINVAL;
+  if (!out_logpx) return fail(h, IWAE_EINVAL, "out_logpx is NULL");
+  if (!masks || n_masks != h->L) return fail(h, IWAE_EINVAL, "expected one mask per stochastic layer");
+  for (int i = 0; i < h->L; ++i)
+    if (!masks[i]) return fail(h, IWAE_EINVAL, "NULL mask");
+  h->masked = true;
+  for (int i = 0; i < h->L; ++i) h->mask[i] = masks[i];
+  const int rc = (eps && n_eps > 0) ? iwae_nll_eps(h, x, N, k, eps, n_eps, out_logpx)
+                                    : nll_core(h, x, N, k, 0, nullptr, nullptr, out_logpx);
+  h->masked = false;
+  for (int i = 0; i < h->L; ++i) h->mask[i] = nullptr;
+  return rc;
 }
 
 int iwae_debug_gemm(iwae_handle* h, const float* A, int lda, const float* B, int ldb, float* C, int ldc,

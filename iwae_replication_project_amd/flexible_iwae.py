@@ -216,6 +216,11 @@ class Flexible_Model:
         self._scratch = torch.zeros(1, device=self.device)
 
     # ------------------------------------------------------------- plumbing
+    def set_seed(self, seed):
+        """Re-key the device Philox stream and restart its counter (reproducible
+        draws from here on).  The reference has no seed."""
+        self._call(self._lib.iwae_set_seed(self._h, int(seed) & ((1 << 64) - 1)))
+
     def _call(self, rc):
         _lib.check(self._lib, self._h, rc)
 
@@ -469,10 +474,119 @@ class Flexible_Model:
         """F:463-F:464: -L_k with k = 5000 by default."""
         return float(-self.log_px(x, k, eps).mean().item())
 
+    # ------------------------------------------------ evaluation statistics
+    def _reconstruct(self, x, eps, want_probs):
+        xd = self._x(x)
+        B = xd.shape[0]
+        L = len(self.n_latent_encoder)
+        arr, n, keep = None, 0, []
+        if eps is not None:
+            eps = list(eps)
+            if len(eps) != 2 * L - 1:
+                raise ValueError(f"expected {2 * L - 1} eps arrays (encoder, then prior), got {len(eps)}")
+            dims = list(self.n_latent_encoder) + [self.n_latent_encoder[L - 2 - j] for j in range(L - 1)]
+            with torch.cuda.stream(self._stream):
+                for e, d in zip(eps, dims):
+                    t = torch.as_tensor(e).to(device=self.device, dtype=torch.float32).contiguous()
+                    if tuple(t.shape) != (1, B, d):
+                        raise ValueError(f"eps arrays must be [1, B={B}, d={d}], got {tuple(t.shape)}")
+                    keep.append(t)
+            arr, n = _lib.fptr_array(keep)
+        with torch.cuda.stream(self._stream):
+            ld = (self.x_dim + 3) // 4 * 4
+            probs = torch.empty(B, ld, device=self.device) if want_probs else None
+            loss = torch.empty(1, device=self.device)
+        self._call(self._lib.iwae_reconstruct(self._h, _lib.fptr(xd), B, arr, n, _lib.fptr(probs),
+                                              ld if want_probs else 0, _lib.fptr(loss)))
+        self._stream.synchronize()
+        return (probs[:, :self.x_dim] if want_probs else None), float(loss.item())
+
+    def reconstructed_x_probs(self, x, eps=None):
+        """F:249-F:254: pixel probabilities [1, B, 784] of x reconstructed from
+        one q(h|x) draw of h_L through the decoder's prior layers (generate_x,
+        F:107-F:119).  ``eps``: L encoder arrays [1,B,d_i], then the L-1 prior
+        draws in generation order ([1,B,d_{L-2-j}])."""
+        probs, _ = self._reconstruct(x, eps, True)
+        return probs.unsqueeze(0)
+
+    def get_reconstruction_loss(self, x, eps=None):
+        """F:256-F:262: mean over the batch of the Keras BCE of x against the
+        reconstructed probabilities, summed over pixels."""
+        return self._reconstruct(x, eps, False)[1]
+
+    def encoder_means(self, x, n_samples, eps=None):
+        """Device [N, d_i] per layer: the mean over n_samples draws of q(h|x)
+        of h_i (the accumulation of F:268-F:276).  ``eps``: [n, N, d_i]."""
+        xd = self._x(x)
+        N = xd.shape[0]
+        arr, n, keep = self._eps(eps, N, n_samples)
+        with torch.cuda.stream(self._stream):
+            outs = [torch.empty(N, d, device=self.device) for d in self.n_latent_encoder]
+        oarr, no = _lib.fptr_array(outs)
+        self._call(self._lib.iwae_encoder_means(self._h, _lib.fptr(xd), N, int(n_samples), arr, n, oarr, no))
+        self._stream.synchronize()
+        return outs
+
+    def get_levels_of_units_activity(self, x, n_samples, eps=None):
+        """F:264-F:281: per stochastic layer, the variance over the batch of
+        E_q[h_i] and the PCA eigenvalues of those means (host float64 on the
+        [N, d_i] means the device produced)."""
+        means = [m.double().cpu().numpy() for m in self.encoder_means(x, n_samples, eps)]
+        variances = [m.var(0) for m in means]
+        return variances, [self.get_eigenvalues_PCA(m) for m in means]
+
+    @staticmethod
+    def get_eigenvalues_PCA(data):
+        """F:284-F:291: ascending eigenvalues of the empirical covariance
+        (divisor N) of data [N, D]."""
+        d = np.asarray(data, dtype=np.float64)
+        z = d - d.mean(0)
+        return np.linalg.eigvalsh(z.T @ z / d.shape[0])
+
+    @staticmethod
+    def get_active_units(variances, eigen_values, threshold=0.01):
+        """F:294-F:300: 0/1 activity per unit, active counts by variance and
+        by PCA eigenvalue."""
+        active_units = [[1 if v > threshold else 0 for v in var] for var in variances]
+        number_active_units = [int(sum(a)) for a in active_units]
+        number_active_units_PCA = [int(sum(1 for e in eig if e > threshold)) for eig in eigen_values]
+        return active_units, number_active_units, number_active_units_PCA
+
+    def log_px_masked(self, x, masks, k=5000, eps=None):
+        """Per-image k-sample log p(x) with every sampled h_i multiplied by
+        masks[i] (0/1, length d_i) before log q and the later layers."""
+        xd = self._x(x)
+        N = xd.shape[0]
+        L = len(self.n_latent_encoder)
+        if len(masks) != L:
+            raise ValueError(f"expected {L} masks, got {len(masks)}")
+        with torch.cuda.stream(self._stream):
+            mts = []
+            for m, d in zip(masks, self.n_latent_encoder):
+                t = torch.as_tensor(np.asarray(m, dtype=np.float32)).to(self.device).contiguous()
+                if tuple(t.shape) != (d,):
+                    raise ValueError(f"mask must have {d} entries, got {tuple(t.shape)}")
+                mts.append(t)
+            out = torch.empty(N, device=self.device)
+        marr, nm = _lib.fptr_array(mts)
+        arr, n, keep = self._eps(eps, N, k)
+        self._call(self._lib.iwae_nll_masked(self._h, _lib.fptr(xd), N, int(k), arr, n, marr, nm, _lib.fptr(out)))
+        self._stream.synchronize()
+        return out
+
+    def get_NLL_without_inactive_units(self, x, threshold=0.01, n_samples=5000, eps=None, eps_activity=None):
+        """F:466-F:494: the activity of the units is measured on x with
+        n_samples draws, inactive units are zeroed in every sample, and the
+        n_samples-sample estimate is returned as -L_k (an NLL)."""
+        variances, eigen_values = self.get_levels_of_units_activity(x, n_samples, eps_activity)
+        active_units, _, _ = self.get_active_units(variances, eigen_values, threshold)
+        return float(-self.log_px_masked(x, active_units, n_samples, eps).mean().item())
+
     def get_training_statistics(self, x, k, batch_size=10):
-        """F:496-F:526, hot-path subset: VAE, IWAE, NLL (k=5000), E_q log p(x|h)
-        and both KL terms.  Reconstruction loss / active units / PCA are not
-        part of this build and are absent from res."""
+        """F:496-F:526: (res, res2) with the reference's keys.  res: batch
+        means of VAE, IWAE, NLL (k=5000), E_q log p(x|h), both KL terms,
+        reconstruction_loss, and LL_pruned (on the first batch); res2: active
+        units (1000 draws over all of x), their counts, PCA counts, variances."""
         xd = self._x(x)
         N = xd.shape[0]
         nb = max(1, N // batch_size)
@@ -480,6 +594,7 @@ class Flexible_Model:
         res["E_q(h|x)[log(p(x|h))]"] = 0.0
         res["D_kl(q(h|x),p(h))"] = 0.0
         res["D_kl(q(h|x),p(h|x))"] = 0.0
+        res["reconstruction_loss"] = 0.0
         for i in range(nb):
             b = xd[i * batch_size:(i + 1) * batch_size]
             vae = self.get_L(b, k)
@@ -490,7 +605,14 @@ class Flexible_Model:
             res["E_q(h|x)[log(p(x|h))]"] += eq / nb
             res["D_kl(q(h|x),p(h))"] += (eq - self.get_L(b, k)) / nb
             res["D_kl(q(h|x),p(h|x))"] += -1 * (self.get_L(b, k) + self.get_NLL(b)) / nb
-        return res, {}
+            res["reconstruction_loss"] += self.get_reconstruction_loss(b) / nb
+        res2 = {}
+        variances, eigen_values = self.get_levels_of_units_activity(xd, 1000)
+        res2["active_units"], res2["number_of_active_units"], res2["number_of_PCA_active_units"] = \
+            self.get_active_units(variances, eigen_values)
+        res2["variances"] = variances
+        res["LL_pruned"] = self.get_NLL_without_inactive_units(xd[:batch_size])
+        return res, res2
 
     # ------------------------------------------------------------ data parallel
     def get_gradient_snr(self, x, k=None, R=1000, loss_function=None, p=None, alpha=None, beta=None, k1=None,

@@ -188,7 +188,7 @@ def normal_log_prob(x, loc, scale):
     return -0.5 * z * z - (x.dtype.type(HALF_LOG_2PI) + np.log(scale)), z
 
 
-def forward(params, spec: ModelSpec, x, eps, need_bce=False, dup_decoder=False):
+def forward(params, spec: ModelSpec, x, eps, need_bce=False, dup_decoder=False, masks=None):
     """get_log_weights (F:327-F:351) with injected noise.
 
     x: [B, 784] in {0,1}; eps: list of [k, B, d_i].  Returns a cache dict
@@ -204,12 +204,16 @@ def forward(params, spec: ModelSpec, x, eps, need_bce=False, dup_decoder=False):
     lq_layers = []
     q0 = _stoch_forward(params, "enc0", x)            # F:58, M = B rows
     h1 = eps[0] * q0["scale"] + q0["mu"]              # F:59 sample(n): eps*scale + loc
+    if masks is not None:
+        h1 = h1 * masks[0]                            # F:474 modified_h1 = h1*active_units[0]
     lp, z = normal_log_prob(h1, q0["mu"], q0["scale"])
     q0["z"] = z
     enc.append(q0); h.append(h1); lq_layers.append(lp.sum(-1))   # F:60
     for i in range(1, L):
         qi = _stoch_forward(params, f"enc{i}", h[-1])             # F:66
         hi = eps[i] * qi["scale"] + qi["mu"]                     # F:68
+        if masks is not None:
+            hi = hi * masks[i]                                   # F:482-F:483
         lp, z = normal_log_prob(hi, qi["mu"], qi["scale"])
         qi["z"] = z
         enc.append(qi); h.append(hi); lq_layers.append(lp.sum(-1))   # F:70
@@ -533,7 +537,7 @@ def train_step(params, spec, x, eps, loss, k, opt: Adam, **kw):
 # ---------------------------------------------------------------------------
 # k-sample NLL (F:463-F:464), chunked over samples with an LSE merge
 # ---------------------------------------------------------------------------
-def log_px_per_image(params, spec, x, k, rng=None, eps=None, chunk=500):
+def log_px_per_image(params, spec, x, k, rng=None, eps=None, chunk=500, masks=None):
     """log p_hat(x) = logmeanexp_k lw per image.  Either ``eps`` (list of
     [k,B,d]) or an rng drawing it chunk by chunk."""
     B = x.shape[0]
@@ -541,9 +545,68 @@ def log_px_per_image(params, spec, x, k, rng=None, eps=None, chunk=500):
     for s0 in range(0, k, chunk):
         kc = min(chunk, k - s0)
         e = [ee[s0:s0 + kc] for ee in eps] if eps is not None else draw_eps(spec, kc, B, rng, x.dtype)
-        lw = forward(params, spec, x, e)["lw"].astype(np.float64)
+        lw = forward(params, spec, x, e, masks=masks)["lw"].astype(np.float64)
         m = lw.max(0)
         M = np.maximum(m_run, m)
         s_run = s_run * np.exp(m_run - M) + np.exp(lw - M).sum(0)
         m_run = M
     return m_run + np.log(s_run) - math.log(k)
+
+
+# ---------------------------------------------------------------------------
+# Evaluation statistics (F:249-F:302, F:466-F:494)
+# ---------------------------------------------------------------------------
+def keras_bce(x, p):
+    """keras.losses.binary_crossentropy per element (TF 2.4 backend form):
+    -(x log(clip(p)+1e-7) + (1-x) log(1-clip(p)+1e-7)), clip to [1e-7, 1-1e-7]."""
+    dt = p.dtype.type
+    pc = np.clip(p, dt(KERAS_EPS), dt(1 - KERAS_EPS))
+    return -(x * np.log(pc + dt(KERAS_EPS)) + (1 - x) * np.log(1 - pc + dt(KERAS_EPS)))
+
+
+def reconstruct(params, spec, x, eps_enc, eps_prior):
+    """reconstructed_x_probs (F:249-F:253) and get_reconstruction_loss (F:256-F:262).
+
+    eps_enc: L arrays [1, B, d_i] (encoder(x, 1)); eps_prior: L-1 arrays, the
+    prior draws of Decoder.generate_x (F:107-F:119) in generation order, j-th
+    is [1, B, d_{L-2-j}].  Returns (probs [1, B, 784], loss)."""
+    dt = x.dtype.type
+    L = spec.L
+    c = forward(params, spec, x, eps_enc)
+    rev = [c["h"][-1]]                                            # h_L only (F:252)
+    for j in range(L - 1):
+        dj = _stoch_forward(params, f"dec{j}", rev[-1])           # F:113
+        rev.append(eps_prior[j] * dj["scale"] + dj["mu"])         # F:114 sample()
+    h1 = rev[-1]
+    W1, b1 = params["out.l1"]; W2, b2 = params["out.l2"]; W3, b3 = params["out.l3"]
+    logit = np.tanh(np.tanh(h1 @ W1 + b1) @ W2 + b2) @ W3 + b3
+    p = (1.0 / (1.0 + np.exp(-logit))) * dt(PROB_SCALE) + dt(PROB_SHIFT)   # F:101-F:102
+    loss = keras_bce(x[None], p).sum(-1).mean()                   # F:258-F:261
+    return p, loss
+
+
+def encoder_means(params, spec, x, eps):
+    """F:264-F:281: per layer, the mean over n samples (eps [n, B, d_i]) of
+    h_i, squeezed to [B, d_i]."""
+    c = forward(params, spec, x, eps)
+    return [hi.mean(0) for hi in c["h"]]
+
+
+def eigenvalues_PCA(data):
+    """get_eigenvalues_PCA (F:284-F:291): eigenvalues (ascending) of the
+    empirical covariance (divisor N) of data [N, D]."""
+    z = data - data.mean(0)
+    return np.linalg.eigvalsh(z.T @ z / data.shape[0])
+
+
+def levels_of_units_activity(means):
+    """F:274-F:281: population variance over the batch and PCA eigenvalues."""
+    return [m.var(0) for m in means], [eigenvalues_PCA(m) for m in means]
+
+
+def active_units(variances, eigen_values, threshold=0.01):
+    """get_active_units (F:294-F:300)."""
+    au = [[1 if v > threshold else 0 for v in var] for var in variances]
+    n_au = [int(sum(a)) for a in au]
+    n_pca = [int(sum(1 if e > threshold else 0 for e in eig)) for eig in eigen_values]
+    return au, n_au, n_pca

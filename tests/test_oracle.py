@@ -262,3 +262,65 @@ def test_spec_param_counts_match_survey():
     # 425,284 (1L) and 521,084 (2L) parameters
     assert O.ModelSpec([200], [200], [50], [784]).n_params() == 425284
     assert O.ModelSpec([200, 100], [100, 200], [100, 50], [100, 784]).n_params() == 521084
+
+
+# ------------------------------------------------ evaluation statistics (F:249-F:300, F:466-F:494)
+def _stat_model(L, seed=3):
+    from oracle import iwae_oracle as O
+    arch = {1: ([32], [32], [8], [784]), 2: ([32, 16], [16, 32], [12, 6], [12, 784])}[L]
+    spec = O.ModelSpec(*arch)
+    rng = np.random.default_rng(seed)
+    mean = rng.uniform(0.05, 0.4, 784)
+    params = O.glorot_init(spec, rng, out_bias=O.output_bias_from_mean(mean))
+    x = (rng.random((5, 784)) < mean).astype(np.float64)
+    return O, spec, params, x, rng
+
+
+def test_oracle_reconstruction_one_layer_is_the_forward_decoder():
+    """L=1: generate_x has no prior layers, so the probabilities are the
+    forward pass's p on the same encoder draw; loss = mean_B sum Keras BCE."""
+    O, spec, params, x, rng = _stat_model(1)
+    eps = O.draw_eps(spec, 1, x.shape[0], rng)
+    p, loss = O.reconstruct(params, spec, x, eps, [])
+    c = O.forward(params, spec, x, eps, need_bce=True)
+    np.testing.assert_allclose(p, c["p"], rtol=1e-12)
+    np.testing.assert_allclose(loss, -c["bce_row"].mean(), rtol=1e-12)
+
+
+def test_oracle_reconstruction_two_layers_redraws_h1_from_the_prior():
+    O, spec, params, x, rng = _stat_model(2)
+    B = x.shape[0]
+    eps = O.draw_eps(spec, 1, B, rng)
+    pri = [rng.standard_normal((1, B, spec.n_latent_encoder[0]))]
+    p, _ = O.reconstruct(params, spec, x, eps, pri)
+    c = O.forward(params, spec, x, eps)
+    d0 = O._stoch_forward(params, "dec0", c["h"][1])
+    h1 = pri[0] * d0["scale"] + d0["mu"]
+    c2 = O.forward(params, spec, x, [(h1 - c["enc"][0]["mu"]) / c["enc"][0]["scale"], eps[1]])
+    # forcing the encoder's h1 to the prior draw gives the same decoder input
+    np.testing.assert_allclose(c2["h"][0], h1, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(p, c2["p"], rtol=1e-9)
+
+
+def test_oracle_pca_eigenvalues_sum_to_the_variances():
+    """trace(cov) = sum of per-unit population variances; eigenvalues >= 0."""
+    O, spec, params, x, rng = _stat_model(2)
+    eps = O.draw_eps(spec, 7, x.shape[0], rng)
+    var, eig = O.levels_of_units_activity(O.encoder_means(params, spec, x, eps))
+    for v, e in zip(var, eig):
+        np.testing.assert_allclose(e.sum(), v.sum(), rtol=1e-10)
+        assert e.min() > -1e-12
+    au, n_au, n_pca = O.active_units([np.array([0.5, 0.001, 0.02])], [np.array([0.0, 0.005, 0.6])])
+    assert au == [[1, 0, 1]] and n_au == [2] and n_pca == [1]
+
+
+def test_oracle_masks_of_ones_change_nothing_and_zero_masks_pin_h():
+    O, spec, params, x, rng = _stat_model(2)
+    eps = O.draw_eps(spec, 4, x.shape[0], rng)
+    ones = [np.ones(d) for d in spec.n_latent_encoder]
+    a = O.forward(params, spec, x, eps)["lw"]
+    b = O.forward(params, spec, x, eps, masks=ones)["lw"]
+    np.testing.assert_array_equal(a, b)
+    zero = [np.zeros(d) for d in spec.n_latent_encoder]
+    c = O.forward(params, spec, x, eps, masks=zero)
+    assert all(np.all(h == 0) for h in c["h"])
