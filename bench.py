@@ -195,7 +195,8 @@ def main():
         xs = model._x(xt[lo:hi])
         # warm the NLL workspace and the torch ops of the bookkeeping below (their first
         # use loads GPU code objects: tens to hundreds of ms, not NLL work)
-        lpw = model.log_px(xs[: max(1, min(64, hi - lo))], args.nll_k)
+        # (a full chunk of images: the workspace reaches its final size here, not in the timed call)
+        lpw = model.log_px(xs[: max(1, min(hi - lo, (1 << 20) // args.nll_k))], args.nll_k)
         torch.stack([lpw.sum(), torch.tensor(1.0, device=lpw.device)])
         barrier()
         torch.cuda.synchronize()

@@ -407,7 +407,7 @@ struct MgLaunch {
   uint64_t seed; const uint64_t* rng_base;
   float* lw;                                      // out: log w per row
 };
-hipError_t launch_mega_fwd(hipStream_t st, const MgLaunch& L, int rt, size_t lds_bytes);
+hipError_t launch_mega_fwd(hipStream_t st, const MgLaunch& L, int rt, int waves, size_t lds_bytes);
 hipError_t mega_setup_attributes();
 
 hipError_t launch_fill_col(hipStream_t st, float* buf, int rows, int ld, int col, float v);

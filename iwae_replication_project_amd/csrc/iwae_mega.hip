@@ -47,7 +47,7 @@ typedef __bf16 mg_bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 mg_bf16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned mg_u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int MG_WAVES = 8;
+constexpr int MG_WAVES = 8;         // waves of the 64-row workgroup (NW template argument: 8 or 4)
 constexpr int MG_KS = 8;             // k steps of 32 per weight fetch (256 k)
 #ifndef IWAE_MG_PF
 #define IWAE_MG_PF 2
@@ -95,9 +95,9 @@ __device__ __forceinline__ float mg_tanh(float x) {
 }
 
 // ones column (K - 1 of the next reader) and zero padding of columns [width, next_k)
-template <int RT>
+template <int RT, int NW>
 __device__ __forceinline__ void mg_pad(const MgBuf& B, int width, int next_k) {
-  constexpr int TPR = (8 * 64) / (16 * RT);     // threads per row
+  constexpr int TPR = (NW * 64) / (16 * RT);    // threads per row
   const int row = threadIdx.x / TPR;
   for (int col = width + threadIdx.x % TPR; col < next_k; col += TPR) {
     B.hi[row * B.ld + col] = (__bf16)(col == width ? 1.f : 0.f);
@@ -375,7 +375,7 @@ __device__ __forceinline__ void mg_tile(const MgLaunch& L, const MgStage& S, con
 // One Dense stage.  Wave w owns the column tiles w, w + 8, ...; when the whole
 // K fits one fetch (ldk <= 256) the first MG_PF steps of the wave's next tile
 // are requested during the current tile's MFMAs (mg_mma).
-template <int RT, int ACT>
+template <int RT, int ACT, int NW>
 __device__ __forceinline__ void mg_dense(const MgLaunch& L, const MgStage& S, uint64_t base, MgRows<RT>& R) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ntile = (S.N + 15) >> 4;
@@ -390,8 +390,8 @@ __device__ __forceinline__ void mg_dense(const MgLaunch& L, const MgStage& S, ui
 #pragma unroll
       for (int u = 0; u < MG_PF; ++u) mg_fetch_step(rh, rl, vb, u, ns, f);
     }
-    for (int t = wave; t < ntile; t += MG_WAVES) {
-      const int tn = t + MG_WAVES;
+    for (int t = wave; t < ntile; t += NW) {
+      const int tn = t + NW;
       const unsigned vb = mg_frag_base(S, t, 0);
 #pragma unroll
       for (int u = MG_PF; u < MG_KS; ++u) mg_fetch_step(rh, rl, vb, u, ns, f);
@@ -400,7 +400,7 @@ __device__ __forceinline__ void mg_dense(const MgLaunch& L, const MgStage& S, ui
   } else {
     // wide K: 256-deep fetches, no prefetch across tiles
     const int g = lane >> 4;
-    for (int t = wave; t < ntile; t += MG_WAVES) {
+    for (int t = wave; t < ntile; t += NW) {
       float4 xv[RT];
       if (ACT == MG_BERN) {
         const __amdgpu_buffer_rsrc_t rx = buf_rsrc(L.x);
@@ -423,16 +423,19 @@ __device__ __forceinline__ void mg_dense(const MgLaunch& L, const MgStage& S, ui
   }
 }
 
-template <int RT>
-__global__ __launch_bounds__(MG_WAVES * 64) void mega_fwd_kernel(MgLaunch L) {
+// NW = 8: one 64-row workgroup per CU (LDS-bound).  NW = 4 with RT = 2: two
+// independent 32-row workgroups per CU, whose weight waits, MFMA loops and
+// epilogues interleave instead of running in lock step behind one barrier.
+template <int RT, int NW>
+__global__ __launch_bounds__(NW * 64) void mega_fwd_kernel(MgLaunch L) {
   constexpr int R = 16 * RT;
-  constexpr int TPR = (MG_WAVES * 64) / R;      // threads per row in the prologue (8 / 16 / 32)
+  constexpr int TPR = (NW * 64) / R;            // threads per row in the prologue
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int row0 = blockIdx.x * R;
   const int nrows = min(R, L.rows - row0);
   float* logq = mgs + L.acc_off;
   float* logp = logq + R;
-  float* red = logp + R;                        // [MG_WAVES][R]
+  float* red = logp + R;                        // [NW][R]
   const uint64_t base = L.rng_base ? *L.rng_base : 0ull;
   const int rr = t / TPR, sub = t - rr * TPR;   // prologue: row rr, lane group sub
   MG_TRACE(0)
@@ -495,13 +498,13 @@ __global__ __launch_bounds__(MG_WAVES * 64) void mega_fwd_kernel(MgLaunch L) {
   for (int s = 0; s < L.nst; ++s) {
     const MgStage& S = L.st[s];
     MG_TRACE(2 + 3 * s)
-    if (S.act == MG_TANH) mg_pad<RT>(mg_buf<RT>(L, S.out_buf), S.N, S.next_k);
-    else if (S.act == MG_SAMPLE) mg_pad<RT>(mg_buf<RT>(L, S.out_buf), S.d, S.next_k);
+    if (S.act == MG_TANH) mg_pad<RT, NW>(mg_buf<RT>(L, S.out_buf), S.N, S.next_k);
+    else if (S.act == MG_SAMPLE) mg_pad<RT, NW>(mg_buf<RT>(L, S.out_buf), S.d, S.next_k);
     switch (S.act) {     // one instantiation per stage kind: one epilogue per tile loop
-      case MG_TANH: mg_dense<RT, MG_TANH>(L, S, base, Rw); break;
-      case MG_SAMPLE: mg_dense<RT, MG_SAMPLE>(L, S, base, Rw); break;
-      case MG_PRIOR: mg_dense<RT, MG_PRIOR>(L, S, base, Rw); break;
-      default: mg_dense<RT, MG_BERN>(L, S, base, Rw); break;
+      case MG_TANH: mg_dense<RT, MG_TANH, NW>(L, S, base, Rw); break;
+      case MG_SAMPLE: mg_dense<RT, MG_SAMPLE, NW>(L, S, base, Rw); break;
+      case MG_PRIOR: mg_dense<RT, MG_PRIOR, NW>(L, S, base, Rw); break;
+      default: mg_dense<RT, MG_BERN, NW>(L, S, base, Rw); break;
     }
     MG_TRACE(3 + 3 * s)
     __syncthreads();
@@ -523,34 +526,40 @@ __global__ __launch_bounds__(MG_WAVES * 64) void mega_fwd_kernel(MgLaunch L) {
   if (t < nrows) {
     float acc = 0.f;
 #pragma unroll
-    for (int w = 0; w < MG_WAVES; ++w) acc += red[w * R + t];
+    for (int w = 0; w < NW; ++w) acc += red[w * R + t];
     // F:345-F:349: log w = (log p(h) + log p(x|h)) - log q(h|x)
     L.lw[row0 + t] = (logp[t] + acc) - logq[t];
   }
   MG_TRACE(127)
 }
 
-hipError_t launch_mega_fwd(hipStream_t st, const MgLaunch& L, int rt, size_t lds_bytes) {
+hipError_t launch_mega_fwd(hipStream_t st, const MgLaunch& L, int rt, int waves, size_t lds_bytes) {
   if (L.rows <= 0) return hipSuccess;
   const int R = 16 * rt;
-  const dim3 grid((L.rows + R - 1) / R), block(MG_WAVES * 64);
+  const dim3 grid((L.rows + R - 1) / R), block(waves * 64);
+  if (waves == 4) {
+    if (rt != 2) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((mega_fwd_kernel<2, 4>), grid, block, lds_bytes, st, L);
+    return hipGetLastError();
+  }
+  if (waves != MG_WAVES) return hipErrorInvalidValue;
   switch (rt) {
-    case 1: hipLaunchKernelGGL(mega_fwd_kernel<1>, grid, block, lds_bytes, st, L); break;
-    case 2: hipLaunchKernelGGL(mega_fwd_kernel<2>, grid, block, lds_bytes, st, L); break;
-    case 4: hipLaunchKernelGGL(mega_fwd_kernel<4>, grid, block, lds_bytes, st, L); break;
+    case 1: hipLaunchKernelGGL((mega_fwd_kernel<1, MG_WAVES>), grid, block, lds_bytes, st, L); break;
+    case 2: hipLaunchKernelGGL((mega_fwd_kernel<2, MG_WAVES>), grid, block, lds_bytes, st, L); break;
+    case 4: hipLaunchKernelGGL((mega_fwd_kernel<4, MG_WAVES>), grid, block, lds_bytes, st, L); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
 hipError_t mega_setup_attributes() {
-  hipError_t e = hipFuncSetAttribute((const void*)mega_fwd_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     160 * 1024);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)mega_fwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)mega_fwd_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  return e;
+  const void* fns[] = {(const void*)mega_fwd_kernel<1, MG_WAVES>, (const void*)mega_fwd_kernel<2, MG_WAVES>,
+                       (const void*)mega_fwd_kernel<4, MG_WAVES>, (const void*)mega_fwd_kernel<2, 4>};
+  for (const void* f : fns) {
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace iwae

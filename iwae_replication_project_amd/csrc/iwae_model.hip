@@ -128,6 +128,7 @@ struct iwae_handle {
   int path = 0;                      // 0 auto, 1 layer-wise kernels, 2 fused row-block kernels
   int x3 = 1;                        // tiled GEMMs: 1 bf16x3 products (default), 0 exact f32 MFMA
   int nll_fused = 1;                 // NLL: fused k-sample forward (mega_fwd_kernel) when it fits
+  int mg_waves = 8;                  // mega_fwd_kernel workgroup: 8 waves (64 rows) or 4 (32 rows, 2 per CU)
   bool masked = false;               // active-unit masks in force (iwae_nll_masked only)
   const float* mask[IWAE_MAX_LAYERS] = {};
   // graphs
@@ -1384,6 +1385,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   h->wsplit_lo = h->wsplit_hi + h->wsplit_elems;
   e = rb_setup_attributes();
   if (e == hipSuccess) e = mega_setup_attributes();
+  if (const char* w = std::getenv("IWAE_MG_WAVES")) h->mg_waves = std::atoi(w) == 4 ? 4 : 8;   // tuning knob
   if (e == hipSuccess) e = smallm_setup_attributes();
   if (e != hipSuccess) {
     g_create_error = std::string("hipFuncSetAttribute failed: ") + hipGetErrorString(e);
@@ -1666,7 +1668,7 @@ int iwae_e_log_px(iwae_handle* h, const float* x, int B, int k, const float* con
 //   decoder prior j:     h_{L-1-j} -> Q -> P -> head: log p(h_{L-2-j} | .)
 //   output MLP:          h_0 -> Q -> P -> Dense(784) + Bernoulli
 // False if it does not fit the LDS.
-static bool mega_plan(iwae_handle* h, MgLaunch& M, int& rt, size_t& lds) {
+static bool mega_plan(iwae_handle* h, MgLaunch& M, int& rt, int& waves, size_t& lds) {
   const int L = h->L;
   std::memset(&M, 0, sizeof(M));
   auto r32 = [](int x) { return (x + 31) & ~31; };
@@ -1716,7 +1718,11 @@ static bool mega_plan(iwae_handle* h, MgLaunch& M, int& rt, size_t& lds) {
   // and the [8][R] reduction scratch as floats.  Row stride s dwords (ld = 2s):
   // s = 8 mod 16 makes the fragment reads (ds_read_b128) conflict-free; s = 4
   // mod 8 (2-way) is the fallback when that does not fit.
+  // 8-wave workgroups of 64 / 32 / 16 rows, or (h->mg_waves == 4) 4-wave
+  // workgroups of 32 rows, two per CU
+  waves = h->mg_waves == 4 ? 4 : 8;
   for (int c : {4, 2, 1}) {
+    if (waves == 4 && c != 2) continue;
     const int R = 16 * c;
     for (int pass = 0; pass < 2; ++pass) {
       int off = 0;                              // bf16 units
@@ -1730,7 +1736,7 @@ static bool mega_plan(iwae_handle* h, MgLaunch& M, int& rt, size_t& lds) {
       }
       M.acc_off = (off + 3) / 2 & ~1;           // floats
       const size_t bytes = (size_t)(M.acc_off + 2 * R + 8 * R) * sizeof(float);
-      if (bytes <= 160 * 1024) {
+      if (bytes <= (waves == 4 ? 80 : 160) * 1024) {
         rt = c;
         lds = bytes;
         for (size_t i = 0; i < st.size(); ++i) M.st[i] = st[i];
@@ -1759,9 +1765,9 @@ static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, flo
   CHK(ensure_capacity(h, imgs, imgs * kS, false));
   if (h->x3) CHK(ensure_wsplit(h));
   MgLaunch MG;
-  int mg_rt = 0;
+  int mg_rt = 0, mg_waves = 8;
   size_t mg_lds = 0;
-  const bool mega = h->x3 && h->nll_fused && !h->masked && mega_plan(h, MG, mg_rt, mg_lds);
+  const bool mega = h->x3 && h->nll_fused && !h->masked && mega_plan(h, MG, mg_rt, mg_waves, mg_lds);
   const size_t wbytes = (size_t)h->xdim * sizeof(float);
   for (int i0 = 0; i0 < N; i0 += imgs) {
     const int n = std::min(imgs, N - i0);
@@ -1781,7 +1787,7 @@ static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, flo
         MG.x = h->x_in.p; MG.ldx = h->x_in.ld;
         MG.seed = h->seed; MG.rng_base = &h->ds->rng[0];
         MG.lw = h->lw;
-        HIPCHK(launch_mega_fwd(h->stream, MG, mg_rt, mg_lds));
+        HIPCHK(launch_mega_fwd(h->stream, MG, mg_rt, mg_waves, mg_lds));
         a.lw = h->lw;
       } else {
         CHK(forward_core(h, P, E, false));
