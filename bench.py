@@ -110,10 +110,15 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    torch.cuda.set_device(local)
+    dev = local % max(1, torch.cuda.device_count())   # = local on a full node; wraps only in a 1-GPU rehearsal
+    torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("IWAE_DIST_BACKEND", "nccl")   # nccl = RCCL; gloo only to rehearse N>1 on one GPU
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     from iwae_replication_project_amd import Adam, Flexible_Model, distributed
 
     x_all, pi = synthetic_images(50_000, 1 + rank)

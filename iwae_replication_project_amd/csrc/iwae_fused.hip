@@ -287,7 +287,7 @@ __global__ __launch_bounds__(RB_WAVES * 64) void rb_fwd_kernel(RbFwdLaunch L) {
   const int blk = blockIdx.x - L.block_start[jb];
   const int row0 = blk * J.rpb;
   const int nrows = min(J.rpb, J.rows - row0);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  [[maybe_unused]] const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;   // trace build
   const int lda = L.ld_lds;
   const int bo[3] = {0, RB_ROWS * lda, 2 * RB_ROWS * lda};   // LDS images (offsets into rbs)
   const int oq = 3 * RB_ROWS * lda;                           // [16] log q of the sampled input
