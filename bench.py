@@ -8,7 +8,9 @@ Data: synthetic fixed-binarised 784-pixel images (MNIST-like pixel means,
 mean ~0.13) resident in HBM; Glorot weights.  `value` = sample-rows (images*k)
 per second over all ranks (weak scaling: 20 images per GPU, RCCL gradient
 all-reduce for N > 1).  The k=5000 NLL over 10k synthetic images (configs[2],
-sharded by image) is reported beside it under "nll".
+sharded by image) is reported beside it under "nll", and the large-batch data-
+parallel train step (configs[4]: B=4096 over 8 GPUs, i.e. 512 images per GPU,
+k=50) under "large_batch" -- weak scaling at that per-GPU share.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...    (one process per GPU)
@@ -29,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 HE, HD, LE, LD = [200, 100], [100, 200], [100, 50], [100, 784]
 B_PER_GPU, K = 20, 50
+LARGE_B_PER_GPU = 512              # configs[4]: global batch 4096 over 8 GPUs
 # algorithmic train FLOP per image*sample, 2L k=50
 TRAIN_FLOP_PER_ROW = 1_712_944
 NLL_FLOP_PER_IMAGE = 2.818e9
@@ -100,6 +103,8 @@ def main():
     ap.add_argument("--nll-images", type=int, default=10000)
     ap.add_argument("--nll-k", type=int, default=5000)
     ap.add_argument("--no-nll", action="store_true")
+    ap.add_argument("--no-large-batch", action="store_true")
+    ap.add_argument("--large-batch-steps", type=int, default=20)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-graphs", action="store_true")
@@ -192,6 +197,36 @@ def main():
                     avg_us=round(avg_ms * 1e3, 3), flop_per_launch=flop_per_launch, launches=int(nl.value),
                     step_tflops=round(TRAIN_FLOP_PER_ROW * rows / el / 1e12, 3))
 
+    # ---- configs[4] per-GPU share: B=512 images per GPU, k=50, same model and
+    # step (RCCL gradient all-reduce for N > 1)
+    large = None
+    if not args.no_large_batch:
+        bl = LARGE_B_PER_GPU
+        xl = model._x(synthetic_images(4 * bl, 7 + rank)[0])
+        lbs = [xl[i * bl:(i + 1) * bl] for i in range(4)]
+        for i in range(3):
+            model.train_step(lbs[i % 4], sync=False)
+        model._stream.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        for i in range(args.large_batch_steps):
+            model.train_step(lbs[i % 4], sync=False)
+        model._stream.synchronize()
+        torch.cuda.synchronize()
+        barrier()
+        el3 = time.perf_counter() - t2
+        if world > 1:
+            t = torch.tensor([el3], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el3 = float(t.item())
+        lrows = world * bl * K * args.large_batch_steps
+        ltf = TRAIN_FLOP_PER_ROW * lrows / el3 / 1e12
+        large = dict(value=round(lrows / el3, 1), unit="image*samples/s", per_gpu_batch=bl, global_batch=bl * world,
+                     k=K, steps=args.large_batch_steps, ms_per_step=round(1e3 * el3 / args.large_batch_steps, 4),
+                     tflops=round(ltf, 3), frac_of_fp32_mfma_peak=round(ltf / (FP32_MFMA_PEAK_TFLOPS * world), 4),
+                     workload="BASELINE configs[4] per-GPU share (4096 over 8 GPUs)")
+
     # ---- k=5000 NLL over the test images, sharded by image
     nll = None
     if not args.no_nll:
@@ -247,6 +282,7 @@ def main():
                        "noise": "device Philox", "graphs": not args.no_graphs},
             "loss": round(loss, 4),
             "nll": nll,
+            "large_batch": large,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
