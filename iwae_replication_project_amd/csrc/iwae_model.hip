@@ -1059,7 +1059,9 @@ static int fused_decoder_bwd(iwae_handle* h, const Plan& P, const float* dlw, co
       a.C = h->ob.dY2.p; a.ldc = h->ob.dY2.ld;
     }
     CHK(prof_begin(h, GEMM_BWD_DATA, EPI_TANH_GRAD, 2.0 * M * d.fout * d.fin));
-    HIPCHK(launch_gemm(h->stream, GEMM_BWD_DATA, EPI_TANH_GRAD, 0, oS, false, a));
+    // large batches: 128x128 tiles (B=512, k=50: 1.132 vs 1.158 ms per step)
+    const int tile = (oS == 1 && M >= 8192) ? 1 : 0;
+    HIPCHK(launch_gemm(h->stream, GEMM_BWD_DATA, EPI_TANH_GRAD, tile, oS, false, a));
     CHK(prof_end(h, GEMM_BWD_DATA, EPI_TANH_GRAD));
   }
   RbBwdLaunch Lb{};
