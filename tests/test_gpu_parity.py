@@ -196,6 +196,26 @@ def test_fused_and_layerwise_paths_agree(arch, loss):
     np.testing.assert_allclose(wb, wa, atol=2 * ADAM_ATOL)      # see the Adam note above
 
 
+def test_fused_and_layerwise_paths_agree_at_large_batch():
+    """configs[1]/[4] architecture at 10,000 sample rows (B=200, k=50): the
+    large-batch kernel choices of the fused step (128x128 output-layer dX
+    tiles, more weight-gradient slabs) against the layer-wise step."""
+    he, hd, le, ld = [200, 100], [100, 200], [100, 50], [100, 784]
+    rng = np.random.default_rng(23)
+    x = (rng.random((200, 784)) < 0.15).astype(np.float32)
+    outs = []
+    for path in ("layerwise", "fused"):
+        from iwae_replication_project_amd import Adam
+        m = make_model(he, hd, le, ld, loss="IWAE", k=50, seed=78, kernel_path=path)
+        m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+        l1 = m.train_step(x)["IWAE"]
+        outs.append((l1, flat(m.get_gradients()), flat(m.get_weights())))
+    (a1, ga, wa), (b1, gb, wb) = outs
+    assert abs(a1 - b1) <= 2 * REL * abs(a1)
+    assert rel_l2(gb, ga) <= 2 * REL
+    np.testing.assert_allclose(wb, wa, atol=2 * ADAM_ATOL)
+
+
 # ----------------------------------------------- multi-step training parity
 def test_five_adam_steps_track_oracle():
     from oracle import iwae_oracle as O
