@@ -89,9 +89,11 @@ def train_schedule(model, x_train, stages=8, batch_size=100, x_test=None, k_test
     """The reference's training driver (E:73-E:97): for stage i = 1..stages set
     the Adam learning rate (E:76), run passes(i) epochs of fit (E:82), then
     optionally evaluate get_training_statistics(x_test, k_test) (E:87),
-    call on_stage(i, total_passes, res) and save the weights (E:95).  With
-    stochastic_rng the training set is re-binarised every epoch.  Returns
-    the list of per-stage statistics."""
+    call on_stage(i, total_passes, res) and save the weights (E:95) and the
+    statistics so far (E:96-E:97: the reference pickles (res1s, res2s); here
+    they are JSON, `<save_prefix>.res2.json`).  With stochastic_rng the
+    training set is re-binarised every epoch.  Returns the list of per-stage
+    statistics ((res1, res2) pairs, or None without x_test)."""
     if model.optimizer is None:
         model.compile()
     results = []
@@ -112,4 +114,39 @@ def train_schedule(model, x_train, stages=8, batch_size=100, x_test=None, k_test
             on_stage(i, total, res)
         if save_prefix is not None:
             model.save_weights(f"{save_prefix}-epoch_{i}.npz")
+            if x_test is not None:
+                save_results(f"{save_prefix}.res2.json", results)
     return results
+
+
+def default_prefix(model):
+    """The reference's file stem (E:95): <loss>-<L>L-k_<k>."""
+    return f"{model.loss_function}-{len(model.n_latent_encoder)}L-k_{model.k}"
+
+
+def _plain(v):
+    if isinstance(v, dict):
+        return {k: _plain(x) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return [_plain(x) for x in v]
+    if isinstance(v, np.ndarray):
+        return v.tolist()
+    if isinstance(v, np.generic):
+        return v.item()
+    return v
+
+
+def save_results(path, results):
+    """(res1s, res2s) of the stages so far as JSON (E:96-E:97 without pickle)."""
+    import json
+    res1s = [r[0] for r in results if r is not None]
+    res2s = [r[1] for r in results if r is not None]
+    with open(path, "w") as f:
+        json.dump({"res1s": _plain(res1s), "res2s": _plain(res2s)}, f)
+
+
+def load_results(path):
+    import json
+    with open(path) as f:
+        d = json.load(f)
+    return d["res1s"], d["res2s"]

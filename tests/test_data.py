@@ -63,3 +63,41 @@ def test_stochastic_binarisation_and_bias():
     bias = D.bias_from_train(xb)
     m = np.clip(xb.astype(np.float64).mean(0), 0.001, 0.999)
     np.testing.assert_allclose(bias, -np.log(1.0 / m - 1.0))
+
+
+class _FakeModel:
+    """Duck-typed stand-in for Flexible_Model: records the driver's calls."""
+    loss_function, k, n_latent_encoder = "IWAE", 5, [8, 4]
+
+    def __init__(self):
+        class _Opt:
+            learning_rate = None
+        self.optimizer = _Opt()
+        self.lrs, self.fits, self.saved = [], 0, []
+
+    def _push_adam(self):
+        self.lrs.append(self.optimizer.learning_rate)
+
+    def fit(self, x, epochs=1, batch_size=100, verbose=0):
+        self.fits += epochs
+
+    def get_training_statistics(self, x, k):
+        return {"NLL": 90.0 + self.fits}, {"variances": [np.ones(2)], "active_units": [[1, 0]]}
+
+    def save_weights(self, path):
+        self.saved.append(path)
+
+
+def test_train_schedule_stages_saves_and_results_roundtrip(tmp_path):
+    from iwae_replication_project_amd import data as D
+    m = _FakeModel()
+    prefix = str(tmp_path / D.default_prefix(m))
+    res = D.train_schedule(m, np.zeros((4, 784), np.float32), stages=3, x_test=np.zeros((2, 784), np.float32),
+                           save_prefix=prefix)
+    assert m.fits == 1 + 3 + 9                                     # E:77: 3**(i-1) passes
+    np.testing.assert_allclose(m.lrs, [1e-3, 7.2e-4, 5.2e-4])      # E:76: 1e-4*round(10**(1-(i-1)/7), 1)
+    assert m.saved == [f"{prefix}-epoch_{i}.npz" for i in (1, 2, 3)]
+    assert prefix.endswith("IWAE-2L-k_5")
+    r1, r2 = D.load_results(prefix + ".res2.json")
+    assert [r["NLL"] for r in r1] == [91.0, 94.0, 103.0] == [r[0]["NLL"] for r in res]
+    assert r2[0]["variances"] == [[1.0, 1.0]] and r2[2]["active_units"] == [[1, 0]]
