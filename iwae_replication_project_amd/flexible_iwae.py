@@ -237,7 +237,7 @@ class Flexible_Model:
         t = torch.as_tensor(x)
         if t.dim() < 2:
             raise ValueError("x must be [B, 28, 28, 1] or [B, 784]")
-        t = t.reshape(t.shape[0], -1)
+        t = t.reshape(t.shape[0], int(np.prod(t.shape[1:])))     # explicit width: an empty batch stays [0, 784]
         if t.shape[1] != self.x_dim:                      # F:57 assert(x.shape[1] == 28*28)
             raise ValueError(f"x must flatten to {self.x_dim} pixels, got {t.shape[1]}")
         with torch.cuda.stream(self._stream):

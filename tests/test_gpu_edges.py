@@ -1,0 +1,109 @@
+"""GPU edge cases of the train step against the float64 oracle: ragged batch
+sizes around the kernels' row-block / few-row / tile boundaries, k = 1 (the
+LSE over one sample, F:369), batch-size changes between captured-graph
+replays, and the argument errors the C ABI reports.  Same tolerances as
+test_gpu_parity.py (north_star: 1e-4 relative on losses and gradients)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-4
+ADAM_ATOL = 6e-5        # see test_gpu_parity.py: Adam's first step amplifies near-zero gradient errors
+ARCH2 = ([200, 100], [100, 200], [100, 50], [100, 784])     # BASELINE configs[1] architecture
+
+
+def _flat(ws):
+    return np.concatenate([np.asarray(w, np.float64).ravel() for w in ws])
+
+
+def _rel_l2(a, b):
+    return float(np.linalg.norm(np.asarray(a) - np.asarray(b)) / max(np.linalg.norm(b), 1e-30))
+
+
+def _model(arch, loss, k, **kw):
+    from iwae_replication_project_amd import Adam, Flexible_Model
+    he, hd, le, ld = arch
+    m = Flexible_Model(he, hd, le, ld, dataset_bias=None, loss_function=loss, k=k, seed=3, **kw)
+    m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+    return m
+
+
+def _oracle_case(arch, B, k, seed):
+    from oracle import iwae_oracle as O
+    he, hd, le, ld = arch
+    rng = np.random.default_rng(seed)
+    mean = rng.uniform(0.01, 0.4, 784)
+    spec = O.ModelSpec(he, hd, le, ld)
+    params = O.glorot_init(spec, rng, out_bias=O.output_bias_from_mean(mean))
+    params = {n: [w.astype(np.float32).astype(np.float64), b.astype(np.float32).astype(np.float64)]
+              for n, (w, b) in params.items()}
+    x = (rng.random((B, 784)) < mean).astype(np.float64)
+    eps = [e.astype(np.float32).astype(np.float64) for e in O.draw_eps(spec, k, B, rng)]
+    return O, spec, params, x, eps
+
+
+# B: 1 image; 15/17 around the 16-row blocks; 32/33 around the few-row input-layer
+# path (<= 32 images); k=1 and odd k put the sample rows off every tile boundary
+@pytest.mark.parametrize("B,k", [(1, 1), (1, 50), (15, 3), (17, 7), (32, 50), (33, 50), (65, 13)])
+def test_ragged_batches_match_oracle(B, k):
+    from iwae_replication_project_amd.flexible_iwae import _split, weight_shapes
+    O, spec, params, x, eps = _oracle_case(ARCH2, B, k, 100 + 7 * B + k)
+    m = _model(ARCH2, "IWAE", k)
+    m.set_weights(_split(O.flatten_params(spec, params).astype(np.float32), weight_shapes(m.dense)))
+    loss = m.train_step(x.astype(np.float32), eps=[e.astype(np.float32) for e in eps])["IWAE"]
+    opt = O.Adam(1e-3, 0.9, 0.999, 1e-4)
+    ref_loss, ref_new, ref_g = O.train_step(params, spec, x, eps, "IWAE", k, opt)
+    assert abs(loss - ref_loss) <= REL * abs(ref_loss), (loss, ref_loss)
+    assert _rel_l2(_flat(m.get_gradients()), ref_g) <= REL
+    np.testing.assert_allclose(_flat(m.get_weights()), O.flatten_params(spec, ref_new), atol=ADAM_ATOL)
+
+
+def test_k1_iwae_equals_vae():
+    """IWAE with k = 1 is the VAE bound (F:369 vs F:331): same noise, same loss and gradient."""
+    rng = np.random.default_rng(5)
+    x = (rng.random((9, 784)) < 0.2).astype(np.float32)
+    eps = [rng.standard_normal((1, 9, d)).astype(np.float32) for d in ARCH2[2]]
+    out = []
+    for loss in ("IWAE", "VAE"):
+        m = _model(ARCH2, loss, 1)
+        out.append((m.train_step(x, eps=eps)[loss], _flat(m.get_gradients())))
+    (a, ga), (b, gb) = out
+    assert abs(a - b) <= REL * abs(a)
+    assert _rel_l2(ga, gb) <= REL
+
+
+def test_batch_size_changes_between_graph_replays():
+    """Captured graphs are per batch shape: alternating batch sizes (few-row
+    path, its boundary and the tiled path) give bit-identical losses and
+    weights with and without graphs."""
+    import torch
+    rng = np.random.default_rng(41)
+    xs = (rng.random((120, 784)) < 0.2).astype(np.float32)
+    sizes = [20, 7, 33, 20, 64, 7, 20]
+    runs = []
+    for graphs in (True, False):
+        m = _model(ARCH2, "IWAE", 50, use_graphs=graphs)
+        X = torch.from_numpy(xs).to(m.device)
+        losses, o = [], 0
+        for b in sizes:
+            losses.append(m.train_step(X[o:o + b])["IWAE"])
+            o = (o + b) % 50
+        runs.append((losses, _flat(m.get_weights())))
+    assert runs[0][0] == runs[1][0]
+    np.testing.assert_array_equal(runs[0][1], runs[1][1])
+
+
+def test_invalid_arguments_raise():
+    """An empty batch and p = 0 are rejected by the C ABI (IWAE_EINVAL, raised as
+    ValueError, the F:242 analogue); wrong eps counts and shapes by the facade."""
+    m = _model(ARCH2, "IWAE", 5)
+    with pytest.raises(ValueError):
+        m.train_step(np.zeros((0, 784), np.float32))
+    x = np.zeros((4, 784), np.float32)
+    with pytest.raises(ValueError):
+        m.train_step(x, eps=[np.zeros((5, 4, 100), np.float32)])          # one eps buffer for two layers
+    with pytest.raises(ValueError):
+        _model(ARCH2, "L_power_p", 5, p=0.0).train_step(x)
+    with pytest.raises(ValueError):
+        m.train_step(x, eps=[np.zeros((5, 3, 100), np.float32), np.zeros((5, 3, 50), np.float32)])   # wrong B
