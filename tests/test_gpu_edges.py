@@ -107,3 +107,18 @@ def test_invalid_arguments_raise():
         _model(ARCH2, "L_power_p", 5, p=0.0).train_step(x)
     with pytest.raises(ValueError):
         m.train_step(x, eps=[np.zeros((5, 3, 100), np.float32), np.zeros((5, 3, 50), np.float32)])   # wrong B
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_nll_k5000_single_and_few_images_match_oracle(B):
+    """k=5000 log p(x) per image (F:463-F:464) on the configs[1] architecture for
+    1 and 3 images, with the oracle's own noise injected: within the
+    north_star's 0.05 nats per image."""
+    O, spec, params, x, eps = _oracle_case(ARCH2, B, 5000, 500 + B)
+    from iwae_replication_project_amd.flexible_iwae import _split, weight_shapes
+    m = _model(ARCH2, "IWAE", 5)
+    m.set_weights(_split(O.flatten_params(spec, params).astype(np.float32), weight_shapes(m.dense)))
+    lp = m.log_px(x.astype(np.float32), 5000, eps=[e.astype(np.float32) for e in eps]).cpu().numpy()
+    ref = O.log_px_per_image(params, spec, x, 5000, eps=eps, chunk=1000)
+    assert lp.shape == (B,)
+    assert np.max(np.abs(lp - ref)) <= 0.05, (lp, ref)
