@@ -105,6 +105,8 @@ struct iwae_handle {
   long long wsplit_elems = 0;
   long long params_version = 1, wsplit_version = 0;   // split copies current iff equal
   bool in_train_step = false;        // weight-operand GEMMs of a train step stay exact f32
+  bool out_x3 = false;               // ... except the output layer's two GEMMs of a large-batch step (bf16x3)
+  long long out_x3_rows = 8192;      // sample rows from which a train step takes that exception (0: never)
   DevState* ds = nullptr;
   uint64_t seed = 0x5eed5eedULL;
   // workspace
@@ -364,6 +366,12 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
 // --------------------------------------------------------------- GEMMs
 // pre-split B operand (weights) for a bf16x3 GEMM: only outside the train step
 static bool use_split_b(const iwae_handle* h) { return h->x3 && !h->in_train_step; }
+// split-weight (bf16x3) operand for Dense d: every tiled GEMM outside the train
+// step; inside it only the output layer of a large-batch step, whose split copy
+// the step refreshes first (run_wsplit_seg)
+static bool split_b_for(const iwae_handle* h, const DenseL& d) {
+  return use_split_b(h) || (h->out_x3 && &d == &h->dense[h->o3]);
+}
 
 static int choose_tile(long long M, long long N, int splits) {
   return (cdiv(M, 128) * cdiv(N, 128) * splits >= 512) ? 1 : 0;
@@ -404,14 +412,14 @@ static int prof_end(iwae_handle* h, GemmKind kind, GemmEpi epi) {
 static int gemm_fwd(iwae_handle* h, GemmEpi epi, const Mat& X, int rows, const DenseL& d, Mat& Y,
                     GemmArgs extra = GemmArgs{}) {
   GemmArgs a = extra;
-  a.x3 = h->in_train_step ? 0 : h->x3;     // weight operand: exact f32 inside the train step
+  a.x3 = split_b_for(h, d) ? 1 : 0;       // weight operand: exact f32 inside the train step (but see out_x3)
   a.A = X.p; a.lda = X.ld;
   a.B = h->params + d.off; a.ldb = d.ldw;
   a.C = Y.p; a.ldc = Y.ld;
   a.M = rows; a.N = d.fout; a.K = d.fin + 1;
   a.kchunk = a.K;
   a.c_split_stride = 0;
-  if (use_split_b(h)) { a.Bhi = h->wsplit_hi + d.f_off; a.Blo = h->wsplit_lo + d.f_off; a.ldbx = d.ldF; }
+  if (split_b_for(h, d)) { a.Bhi = h->wsplit_hi + d.f_off; a.Blo = h->wsplit_lo + d.f_off; a.ldbx = d.ldF; }
   CHK(prof_begin(h, GEMM_FWD, epi, 2.0 * rows * d.fout * d.fin));
   prof_note(h, GEMM_FWD, epi, choose_tile(a.M, a.N, 1), 1, false, a, 2.0 * rows * d.fout * d.fin);
   HIPCHK(launch_gemm(h->stream, GEMM_FWD, epi, choose_tile(a.M, a.N, 1), 1, false, a));
@@ -423,14 +431,14 @@ static int gemm_fwd(iwae_handle* h, GemmEpi epi, const Mat& X, int rows, const D
 static int gemm_bwd_data(iwae_handle* h, const Mat& dZ, int rows, const DenseL& d, Mat& dX,
                          const Mat* Y, const float* rowscale) {
   GemmArgs a{};
-  a.x3 = h->in_train_step ? 0 : h->x3;     // weight operand: exact f32 inside the train step
+  a.x3 = split_b_for(h, d) ? 1 : 0;       // weight operand: exact f32 inside the train step (but see out_x3)
   a.A = dZ.p; a.lda = dZ.ld;
   a.B = h->params + d.off; a.ldb = d.ldw;
   a.C = dX.p; a.ldc = dX.ld;
   a.M = rows; a.N = d.fin; a.K = d.fout;
   a.kchunk = a.K;
   a.rowscale = rowscale;
-  if (use_split_b(h)) { a.Bhi = h->wsplit_hi + d.g_off; a.Blo = h->wsplit_lo + d.g_off; a.ldbx = d.ldG; }
+  if (split_b_for(h, d)) { a.Bhi = h->wsplit_hi + d.g_off; a.Blo = h->wsplit_lo + d.g_off; a.ldbx = d.ldG; }
   GemmEpi epi = EPI_STORE;
   if (Y) { a.aux = Y->p; a.ldaux = Y->ld; epi = EPI_TANH_GRAD; }
   CHK(prof_begin(h, GEMM_BWD_DATA, epi, 2.0 * rows * d.fout * d.fin));
@@ -719,6 +727,22 @@ static int run_wsplit(iwae_handle* h) {
   }
   a.nseg = (int)h->dense.size();
   HIPCHK(launch_wsplit(h->stream, a, mx));
+  return IWAE_OK;
+}
+
+// refresh one Dense layer's split copy (the train step's output layer, on the
+// step's stream, so a captured graph re-splits after every Adam update);
+// the other layers' copies stay stale until ensure_wsplit
+static int run_wsplit_seg(iwae_handle* h, int di) {
+  WSplitArgs a{};
+  a.param = h->params; a.hi = h->wsplit_hi; a.lo = h->wsplit_lo;
+  const DenseL& d = h->dense[di];
+  WSplitSeg& g = a.seg[0];
+  g.off = d.off; g.fin = d.fin; g.fout = d.fout; g.ldw = d.ldw;
+  g.f_off = d.f_off; g.g_off = d.g_off; g.ldF = d.ldF; g.ldG = d.ldG;
+  a.nseg = 1;
+  HIPCHK(launch_wsplit(h->stream, a, (long long)(d.fin + 1) * d.fout));
+  h->wsplit_version = -1;
   return IWAE_OK;
 }
 
@@ -1039,12 +1063,12 @@ static int fused_decoder_bwd(iwae_handle* h, const Plan& P, const float* dlw, co
   {
     const DenseL& d = h->dense[h->o3];
     GemmArgs a{};
-    a.x3 = h->in_train_step ? 0 : h->x3;
+    a.x3 = split_b_for(h, d) ? 1 : 0;
     a.A = h->ob.P.p; a.lda = h->ob.P.ld;
     a.B = h->params + d.off; a.ldb = d.ldw;
     a.M = M; a.N = d.fin; a.K = d.fout;
     a.rowscale = dpx; a.aux = h->ob.y2.p; a.ldaux = h->ob.y2.ld;
-    if (use_split_b(h)) { a.Bhi = h->wsplit_hi + d.g_off; a.Blo = h->wsplit_lo + d.g_off; a.ldbx = d.ldG; }
+    if (split_b_for(h, d)) { a.Bhi = h->wsplit_hi + d.g_off; a.Blo = h->wsplit_lo + d.g_off; a.ldbx = d.ldG; }
     const long long tiles = cdiv(M, 64) * cdiv(d.fin, 64);
     if (h->oslab && h->oslab_S > 1 && tiles < 256) {
       oS = (int)std::min<long long>(h->oslab_S, cdiv(256, tiles));
@@ -1216,6 +1240,10 @@ static int fused_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool
 
 // forward + backward (+ Adam) after x is staged
 static int train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
+  // large batches: the output layer's forward (Bernoulli) and dX GEMMs on bf16x3
+  // products of a split copy refreshed here, after the previous step's Adam
+  h->out_x3 = h->x3 && h->out_x3_rows > 0 && (long long)P.Bimg * P.kS >= h->out_x3_rows;
+  if (h->out_x3) CHK(run_wsplit_seg(h, h->o3));
   if (use_fused(h, P)) return fused_train_body(h, P, E, adam);
   CHK(forward_core(h, P, E, true));
   CHK(run_bound(h, P, true, -1.f, train_loss_ptr(h), adam));
@@ -1249,7 +1277,7 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
   h->in_train_step = true;
   struct Reset {
     iwae_handle* h;
-    ~Reset() { h->in_train_step = false; h->x_user = nullptr; h->capturing = false; }
+    ~Reset() { h->in_train_step = false; h->out_x3 = false; h->x_user = nullptr; h->capturing = false; }
   } reset_flag{h};
   if (h->use_graphs && philox && h->prof_kind < 0) {
     std::vector<long long> key = {adam ? 1 : 0, lc->loss, B, lc->k, lc->k1, lc->k2, (long long)(uintptr_t)loss_dev,
@@ -1387,6 +1415,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   h->wsplit_lo = h->wsplit_hi + h->wsplit_elems;
   e = rb_setup_attributes();
   if (e == hipSuccess) e = mega_setup_attributes();
+  if (const char* w = std::getenv("IWAE_TRAIN_OUT_X3_ROWS")) h->out_x3_rows = std::atoll(w);   // tuning knob
   if (const char* w = std::getenv("IWAE_MG_WAVES")) h->mg_waves = std::atoi(w) == 4 ? 4 : 8;   // tuning knob
   if (e == hipSuccess) e = smallm_setup_attributes();
   if (e != hipSuccess) {

@@ -45,7 +45,8 @@ def _oracle_case(arch, B, k, seed):
 
 # B: 1 image; 15/17 around the 16-row blocks; 32/33 around the few-row input-layer
 # path (<= 32 images); k=1 and odd k put the sample rows off every tile boundary
-@pytest.mark.parametrize("B,k", [(1, 1), (1, 50), (15, 3), (17, 7), (32, 50), (33, 50), (65, 13)])
+# (200, 50): 10,000 sample rows, where the output layer's GEMMs switch to bf16x3 products
+@pytest.mark.parametrize("B,k", [(1, 1), (1, 50), (15, 3), (17, 7), (32, 50), (33, 50), (65, 13), (200, 50)])
 def test_ragged_batches_match_oracle(B, k):
     from iwae_replication_project_amd.flexible_iwae import _split, weight_shapes
     O, spec, params, x, eps = _oracle_case(ARCH2, B, k, 100 + 7 * B + k)
