@@ -225,7 +225,9 @@ def main():
         large = dict(value=round(lrows / el3, 1), unit="image*samples/s", per_gpu_batch=bl, global_batch=bl * world,
                      k=K, steps=args.large_batch_steps, ms_per_step=round(1e3 * el3 / args.large_batch_steps, 4),
                      tflops=round(ltf, 3), frac_of_fp32_mfma_peak=round(ltf / (FP32_MFMA_PEAK_TFLOPS * world), 4),
-                     workload="BASELINE configs[4] per-GPU share (4096 over 8 GPUs)")
+                     workload="BASELINE configs[4] per-GPU share (4096 over 8 GPUs)",
+                     precision="as the train step, except the output layer's Bernoulli and dX GEMMs: bf16x3 "
+                               "(>= 8192 sample rows, DESIGN.md section 4)")
 
     # ---- k=5000 NLL over the test images, sharded by image
     nll = None
