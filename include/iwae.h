@@ -93,6 +93,12 @@ const char* iwae_last_error(const iwae_handle* h);
 int iwae_set_stream(iwae_handle* h, void* hip_stream);
 int iwae_synchronize(iwae_handle* h);
 int iwae_set_seed(iwae_handle* h, unsigned long long seed);
+/* Noise stream of this handle (one per rank): the Philox key becomes
+ * splitmix64(seed ^ splitmix64(stream)) for stream != 0 (stream 0: the seed
+ * itself), so ranks that share a seed still draw independent noise -- the iid
+ * draws of F:59 qh1Ix.sample(n) / F:68 .sample() hold across the ranks of a
+ * data-parallel step or a sample-sharded NLL.  Restarts the Philox counter. */
+int iwae_set_noise_stream(iwae_handle* h, unsigned long long stream);
 /* 1 = capture the Philox train step in a hipGraph per shape and replay it. */
 int iwae_set_graphs(iwae_handle* h, int enable);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --
@@ -142,8 +148,34 @@ int iwae_bind_grad_buffer(iwae_handle* h, float* grad_dev, long long n);
  * iwae_export_internal converts such a buffer to the Keras weight order. */
 int iwae_grad_moments(iwae_handle* h, float* sum_dev, float* sumsq_dev);
 int iwae_export_internal(iwae_handle* h, const float* internal_dev, float* host, long long n);
-/* Adam over the gradient buffer times grad_scale (1/world_size under DP). */
+/* Adam over the gradient buffer times grad_scale.  grad_scale <= 0 (data
+ * parallel, after iwae_dp_init): 1 / the buffer's tail element, i.e. the
+ * all-reduced sum of the ranks' batch sizes (see iwae_dp_init).  The scaled
+ * gradient is written back, so iwae_get_grads returns what Adam used. */
 int iwae_apply_adam(iwae_handle* h, float grad_scale);
+
+/* --- data parallelism (SURVEY s8(e), configs[4]) --------------------------- */
+/* Make this handle rank `rank` of `world`.  Effects:
+ *  - noise stream = rank (iwae_set_noise_stream): per-rank iid Philox noise;
+ *  - iwae_forward_backward writes B_local * grad into the gradient buffer and
+ *    B_local into its tail element n (the buffer then needs n + 4 floats: the
+ *    handle's own one has them; a bound one must too), so one sum all-reduce of
+ *    n + 4 floats yields sum_r B_r g_r and B_global = sum_r B_r, and
+ *    iwae_apply_adam(h, 0) steps with the exact global batch-mean gradient
+ *    (each rank's loss is its local batch mean, F:369) for unequal shards too;
+ *  - rccl_unique_id != NULL (128 bytes of ncclGetUniqueId from rank 0, see
+ *    iwae_dp_unique_id): the library creates an RCCL communicator over xGMI and
+ *    iwae_train_step then runs forward_backward -> ncclAllReduce(sum) on the
+ *    handle's stream -> Adam as one step (one hipGraph when graphs are on).
+ *    With NULL, the caller reduces the buffer itself between
+ *    iwae_forward_backward and iwae_apply_adam(h, 0); iwae_train_step then
+ *    returns IWAE_EINVAL.
+ * world == 1 with NULL restores single-process behaviour. */
+int iwae_dp_unique_id(void* out128);
+int iwae_dp_init(iwae_handle* h, int rank, int world, const void* rccl_unique_id);
+/* Broadcast parameters, Adam moments and the Adam step from rank 0 over the
+ * library communicator (needs iwae_dp_init with an RCCL id); synchronous. */
+int iwae_dp_broadcast_state(iwae_handle* h);
 
 /* --- evaluation ----------------------------------------------------------- */
 /* get_log_weights (F:327-F:351): lw [dev] [B][k] (image-major). */
@@ -196,6 +228,9 @@ int iwae_debug_gemm(iwae_handle* h, const float* A, int lda, const float* B, int
                     float* C, int ldc, int M, int N, int K);
 /* Bytes of device workspace currently allocated by the handle. */
 double iwae_workspace_bytes(const iwae_handle* h);
+/* Launch counters (tests): what = 0 fused k-sample NLL kernel (mega_fwd_kernel)
+ * launches, 1 those of them fed injected noise; -1 for an unknown id. */
+long long iwae_debug_count(const iwae_handle* h, int what);
 /* Live kernel timing: bracket every launch of one GEMM class (kind: 0 forward,
  * 1 backward-data, 2 backward-weight; epi: 0 store, 1 tanh, 2 Bernoulli,
  * 3 tanh-grad; kind = -1 disables) with HIP events on the handle's stream.

@@ -51,6 +51,7 @@ SIGNATURES = {
     "iwae_set_stream": (c_int, [H, c_void_p]),
     "iwae_synchronize": (c_int, [H]),
     "iwae_set_seed": (c_int, [H, c_ulonglong]),
+    "iwae_set_noise_stream": (c_int, [H, c_ulonglong]),
     "iwae_set_graphs": (c_int, [H, c_int]),
     "iwae_set_path": (c_int, [H, c_int]),
     "iwae_set_precision": (c_int, [H, c_int]),
@@ -66,6 +67,9 @@ SIGNATURES = {
     "iwae_grad_buffer": (c_int, [H, POINTER(FP), POINTER(c_longlong)]),
     "iwae_bind_grad_buffer": (c_int, [H, FP, c_longlong]),
     "iwae_apply_adam": (c_int, [H, c_float]),
+    "iwae_dp_unique_id": (c_int, [c_void_p]),
+    "iwae_dp_init": (c_int, [H, c_int, c_int, c_void_p]),
+    "iwae_dp_broadcast_state": (c_int, [H]),
     "iwae_grad_moments": (c_int, [H, FP, FP]),
     "iwae_export_internal": (c_int, [H, FP, FP, c_longlong]),
     "iwae_log_weights": (c_int, [H, FP, c_int, c_int, FPP, c_int, FP]),
@@ -79,6 +83,7 @@ SIGNATURES = {
     "iwae_nll_masked": (c_int, [H, FP, c_int, c_int, FPP, c_int, FPP, c_int, FP]),
     "iwae_debug_gemm": (c_int, [H, FP, c_int, FP, c_int, FP, c_int, c_int, c_int, c_int]),
     "iwae_workspace_bytes": (c_double, [H]),
+    "iwae_debug_count": (c_longlong, [H, c_int]),
     "iwae_profile_gemm": (c_int, [H, c_int, c_int]),
     "iwae_profile_read": (c_int, [H, POINTER(c_double), POINTER(c_double), POINTER(c_longlong)]),
     "iwae_profile_replay": (c_int, [H, c_int, POINTER(c_double), POINTER(c_double)]),

@@ -585,17 +585,23 @@ __device__ __forceinline__ void adam_one(const AdamArgs& a, const AdamSeg& sg, l
     } else {
       g = *reinterpret_cast<const float4*>(a.grad + pidx);
     }
+    // gradient scale: data parallel 1 / (sum of the ranks' batch sizes), else the
+    // launch's override (a rank's batch size in the DP write pass), else the state's
+    float scale = 1.f;
+    if (a.scale_dev) scale = 1.f / *a.scale_dev;
+    else if (a.grad_scale_override > 0.f) scale = a.grad_scale_override;
+    else if (a.do_adam) scale = a.state->grad_scale;
+    if (scale != 1.f) { g.x *= scale; g.y *= scale; g.z *= scale; g.w *= scale; }
     if (a.write_grad) *reinterpret_cast<float4*>(a.grad + pidx) = g;
     if (a.do_adam) {
       // the step's Adam constants (state->t was already advanced for this step by
       // the bound kernel / adam_tick_kernel); read after the data loads are issued
       const AdamState st = *a.state;
-      const float scale = a.grad_scale_override > 0.f ? a.grad_scale_override : st.grad_scale;
       const float t = (float)st.t;
       const float b1p = powf(st.b1, t), b2p = powf(st.b2, t);
       const float alpha = st.lr * sqrtf(1.f - b2p) / (1.f - b1p);
       const float omb1 = 1.f - st.b1, omb2 = 1.f - st.b2, eps = st.eps;
-      float gg[4] = {g.x * scale, g.y * scale, g.z * scale, g.w * scale};
+      float gg[4] = {g.x, g.y, g.z, g.w};
       float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w}, pp[4] = {p.x, p.y, p.z, p.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -632,6 +638,7 @@ __device__ __forceinline__ void adam_one(const AdamArgs& a, const AdamSeg& sg, l
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const long long gi = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long g0 = gi - (threadIdx.x & 63);
+  if (a.tail && gi == 0) *a.tail = a.tail_val;
   long long c = 0;
   for (int s = 0; s < a.nseg; ++s) {
     const long long n4 = a.seg[s].n >> 2;     // segment sizes and offsets are multiples of 4 floats

@@ -280,6 +280,8 @@ struct AdamArgs {
   int write_grad, do_adam, read_slabs;
   AdamState* state; unsigned* ticket;
   float grad_scale_override;   // >0: use this instead of state->grad_scale
+  const float* scale_dev;      // data parallel: scale = 1 / *scale_dev (the all-reduced batch total), or null
+  float* tail; float tail_val; // data parallel write pass: *tail = tail_val (this rank's batch size), or null
   int tick;                    // advance state->t in a tick kernel first (else the bound kernel did)
 };
 hipError_t launch_adam(hipStream_t st, const AdamArgs& a, long long max_seg_n);
@@ -405,6 +407,10 @@ struct MgLaunch {
   const float* P0; int ldP0; int d0; int h0_buf; int h0_next_k; int h0_stdnormal;   // prologue sampling
   const float* x; int ldx;                        // pixels [images][ldx]
   uint64_t seed; const uint64_t* rng_base;
+  // injected noise (parity: iwae_nll_eps) instead of Philox: eps[i] is layer i's
+  // [k][eps_N][d_i] buffer in the reference's sample-major layout (F:59, F:68);
+  // chunk row r is sample eps_s0 + r % kS of image eps_i0 + r / kS.  Null: Philox.
+  const float* eps[8]; int eps_N, eps_i0, eps_s0;
   float* lw;                                      // out: log w per row
 };
 hipError_t launch_mega_fwd(hipStream_t st, const MgLaunch& L, int rt, int waves, size_t lds_bytes);

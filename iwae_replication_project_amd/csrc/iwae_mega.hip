@@ -283,7 +283,16 @@ __device__ __forceinline__ void mg_head(const MgLaunch& L, const MgStage& S, int
     if (ACT == MG_SAMPLE) {
       const int row0 = blockIdx.x * 16 * RT;
       const int grow = row0 + min(row, L.rows - 1 - row0);      // global row (clamped into the chunk)
-      const float2 e = philox_normal2(L.seed, base, (unsigned)grow, (unsigned)S.layer, (unsigned)q, (g & 1) != 0);
+      float2 e;
+      if (L.eps[S.layer]) {
+        // injected [k][N][d] noise; columns past d read 0 (masked below anyway)
+        const size_t eo = ((size_t)(L.eps_s0 + grow % L.kS) * L.eps_N + (L.eps_i0 + grow / L.kS)) * d;
+        const float* ep = L.eps[S.layer] + eo;
+        e.x = j0 < d ? ep[j0] : 0.f;
+        e.y = j0 + 1 < d ? ep[j0 + 1] : 0.f;
+      } else {
+        e = philox_normal2(L.seed, base, (unsigned)grow, (unsigned)S.layer, (unsigned)q, (g & 1) != 0);
+      }
       float hv[2];
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
@@ -454,8 +463,15 @@ __global__ __launch_bounds__(NW * 64) void mega_fwd_kernel(MgLaunch L) {
         mu[q] = Pp[jc];
         zs[q] = Pp[d + jc];
       }
-      const float4 e4 = 4 * gq < d ? philox_normal4(L.seed, base, (unsigned)rg, 0u, (unsigned)gq)
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 e4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (L.eps[0]) {
+        const float* ep = L.eps[0] + ((size_t)(L.eps_s0 + rg % L.kS) * L.eps_N + (L.eps_i0 + rg / L.kS)) * d;
+        const int j = 4 * gq;
+        e4 = make_float4(j < d ? ep[j] : 0.f, j + 1 < d ? ep[j + 1] : 0.f, j + 2 < d ? ep[j + 2] : 0.f,
+                         j + 3 < d ? ep[j + 3] : 0.f);
+      } else if (4 * gq < d) {
+        e4 = philox_normal4(L.seed, base, (unsigned)rg, 0u, (unsigned)gq);
+      }
       mg_bf16x4 vh, vl;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {

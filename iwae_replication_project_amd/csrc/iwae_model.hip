@@ -15,6 +15,8 @@
 #include <tuple>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/iwae.h"
 #include "iwae_kernels.h"
 
@@ -108,7 +110,13 @@ struct iwae_handle {
   bool out_x3 = false;               // ... except the output layer's two GEMMs of a large-batch step (bf16x3)
   long long out_x3_rows = 8192;      // sample rows from which a train step takes that exception (0: never)
   DevState* ds = nullptr;
-  uint64_t seed = 0x5eed5eedULL;
+  uint64_t seed = 0x5eed5eedULL;       // Philox key actually used (derived from user_seed, noise_stream)
+  uint64_t user_seed = 0x5eed5eedULL;
+  uint64_t noise_stream = 0;
+  // data parallelism (iwae_dp_init)
+  int dp_rank = 0, dp_world = 1;
+  bool dp_weighted = false;            // forward_backward writes B_local * grad and B_local at grad[nparam_int]
+  ncclComm_t comm = nullptr;           // library-owned RCCL communicator (or null: the caller reduces)
   // workspace
   char* arena = nullptr;
   size_t arena_bytes = 0;
@@ -132,6 +140,7 @@ struct iwae_handle {
   int nll_fused = 1;                 // NLL: fused k-sample forward (mega_fwd_kernel) when it fits
   int mg_waves = 8;                  // mega_fwd_kernel workgroup: 8 waves (64 rows) or 4 (32 rows, 2 per CU)
   bool masked = false;               // active-unit masks in force (iwae_nll_masked only)
+  long long n_mega = 0, n_mega_eps = 0;  // mega_fwd_kernel launches (all / injected noise), iwae_debug_count
   const float* mask[IWAE_MAX_LAYERS] = {};
   // graphs
   bool use_graphs = false;
@@ -755,8 +764,10 @@ static int ensure_wsplit(iwae_handle* h) {
 
 
 static int run_adam(iwae_handle* h, bool read_slabs, bool write_grad, bool do_adam, float scale_override,
-                    bool tick) {
+                    bool tick, const float* scale_dev = nullptr, float* tail = nullptr) {
   AdamArgs a{};
+  a.scale_dev = scale_dev;
+  a.tail = tail; a.tail_val = scale_override;
   a.param = h->params; a.m = h->adam_m; a.v = h->adam_v; a.grad = h->grad; a.slabs = h->slabs;
   a.whi = nullptr; a.wlo = nullptr;          // split copies are refreshed lazily (ensure_wsplit)
   if (do_adam) h->params_version++;
@@ -1220,6 +1231,23 @@ static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const
 
 static float* train_loss_ptr(iwae_handle* h) { return h->loss_out ? h->loss_out : &h->ds->scalars[0]; }
 
+// End of a train step / forward_backward: sum the weight-gradient slabs into the
+// gradient buffer and (adam) step.  Data parallel (iwae_dp_init): the buffer gets
+// B_local * g and B_local in its tail element; with the library communicator the
+// n + 4 floats are summed over the ranks right here (ncclAllReduce on the step's
+// stream, inside the captured graph) and Adam scales by 1 / sum_r B_r.
+static int finish_step(iwae_handle* h, const Plan& P, bool adam) {
+  if (!h->dp_weighted) return run_adam(h, true, true, adam, 1.f, false);
+  float* tail = h->grad + h->nparam_int;
+  CHK(run_adam(h, true, true, false, (float)P.B, false, nullptr, tail));
+  if (!adam) return IWAE_OK;
+  if (!h->comm) return fail(h, IWAE_EINVAL, "data parallel without a library communicator");
+  if (ncclAllReduce(h->grad, h->grad, (size_t)h->nparam_int + 4, ncclFloat32, ncclSum, h->comm, h->stream) !=
+      ncclSuccess)
+    return fail(h, IWAE_EHIP, "ncclAllReduce of the gradient failed");
+  return run_adam(h, false, true, true, 0.f, false, tail);
+}
+
 static int fused_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
   CHK(fused_forward(h, P, E, true));
   CHK(run_bound(h, P, true, -1.f, train_loss_ptr(h), adam));
@@ -1234,8 +1262,7 @@ static int fused_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool
     CHK(fused_encoder_bwd(h, P, h->dlw));
     CHK(weight_grads(h, P, true, true, h->dpx));
   }
-  CHK(run_adam(h, true, true, adam, 1.f, false));
-  return IWAE_OK;
+  return finish_step(h, P, adam);
 }
 
 // forward + backward (+ Adam) after x is staged
@@ -1255,13 +1282,15 @@ static int train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam)
     CHK(decoder_bwd(h, P, h->dlw, h->dpx, true, true));
     CHK(encoder_bwd(h, P, h->dlw));
   }
-  CHK(run_adam(h, true, true, adam, 1.f, false));
-  return IWAE_OK;
+  return finish_step(h, P, adam);
 }
 
 static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,
                     const float* const* eps, int n_eps, float* loss_dev, bool adam) {
   if (!x) return fail(h, IWAE_EINVAL, "x is NULL");
+  if (adam && h->dp_weighted && !h->comm)
+    return fail(h, IWAE_EINVAL, "data parallel without a library communicator: call iwae_forward_backward, "
+                                "all-reduce the gradient buffer, then iwae_apply_adam(h, 0)");
   Plan P;
   CHK(make_plan(h, lc, B, P));
   EpsSet E;
@@ -1327,6 +1356,9 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
       g.x_cap = x;
     }
     HIPCHK(hipGraphLaunch(g.exec, h->stream));
+    // the replayed Adam moved the parameters: the split (bf16x3) copies the
+    // evaluation paths read are stale from here (run_adam's bump only ran at capture)
+    if (adam) h->params_version++;
   } else {
     CHK(train_body(h, P, E, adam));
   }
@@ -1392,14 +1424,14 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (e == hipSuccess) e = hipMalloc(&h->params, h->params_bytes);
   if (e == hipSuccess) e = hipMalloc(&h->adam_m, pb);
   if (e == hipSuccess) e = hipMalloc(&h->adam_v, pb);
-  if (e == hipSuccess) e = hipMalloc(&h->grad_own, pb);
+  if (e == hipSuccess) e = hipMalloc(&h->grad_own, pb + 4 * sizeof(float));   // + the DP batch-size tail
   if (e == hipSuccess) e = hipMalloc(&h->ds, sizeof(DevState));
   if (e == hipSuccess) e = hipMalloc(&h->wsplit_hi, (size_t)(2 * h->wsplit_elems) * sizeof(__bf16));
   if (e == hipSuccess) e = hipMemset(h->wsplit_hi, 0, (size_t)(2 * h->wsplit_elems) * sizeof(__bf16));
   if (e == hipSuccess) e = hipMemset(h->params, 0, h->params_bytes);
   if (e == hipSuccess) e = hipMemset(h->adam_m, 0, pb);
   if (e == hipSuccess) e = hipMemset(h->adam_v, 0, pb);
-  if (e == hipSuccess) e = hipMemset(h->grad_own, 0, pb);
+  if (e == hipSuccess) e = hipMemset(h->grad_own, 0, pb + 4 * sizeof(float));
   if (e == hipSuccess) {
     DevState s{};
     s.adam.lr = 1e-3f; s.adam.b1 = 0.9f; s.adam.b2 = 0.999f; s.adam.eps = 1e-7f;  // Keras defaults
@@ -1433,6 +1465,7 @@ void iwae_destroy(iwae_handle* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   free_workspace(h);
+  if (h->comm) (void)ncclCommDestroy(h->comm);
   for (auto e : h->prof_ev) (void)hipEventDestroy(e);
   if (h->params) (void)hipFree(h->params);
   if (h->adam_m) (void)hipFree(h->adam_m);
@@ -1458,9 +1491,24 @@ int iwae_synchronize(iwae_handle* h) {
   return IWAE_OK;
 }
 
+static uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+int iwae_set_noise_stream(iwae_handle* h, unsigned long long stream) {
+  if (!h) return IWAE_EINVAL;
+  h->noise_stream = stream;
+  return iwae_set_seed(h, h->user_seed);
+}
+
 int iwae_set_seed(iwae_handle* h, unsigned long long seed) {
   if (!h) return IWAE_EINVAL;
-  h->seed = seed;
+  h->user_seed = seed;
+  // Philox key of this handle's noise stream (per rank under data parallelism)
+  h->seed = h->noise_stream == 0 ? seed : splitmix64(seed ^ splitmix64(h->noise_stream));
   for (auto& kv : h->graphs) destroy_graph(kv.second);   // seed is a captured kernel argument
   h->graphs.clear();
   uint64_t z[2] = {0, 0};
@@ -1627,8 +1675,12 @@ int iwae_export_internal(iwae_handle* h, const float* internal_dev, float* host,
 
 int iwae_bind_grad_buffer(iwae_handle* h, float* g, long long n) {
   if (!h) return IWAE_EINVAL;
-  if (g && n != h->nparam_int)
-    return fail(h, IWAE_EINVAL, "grad buffer must hold " + std::to_string(h->nparam_int) + " floats");
+  const long long need = h->nparam_int + (h->dp_weighted ? 4 : 0);
+  if (g && n != h->nparam_int && n != h->nparam_int + 4)
+    return fail(h, IWAE_EINVAL, "grad buffer must hold " + std::to_string(h->nparam_int) + " (+4 under data "
+                                "parallelism) floats");
+  if (g && n < need)
+    return fail(h, IWAE_EINVAL, "data parallel: the grad buffer needs " + std::to_string(need) + " floats");
   h->grad = g ? g : h->grad_own;
   for (auto& kv : h->graphs) destroy_graph(kv.second);
   h->graphs.clear();
@@ -1637,8 +1689,67 @@ int iwae_bind_grad_buffer(iwae_handle* h, float* g, long long n) {
 
 int iwae_apply_adam(iwae_handle* h, float grad_scale) {
   if (!h) return IWAE_EINVAL;
-  if (!(grad_scale > 0.f)) return fail(h, IWAE_EINVAL, "grad_scale must be > 0");
-  return run_adam(h, false, false, true, grad_scale, true);
+  if (!(grad_scale > 0.f)) {
+    // data parallel: 1 / the all-reduced batch total in the buffer's tail
+    if (!h->dp_weighted) return fail(h, IWAE_EINVAL, "grad_scale must be > 0 (0 only after iwae_dp_init)");
+    return run_adam(h, false, true, true, 0.f, true, h->grad + h->nparam_int);
+  }
+  return run_adam(h, false, true, true, grad_scale, true);
+}
+
+int iwae_dp_unique_id(void* out128) {
+  if (!out128) return IWAE_EINVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return IWAE_EHIP;
+  static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+  std::memcpy(out128, &id, sizeof(id));
+  return IWAE_OK;
+}
+
+int iwae_dp_init(iwae_handle* h, int rank, int world, const void* uid) {
+  if (!h) return IWAE_EINVAL;
+  if (world < 1 || rank < 0 || rank >= world) return fail(h, IWAE_EINVAL, "need 0 <= rank < world");
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (h->comm) {
+    (void)ncclCommDestroy(h->comm);
+    h->comm = nullptr;
+  }
+  h->dp_rank = rank;
+  h->dp_world = world;
+  h->dp_weighted = world > 1 || uid != nullptr;
+  if (h->dp_weighted && h->grad != h->grad_own)
+    return fail(h, IWAE_EINVAL, "iwae_dp_init before binding a grad buffer (then bind n + 4 floats)");
+  if (uid) {
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof(id));
+    HIPCHK(hipSetDevice(h->device));
+    const ncclResult_t r = ncclCommInitRank(&h->comm, world, id, rank);
+    if (r != ncclSuccess) {
+      h->comm = nullptr;
+      return fail(h, IWAE_EHIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+  }
+  for (auto& kv : h->graphs) destroy_graph(kv.second);
+  h->graphs.clear();
+  return iwae_set_noise_stream(h, (unsigned long long)rank);
+}
+
+int iwae_dp_broadcast_state(iwae_handle* h) {
+  if (!h) return IWAE_EINVAL;
+  if (!h->comm) return fail(h, IWAE_EINVAL, "iwae_dp_broadcast_state needs iwae_dp_init with an RCCL id");
+  const size_t n = (size_t)h->nparam_int;
+  ncclResult_t r = ncclGroupStart();
+  if (r == ncclSuccess) r = ncclBroadcast(h->params, h->params, n, ncclFloat32, 0, h->comm, h->stream);
+  if (r == ncclSuccess) r = ncclBroadcast(h->adam_m, h->adam_m, n, ncclFloat32, 0, h->comm, h->stream);
+  if (r == ncclSuccess) r = ncclBroadcast(h->adam_v, h->adam_v, n, ncclFloat32, 0, h->comm, h->stream);
+  // the Adam step counter (an int64 at DevState::adam.t)
+  if (r == ncclSuccess) r = ncclBroadcast(&h->ds->adam.t, &h->ds->adam.t, 1, ncclInt64, 0, h->comm, h->stream);
+  const ncclResult_t r2 = ncclGroupEnd();
+  if (r != ncclSuccess || r2 != ncclSuccess)
+    return fail(h, IWAE_EHIP, std::string("ncclBroadcast: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->params_version++;
+  return IWAE_OK;
 }
 
 static int eval_forward(iwae_handle* h, const Plan& P, const float* x, const float* const* eps, int n_eps,
@@ -1781,8 +1892,17 @@ static bool mega_plan(iwae_handle* h, MgLaunch& M, int& rt, int& waves, size_t& 
 }
 
 // chunked k-sample NLL over N images; accumulates per-image (m, s)
+// eps (optional, parity): L buffers [k][N][d_i]; only the fused kernel takes
+// them chunk by chunk (the caller checks nll_mega_ok first)
+static bool nll_mega_ok(iwae_handle* h) {
+  MgLaunch MG;
+  int rt = 0, w = 8;
+  size_t lds = 0;
+  return h->x3 && h->nll_fused && !h->masked && mega_plan(h, MG, rt, w, lds);
+}
+
 static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, float* out_m, float* out_s,
-                    float* out_logpx) {
+                    float* out_logpx, const float* const* eps = nullptr) {
   if (!h) return IWAE_EINVAL;
   if (!x) return fail(h, IWAE_EINVAL, "x is NULL");
   if (N <= 0 || k <= 0) return fail(h, IWAE_EINVAL, "N and k must be positive");
@@ -1799,6 +1919,9 @@ static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, flo
   int mg_rt = 0, mg_waves = 8;
   size_t mg_lds = 0;
   const bool mega = h->x3 && h->nll_fused && !h->masked && mega_plan(h, MG, mg_rt, mg_waves, mg_lds);
+  if (eps && !mega) return fail(h, IWAE_EINVAL, "injected-noise NLL chunks need the fused kernel");
+  for (int i = 0; i < 8; ++i) MG.eps[i] = (eps && i < h->L) ? eps[i] : nullptr;
+  MG.eps_N = N;
   const size_t wbytes = (size_t)h->xdim * sizeof(float);
   for (int i0 = 0; i0 < N; i0 += imgs) {
     const int n = std::min(imgs, N - i0);
@@ -1814,11 +1937,14 @@ static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, flo
         // first encoder layer on the chunk's images, then everything else fused
         CHK(stoch_fwd(h, h->enc[0], h->x_in, n, h->eb[0]));
         MG.rows = n * P.kS; MG.kS = P.kS;
+        MG.eps_i0 = i0; MG.eps_s0 = s0;
         MG.P0 = h->eb[0].P.p; MG.ldP0 = h->eb[0].P.ld;
         MG.x = h->x_in.p; MG.ldx = h->x_in.ld;
         MG.seed = h->seed; MG.rng_base = &h->ds->rng[0];
         MG.lw = h->lw;
         HIPCHK(launch_mega_fwd(h->stream, MG, mg_rt, mg_waves, mg_lds));
+        ++h->n_mega;
+        if (eps) ++h->n_mega_eps;
         a.lw = h->lw;
       } else {
         CHK(forward_core(h, P, E, false));
@@ -1852,6 +1978,12 @@ int iwae_nll_eps(iwae_handle* h, const float* x, int N, int k, const float* cons
                  float* out_logpx) {
   if (!h) return IWAE_EINVAL;
   if (!out_logpx) return fail(h, IWAE_EINVAL, "out_logpx is NULL");
+  if (eps && n_eps == h->L && nll_mega_ok(h)) {
+    // the kernel the NLL benchmark times (mega_fwd_kernel), fed the caller's noise
+    for (int i = 0; i < h->L; ++i)
+      if (!eps[i]) return fail(h, IWAE_EINVAL, "NULL eps buffer");
+    return nll_core(h, x, N, k, 0, nullptr, nullptr, out_logpx, eps);
+  }
   iwae_loss_config lc{IWAE_LOSS_IWAE, k, 1.f, 1.f, 0.5f, 0, 0};
   Plan P;
   CHK(make_plan(h, &lc, N, P));
@@ -1990,6 +2122,15 @@ int iwae_debug_gemm(iwae_handle* h, const float* A, int lda, const float* B, int
 }
 
 double iwae_workspace_bytes(const iwae_handle* h) { return h ? (double)h->arena_bytes : 0.0; }
+
+long long iwae_debug_count(const iwae_handle* h, int what) {
+  if (!h) return -1;
+  switch (what) {
+    case 0: return h->n_mega;
+    case 1: return h->n_mega_eps;
+    default: return -1;
+  }
+}
 
 int iwae_profile_gemm(iwae_handle* h, int kind, int epi) {
   if (!h) return IWAE_EINVAL;

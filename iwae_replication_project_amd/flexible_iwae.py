@@ -221,6 +221,11 @@ class Flexible_Model:
         draws from here on).  The reference has no seed."""
         self._call(self._lib.iwae_set_seed(self._h, int(seed) & ((1 << 64) - 1)))
 
+    def set_noise_stream(self, stream):
+        """Select the noise stream (one per rank: Philox key derived from (seed,
+        stream); stream 0 is the seed's own) and restart its counter."""
+        self._call(self._lib.iwae_set_noise_stream(self._h, int(stream) & ((1 << 64) - 1)))
+
     def _call(self, rc):
         _lib.check(self._lib, self._h, rc)
 
@@ -470,6 +475,20 @@ class Flexible_Model:
         self._stream.synchronize()
         return out
 
+    def log_px_partials(self, x, k_local, chunk=0):
+        """Per-image log-sum-exp partials over k_local device-noise samples of
+        this handle's noise stream: (m, s) with m = max_s lw, s = sum_s exp(lw - m)
+        (the sample-sharded NLL's per-rank contribution)."""
+        xd = self._x(x)
+        N = xd.shape[0]
+        with torch.cuda.stream(self._stream):
+            m = torch.empty(N, device=self.device)
+            s = torch.empty(N, device=self.device)
+        self._call(self._lib.iwae_nll_partials(self._h, _lib.fptr(xd), N, int(k_local), int(chunk), _lib.fptr(m),
+                                               _lib.fptr(s)))
+        self._stream.synchronize()
+        return m, s
+
     def get_NLL(self, x, k=5000, eps=None):
         """F:463-F:464: -L_k with k = 5000 by default."""
         return float(-self.log_px(x, k, eps).mean().item())
@@ -589,7 +608,10 @@ class Flexible_Model:
         units (1000 draws over all of x), their counts, PCA counts, variances."""
         xd = self._x(x)
         N = xd.shape[0]
-        nb = max(1, N // batch_size)
+        if batch_size <= 0 or N == 0 or N % batch_size != 0:
+            # F:500 tf.reshape(x, (-1, batch_size, 28, 28, 1)) raises on a ragged tail
+            raise ValueError(f"get_training_statistics: {N} images do not split into batches of {batch_size}")
+        nb = N // batch_size
         res = dict(VAE=0.0, IWAE=0.0, NLL=0.0)
         res["E_q(h|x)[log(p(x|h))]"] = 0.0
         res["D_kl(q(h|x),p(h))"] = 0.0
@@ -631,7 +653,9 @@ class Flexible_Model:
         B = xd.shape[0]
         lc = self._lc(loss_function, k, p, alpha, beta, k1, k2)
         if seed is not None:
-            self._call(self._lib.iwae_set_seed(self._h, (int(seed) + rank) & ((1 << 64) - 1)))
+            self._call(self._lib.iwae_set_seed(self._h, int(seed) & ((1 << 64) - 1)))
+        if w > 1:
+            self.set_noise_stream(rank)       # per-rank independent draws (also with the default seed)
         import ctypes
         g = _lib.FP()
         n = ctypes.c_longlong(0)

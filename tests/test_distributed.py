@@ -129,3 +129,32 @@ def test_data_parallel_gradient_average_equals_full_batch():
     for r in (0, 1):
         assert not isinstance(out[r], str), out[r]
         np.testing.assert_allclose(out[r], ref, rtol=1e-10, atol=1e-13)
+
+
+def dp_grads_unequal(rank, world):
+    """Unequal shards (4 + 3 images): the weighted merge sum_r B_r g_r / sum_r B_r
+    (what the library's data-parallel step computes from one all-reduce of the
+    gradient buffer plus its batch-size tail) equals the full-batch gradient."""
+    from iwae_replication_project_amd import distributed as D
+    O, spec, params, x, eps = _model()
+    lo, hi = D.shard_range(7, rank, world)
+    _, g = O.objective_and_grads(params, spec, x[lo:hi], [e[:, lo:hi] for e in eps], "IWAE", eps[0].shape[0])
+    t = torch.tensor(np.concatenate([O.flatten_params(spec, g), [0.0]]))
+    return D.weighted_grad_merge_(t, hi - lo).numpy().tolist()
+
+
+def test_data_parallel_weighted_merge_unequal_shards_equals_full_batch():
+    out = spawn(dp_grads_unequal)
+    O, spec, params, x, eps = _model()
+    _, g = O.objective_and_grads(params, spec, x, eps, "IWAE", eps[0].shape[0])
+    ref = O.flatten_params(spec, g)
+    for r in (0, 1):
+        assert not isinstance(out[r], str), out[r]
+        np.testing.assert_allclose(out[r], ref, rtol=1e-10, atol=1e-13)
+    # the unweighted 1/world average is wrong for unequal shards
+    lo = []
+    for r in (0, 1):
+        a, b = (0, 4) if r == 0 else (4, 7)
+        _, gr = O.objective_and_grads(params, spec, x[a:b], [e[:, a:b] for e in eps], "IWAE", eps[0].shape[0])
+        lo.append(O.flatten_params(spec, gr))
+    assert np.abs((lo[0] + lo[1]) / 2 - ref).max() > 1e-6

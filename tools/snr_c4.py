@@ -1,5 +1,6 @@
 """Config C4: gradient SNR over R noise draws for the 2L model at
-k = 64 (IWAE, and PIWAE / MIWAE with M = K = 8), batch 20; prints draws/s and
+k = 64 (IWAE, PIWAE / MIWAE with M = K = 8, CIWAE with beta = 0.5: two
+independent draws per estimate, F:382-F:383), batch 20; prints draws/s and
 the median SNR of the encoder and decoder parameters.  Under torchrun the R
 draws are split over the ranks (one all-reduce of the moments)."""
 import os
@@ -16,7 +17,7 @@ from iwae_replication_project_amd import Flexible_Model  # noqa: E402
 
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
 x, pi = bench.synthetic_images(20, 1)
-for loss, kw in (("IWAE", {}), ("PIWAE", dict(k1=8, k2=8)), ("MIWAE", dict(k1=8, k2=8))):
+for loss, kw in (("IWAE", {}), ("PIWAE", dict(k1=8, k2=8)), ("MIWAE", dict(k1=8, k2=8)), ("CIWAE", dict(beta=0.5))):
     m = Flexible_Model(bench.HE, bench.HD, bench.LE, bench.LD, dataset_bias=pi, loss_function=loss, k=64, seed=2,
                        **kw)
     m.get_gradient_snr(x, R=4, seed=1)                 # warm-up (workspace, graph capture)
