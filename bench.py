@@ -58,6 +58,19 @@ def synthetic_images(n, seed):
     return (rng.random((n, 784)) < pi).astype(np.float32), pi
 
 
+def host_cores():
+    """(threads used, cores this process may run on, nproc): the threads are the
+    cores of the process's CPU affinity set (the box's share), capped by
+    OMP_NUM_THREADS when the environment sets it."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except Exception:          # pragma: no cover
+        avail = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    used = min(avail, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else avail
+    return used, avail, os.cpu_count() or 1
+
+
 def cpu_baseline(seconds=12.0):
     """The oracle (numpy restatement of the reference's op sequence, incl. the
     duplicate decoder pass at F:340) timed on host cores: IWAE train steps at
@@ -67,7 +80,7 @@ def cpu_baseline(seconds=12.0):
         from threadpoolctl import threadpool_limits
     except Exception:          # pragma: no cover
         threadpool_limits = None
-    cores = min(16, os.cpu_count() or 1)
+    cores, avail, nproc = host_cores()
     ctx = threadpool_limits(limits=cores) if threadpool_limits else None
     try:
         spec = O.ModelSpec(HE, HD, LE, LD)
@@ -90,9 +103,50 @@ def cpu_baseline(seconds=12.0):
     finally:
         if ctx is not None:
             ctx.__exit__(None, None, None)
-    return dict(value=steps * B_PER_GPU * K / el, unit="image*samples/s", cores=cores, kind="port",
+    return dict(value=steps * B_PER_GPU * K / el, unit="image*samples/s", cores=cores, cores_available=avail,
+                nproc=nproc, kind="port",
                 sample=f"{steps} IWAE train steps (2L, k={K}, batch {B_PER_GPU}, float32 numpy, incl. the "
                        f"F:340 duplicate decoder pass) in {el:.1f} s")
+
+
+def cpu_baseline_nll(seconds=8.0, k=5000):
+    """the k=5000 NLL (get_NLL F:463 -> get_log_weights F:327-F:351,
+    incl. the F:340 duplicate decoder pass) on the oracle, float32, on the host
+    cores, over as many synthetic test images as fit in `seconds`; images/s
+    extrapolates linearly to the 10k-image set (the path is per-image)."""
+    from oracle import iwae_oracle as O
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:          # pragma: no cover
+        threadpool_limits = None
+    cores, avail, nproc = host_cores()
+    ctx = threadpool_limits(limits=cores) if threadpool_limits else None
+    try:
+        spec = O.ModelSpec(HE, HD, LE, LD)
+        xt, pi = synthetic_images(64, 99)
+        rng = np.random.default_rng(2)
+        params = O.cast_params(O.glorot_init(spec, rng, out_bias=O.output_bias_from_mean(pi)), np.float32)
+        chunk = 1000
+        n, t0 = 0, time.perf_counter()
+        while n < xt.shape[0]:
+            x = xt[n:n + 1].astype(np.float32)
+            m_run, s_run = -np.inf, 0.0
+            for s0 in range(0, k, chunk):
+                e = O.draw_eps(spec, chunk, 1, rng, np.float32)
+                lw = O.forward(params, spec, x, e, dup_decoder=True)["lw"].astype(np.float64)[:, 0]
+                M = max(m_run, lw.max())
+                s_run = s_run * math.exp(m_run - M) + np.exp(lw - M).sum()
+                m_run = M
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    finally:
+        if ctx is not None:
+            ctx.__exit__(None, None, None)
+    return dict(value=n / el, unit="images/s", cores=cores, cores_available=avail, nproc=nproc, kind="port",
+                sample=f"{n} test images at k={k} (2L, float32 numpy, incl. the F:340 duplicate decoder pass) in "
+                       f"{el:.1f} s; extrapolates linearly to 10k images")
 
 
 def main():
@@ -108,6 +162,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-c0", action="store_true")
+    ap.add_argument("--c0-steps", type=int, default=200)
     args = ap.parse_args()
 
     import torch
@@ -258,9 +314,40 @@ def main():
                    tflops=round(NLL_FLOP_PER_IMAGE * (args.nll_k / 5000) * args.nll_images / el2 / 1e12, 3),
                    precision="bf16x3")
 
-    cpu = None
+    # ---- configs[0]: 1 stochastic layer 784-200-200-50, IWAE k=5, batch 20 per GPU
+    c0 = None
+    if not args.no_c0:
+        m0 = Flexible_Model([200], [200], [50], [784], dataset_bias=pi, loss_function="IWAE", k=5, seed=2,
+                            use_graphs=not args.no_graphs)
+        m0.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+        if world > 1:
+            distributed.enable_data_parallel(m0)
+        for i in range(10):
+            m0.train_step(batches[i % nb], sync=False)
+        m0._stream.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        for i in range(args.c0_steps):
+            m0.train_step(batches[i % nb], sync=False)
+        m0._stream.synchronize()
+        torch.cuda.synchronize()
+        barrier()
+        el4 = time.perf_counter() - t3
+        if world > 1:
+            t = torch.tensor([el4], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el4 = float(t.item())
+        c0rows = world * B_PER_GPU * 5 * args.c0_steps
+        c0 = dict(value=round(c0rows / el4, 1), unit="image*samples/s", workload="BASELINE configs[0]: IWAE k=5, "
+                  "1 stochastic layer 784-200-200-50, batch 20 per GPU", steps=args.c0_steps,
+                  ms_per_step=round(1e3 * el4 / args.c0_steps, 5),
+                  tflops=round(1_438_240 * c0rows / el4 / 1e12, 3))
+
+    cpu = cpu_nll = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_seconds)
+        cpu_nll = cpu_baseline_nll(max(4.0, args.cpu_seconds / 2))
 
     if rank == 0:
         out = {
@@ -274,9 +361,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
-            "precision": "train step: exact-f32 MFMA for weight products, bf16x3 (hi/lo split, f32 accumulate) "
-                         "for weight-gradient GEMMs; NLL: bf16x3 GEMMs",
+            "dtype": "fp32 (bf16x3 split products)",
+            "precision": "fp32 values, fp32 accumulate; matrix products either exact f32 MFMA or bf16x3 split "
+                         "products (a_hi b_hi + a_hi b_lo + a_lo b_hi, ~2^-16 relative per product): train step "
+                         "weight-operand products f32 except as DESIGN.md section 4 lists, weight gradients bf16x3, "
+                         "NLL bf16x3",
             "data": "synthetic",
             "config": {"workload": "IWAE train step (fwd+bound+bwd+Adam), k=50, 2 stochastic layers "
                                    "784-200-200-100-100-50, batch 20 per GPU (BASELINE configs[1])",
@@ -285,8 +374,10 @@ def main():
             "loss": round(loss, 4),
             "nll": nll,
             "large_batch": large,
+            "configs0_train": c0,
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "cpu_baseline_nll": cpu_nll,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
