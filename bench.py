@@ -36,10 +36,9 @@ LARGE_B_PER_GPU = 512              # configs[4]: global batch 4096 over 8 GPUs
 TRAIN_FLOP_PER_ROW = 1_712_944
 NLL_FLOP_PER_IMAGE = 2.818e9
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec peak
+BF16_PEAK_TFLOPS = 2500.0          # MI355X_MICROARCH.md: BF16 MFMA dense peak
+BF16X3_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 3, 1)   # f32-accurate bf16x3 products: 3 bf16 MFMAs each
 HBM_PEAK_GBS = 8000.0
-# algorithmic HBM bytes of one train-step Bernoulli GEMM launch (1000 rows):
-# read y2 [1000 x 201] + W3_aug [201 x 784] + x [20 x 784]; write g [1000 x 784] + partials [1000 x 25]
-ALGO_MB_BERN = (1000 * 201 + 201 * 784 + 20 * 784 + 1000 * 784 + 1000 * 25) * 4 / 1e6
 
 
 def pixel_profile():
@@ -222,36 +221,53 @@ def main():
     value = rows / el
     ms_per_step = 1e3 * el / args.steps
 
-    # ---- dominant kernel live timing: the decoder output GEMM (200 -> 784,
-    # fused Bernoulli epilogue) of this workload, recorded from one eager step,
+    # ---- dominant kernel live timing.  Candidates: the train engine's forward and
+    # backward launches (iwae_train.hip) and, where the step still uses it, the
+    # output-layer Bernoulli GEMM.  Each is recorded from one eager step and
     # re-launched K times back to back between two HIP events on the library's
-    # stream (the stream it runs on); avg = elapsed / K
-    model._call(model._lib.iwae_profile_gemm(model._h, 0, 2))
-    run(1, args.warmup + args.steps)
+    # stream (the stream it runs on); avg = elapsed / K.  The dominant one (the
+    # longest) is priced against its matrix-core peak.
     import ctypes
-    ms, fl = ctypes.c_double(), ctypes.c_double()
-    model._call(model._lib.iwae_profile_replay(model._h, args.steps, ctypes.byref(ms), ctypes.byref(fl)))
-    model._call(model._lib.iwae_profile_gemm(model._h, -1, -1))
-    nl = ctypes.c_longlong(args.steps)
-    avg_ms = ms.value / max(1, nl.value)
-    flop_per_launch = fl.value / max(1, nl.value)
-    achieved = flop_per_launch / (avg_ms * 1e-3) / 1e12
+
+    def live(kind, epi):
+        model._call(model._lib.iwae_profile_gemm(model._h, kind, epi))
+        run(1, args.warmup + args.steps)
+        ms, fl = ctypes.c_double(), ctypes.c_double()
+        rc = model._lib.iwae_profile_replay(model._h, args.steps, ctypes.byref(ms), ctypes.byref(fl))
+        model._call(model._lib.iwae_profile_gemm(model._h, -1, -1))
+        if rc != 0:
+            return None
+        return ms.value / args.steps, fl.value / args.steps
+
+    cands = {"tc_kernel forward (train engine, bf16x3)": (live(10, 0), BF16X3_PEAK_TFLOPS),
+             "tc_kernel backward (train engine, bf16x3)": (live(11, 0), BF16X3_PEAK_TFLOPS),
+             "gemm_kernel<FWD, EPI_BERN> (output layer, f32 MFMA)": (live(0, 2), FP32_MFMA_PEAK_TFLOPS)}
+    kern = {k: dict(avg_us=round(v[0] * 1e3, 3), flop_per_launch=v[1],
+                    tflops=round(v[1] / (v[0] * 1e-3) / 1e12, 3), peak=pk)
+            for k, (v, pk) in cands.items() if v is not None}
+    dom = max(kern, key=lambda k: kern[k]["avg_us"])
+    kd = kern[dom]
+    achieved = kd["tflops"]
+    peak = kd["peak"]
     # HBM traffic of the same kernel: committed rocprofv3 PMC record (tools/pmc_passes.sh +
     # tools/pmc_to_json.py; FETCH_SIZE x2 per the gfx950 correction, WRITE_SIZE as is)
     traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    pmc = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             rec = json.load(f)
-        traffic = round(rec["traffic_bytes"] / 1e6, 3)
-        traffic_src = f"profiles/r01_pmc_traffic.json (MB per launch: fetch {rec['fetch_bytes'] / 1e6:.2f} + " \
-                      f"write {rec['write_bytes'] / 1e6:.2f}; algorithmic {ALGO_MB_BERN:.2f})"
-    roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
-                    frac=round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), traffic=traffic, traffic_unit="MB/launch",
-                    traffic_source=traffic_src,
-                    kernel="gemm_kernel<FWD, EPI_BERN> f32 MFMA (decoder 200->784 + Bernoulli log-prob + dlogit)",
-                    avg_us=round(avg_ms * 1e3, 3), flop_per_launch=flop_per_launch, launches=int(nl.value),
-                    step_tflops=round(TRAIN_FLOP_PER_ROW * rows / el / 1e12, 3))
+        if rec.get("kernel_label") == dom:
+            traffic = round(rec["traffic_bytes"] / 1e6, 3)
+            traffic_src = f"profiles/r02_pmc_traffic.json (MB per launch: fetch {rec['fetch_bytes'] / 1e6:.2f} + " \
+                          f"write {rec['write_bytes'] / 1e6:.2f})"
+    roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=peak, unit="TFLOP/s",
+                    frac=round(achieved / peak, 4), traffic=traffic, traffic_unit="MB/launch",
+                    traffic_source=traffic_src, kernel=dom, avg_us=kd["avg_us"],
+                    flop_per_launch=kd["flop_per_launch"], launches=args.steps,
+                    peak_basis=("bf16 dense 2.5 PFLOP/s / 3 bf16 MFMAs per bf16x3 product" if peak == BF16X3_PEAK_TFLOPS
+                                else "f32 MFMA 157.3 TFLOP/s"),
+                    frac_of_bf16_dense_peak=round(achieved / BF16_PEAK_TFLOPS, 4),
+                    kernels=kern, step_tflops=round(TRAIN_FLOP_PER_ROW * rows / el / 1e12, 3))
 
     # ---- configs[4] per-GPU share: B=512 images per GPU, k=50, same model and
     # step (RCCL gradient all-reduce for N > 1)

@@ -106,8 +106,11 @@ int iwae_set_graphs(iwae_handle* h, int enable);
  * f32 accumulate on v_mfma_f32_32x32x16_bf16 (~2^-16 relative per product,
  * 5.3x the f32-MFMA rate); 0 exact f32 on v_mfma_f32_32x32x2_f32. */
 int iwae_set_precision(iwae_handle* h, int mode);
-/* Kernel path: 0 auto (fused row-block kernels up to 65536 sample rows, then
- * layer-wise GEMMs), 1 layer-wise only, 2 fused whenever the widths allow. */
+/* Kernel path: 0 auto (train step on the bf16x3 row-chain engine where it
+ * applies -- every loss but L_alpha / VAE_V1 / PIWAE, up to 3 stochastic
+ * layers -- else the f32 fused row-block kernels up to 65536 sample rows, else
+ * layer-wise GEMMs), 1 layer-wise only, 2 fused row-block kernels whenever the
+ * widths allow, 3 the engine (as auto). */
 int iwae_set_path(iwae_handle* h, int path);
 
 /* --- parameters (synchronous host copies) --------------------------------- */
@@ -231,9 +234,11 @@ double iwae_workspace_bytes(const iwae_handle* h);
 /* Launch counters (tests): what = 0 fused k-sample NLL kernel (mega_fwd_kernel)
  * launches, 1 those of them fed injected noise; -1 for an unknown id. */
 long long iwae_debug_count(const iwae_handle* h, int what);
-/* Live kernel timing: bracket every launch of one GEMM class (kind: 0 forward,
- * 1 backward-data, 2 backward-weight; epi: 0 store, 1 tanh, 2 Bernoulli,
- * 3 tanh-grad; kind = -1 disables) with HIP events on the handle's stream.
+/* Live kernel timing: bracket every launch of one kernel class with HIP events
+ * on the handle's stream -- a GEMM class (kind: 0 forward, 1 backward-data,
+ * 2 backward-weight; epi: 0 store, 1 tanh, 2 Bernoulli, 3 tanh-grad) or the
+ * train engine's forward (kind 10) / backward (kind 11) launch (epi ignored);
+ * kind = -1 disables.
  * Disables hipGraph replay while active.  iwae_profile_read synchronizes and
  * returns the summed kernel milliseconds, the algorithmic FLOPs of those
  * launches (2*rows*fan_in*fan_out each) and the launch count. */

@@ -717,6 +717,64 @@ hipError_t launch_wsplit(hipStream_t st, const WSplitArgs& a, long long max_seg_
   return hipGetLastError();
 }
 
+// ------------------------------------------- fragment-major split copies
+// One thread = one lane's 8 consecutive k of one fragment (see FxSeg):
+// 8 f32 parameters in, 16 bytes per plane out (consecutive threads write
+// consecutive 16-byte chunks).
+__global__ __launch_bounds__(256) void fx_refresh_kernel(FxArgs a) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.total) return;
+  int s = 0;
+  while (s + 1 < a.nseg && c >= a.seg[s + 1].start) ++s;
+  const FxSeg& g = a.seg[s];
+  long long q = c - g.start;
+  const long long nfx = (long long)g.fx_tiles * g.fx_steps * 64;
+  const bool fwd = q < nfx;
+  if (!fwd) q -= nfx;
+  const int steps = fwd ? g.fx_steps : g.gx_steps;
+  const int lane = (int)(q & 63);
+  const int u = (int)((q >> 6) % steps);
+  const int t = (int)((q >> 6) / steps);
+  const int n = 16 * t + (lane & 15);
+  const int k0 = 32 * u + 8 * (lane >> 4);
+  float v[8];
+  if (fwd) {
+    // output feature of row n (head rows permuted), k over the fin + 1 rows of W_aug
+    int j = n < g.fout ? n : -1;
+    if (g.head_d > 0) {
+      const int qq = n >> 3, w = n & 7, jj = 4 * qq + (w & 3);
+      j = jj >= g.head_d ? -1 : (w < 4 ? jj : g.head_d + jj);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = k0 + i;
+      v[i] = (j >= 0 && k <= g.fin) ? a.param[g.off + (long long)k * g.ldw + j] : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = k0 + i;
+      v[i] = (n < g.fin && k < g.fout) ? a.param[g.off + (long long)n * g.ldw + k] : 0.f;
+    }
+  }
+  typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+  bf16x8_t h, l;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    h[i] = (__bf16)v[i];
+    l[i] = (__bf16)(v[i] - (float)h[i]);
+  }
+  const long long o = (fwd ? g.fx_off : g.gx_off) + q * 8;
+  *reinterpret_cast<bf16x8_t*>(a.hi + o) = h;
+  *reinterpret_cast<bf16x8_t*>(a.lo + o) = l;
+}
+
+hipError_t launch_fx_refresh(hipStream_t st, const FxArgs& a) {
+  if (a.total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fx_refresh_kernel, dim3((unsigned)((a.total + 255) / 256)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- utility
 __global__ void fill_col_kernel(float* buf, int rows, int ld, int col, float v) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;

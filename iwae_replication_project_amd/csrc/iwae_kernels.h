@@ -306,6 +306,30 @@ struct WSplitArgs {
 };
 hipError_t launch_wsplit(hipStream_t st, const WSplitArgs& a, long long max_seg_elems);
 
+// Fragment-major split copies (bf16 hi / lo planes) for the kernels that take
+// the weights as the MFMA A operand of v_mfma_f32_16x16x32_bf16 (the row-chain
+// train engine; iwae_train.hip): per Dense layer and direction, the 16-row x
+// 32-k fragment of tile t, k step u is stored as 64 lanes x 8 bf16 contiguous
+// (lane l holds row 16t + (l & 15), k = 32u + 8(l >> 4) .. +7), so one
+// buffer_load_dwordx4 per plane reads 1 KiB of consecutive memory (the plain
+// row-major copies touch 16 half-used lines per load).
+//   FX (forward):  rows = output features (a head's rows permuted into groups
+//                  of 8, [mu 4q..4q+3 | zs 4q..4q+3], when head_d > 0),
+//                  k = fin + 1 (the bias row last);
+//   GX (backward): rows = input features, k = fout.
+struct FxSeg {
+  long long off; int fin, fout, ldw;           // W_aug [fin+1][ldw] in the parameters
+  long long fx_off; int fx_tiles, fx_steps, head_d;
+  long long gx_off; int gx_tiles, gx_steps;
+  long long start;                             // first 8-value chunk of this segment in the launch
+};
+struct FxArgs {
+  const float* param; __bf16* hi; __bf16* lo;
+  FxSeg seg[kMaxSegs]; int nseg;
+  long long total;                             // chunks
+};
+hipError_t launch_fx_refresh(hipStream_t st, const FxArgs& a);
+
 // ------------------------------------------------- fused row-block kernels ----
 struct RbNoise {             // where a sampling layer's eps comes from (see eps_at)
   const float* eps_a; const float* eps_b;
@@ -415,6 +439,66 @@ struct MgLaunch {
 };
 hipError_t launch_mega_fwd(hipStream_t st, const MgLaunch& L, int rt, int waves, size_t lds_bytes);
 hipError_t mega_setup_attributes();
+
+// ---------------------------------------- row-chain train engine (bf16x3) ----
+// The small- and large-batch train step's per-sample-row work (everything
+// after the first encoder layer, forward and backward) as chains of ops run by
+// one workgroup on 16*RT sample rows whose activations stay in LDS as split
+// bf16 planes (iwae_train.hip).  Dense ops take the layer's split copy F
+// (forward, k = fin + 1) or G (backward, k = fout) as the MFMA A operand
+// streamed from L2, the LDS activations as B, bf16x3 products on
+// v_mfma_f32_16x16x32_bf16; epilogues write the f32 tensors the weight
+// gradients and later ops read.  A launch runs up to kTcMaxJobs independent
+// chains (workgroups [block_start[j], block_start[j+1]) run job j).
+enum TcKind {
+  TC_TANH = 0,       // out = tanh(acc)                                   Dense(tanh) F:26-F:27, F:92-F:93
+  TC_SAMPLE = 1,     // encoder head: h = eps*scale + mu, log q (+ log N(h;0,1))   F:37, F:68-F:73
+  TC_PRIOR = 2,      // decoder head: log N(h_t; mu, scale), h_t read (f32)       F:138-F:141
+  TC_BERN = 3,       // output Dense(784): Bernoulli log-prob row sum + dLoss/dlogit factor g   F:123-F:128
+  TC_TGRAD = 4,      // backward dX = dZ W^T (1 - y^2)  (tanh of the forward layer below)
+  TC_LIN = 5,        // backward dX = dZ W^T (no activation): dL/dh contribution
+  TC_SAMPLE0 = 6,    // sample h1 from the image's first-layer (mu | zs)         F:58-F:60
+  TC_GBWD_PRIOR = 7, // dP of a decoder head (+ dL/dh of its target)
+  TC_GBWD_ENC = 8,   // dP of an encoder sampling head from the dL/dh sources
+  TC_LOADG = 9       // B operand = dpx[row] * g[row][:] (output layer backward)
+};
+constexpr int kTcMaxOps = 20, kTcMaxBufs = 12, kTcMaxJobs = 2;
+struct TcOp {
+  int kind;
+  const __bf16* Whi; const __bf16* Wlo; unsigned W_bytes; int ldk, K, N;   // dense ops: split rows [.][ldk]
+  int in_buf, out_buf;        // LDS buffers (-1: none)
+  int next_k;                 // columns of out_buf its reader consumes (zero padded)
+  int ones;                   // forward: ones column (bias row of W_aug) at the output width
+  int d, layer, stdnormal;    // heads / Gaussian ops: latent width, Philox layer, add log N(h; 0, 1)
+  int acc;                    // SAMPLE0 / heads: this job accumulates the row's log q / log p terms
+  float* out; int ld_out;     // f32 copy of the output: y, dZ, dX, P (mu | zs), dP, g
+  float* h; int ld_h;         // SAMPLE / SAMPLE0: h (write); PRIOR / GBWD_*: h (read)
+  float* eps; int ld_eps;     // SAMPLE / SAMPLE0: eps (write); GBWD_ENC: eps (read)
+  const float* y; int ld_y;   // TGRAD: forward tanh output; LOADG: g
+  const float* P; int ld_P; int P_div;   // SAMPLE0: image P0 (row / P_div); GBWD_*: head P
+  const float* src[4]; int ld_src[4]; int nsrc;   // GBWD_ENC: dL/dh sources summed
+  float* dh; int ld_dh;       // GBWD_PRIOR: dL/dh of the target h
+};
+struct TcJob {
+  TcOp op[kTcMaxOps]; int nop;
+  int buf_off[kTcMaxBufs], buf_ld[kTcMaxBufs];   // bf16 offset of the hi plane / row stride
+  float* logq; float* logp; float* bern; int ld_bern;   // per-row sums this job writes (null: none)
+};
+struct TcPlan {              // device resident (built once per shape)
+  TcJob job[kTcMaxJobs]; int njobs;
+  int acc_off;               // float offset of the per-row accumulators + reduction scratch
+};
+struct TcArgs {
+  const TcPlan* plan;
+  int block_start[kTcMaxJobs + 1];
+  int rows, kS;
+  const float* x; int ldx;                  // pixels by image
+  uint64_t seed; const uint64_t* rng_base;
+  const float* eps_a[8]; const float* eps_b[8]; int Bsplit, Bimg;   // injected noise ([k][B][d]) or null
+  const float* dlw; const float* dpx; float wa;
+};
+hipError_t launch_tc(hipStream_t st, const TcArgs& a, int rt, size_t lds_bytes);
+hipError_t tc_setup_attributes();
 
 hipError_t launch_fill_col(hipStream_t st, float* buf, int rows, int ld, int col, float v);
 // Evaluation statistics (F:249-F:302).  out[b][j] (+)= scale * sum_s H[b*n+s][j]

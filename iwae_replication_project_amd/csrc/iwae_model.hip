@@ -38,6 +38,10 @@ struct DenseL {
   int max_splits = 1, splits = 1;
   long long slab_off = 0;
   int rows_kind = 1;           // 0: image rows (encoder layer 0), 1: sample rows
+  int head_d = 0;              // a stochastic layer's (mu | zs) head: its latent width
+  // fragment-major split copies FX / GX (FxSeg)
+  long long fx_off = 0, gx_off = 0;
+  int fx_tiles = 0, fx_steps = 0, gx_tiles = 0, gx_steps = 0;
 };
 
 struct StochL {
@@ -106,6 +110,10 @@ struct iwae_handle {
   __bf16* wsplit_lo = nullptr;
   long long wsplit_elems = 0;
   long long params_version = 1, wsplit_version = 0;   // split copies current iff equal
+  __bf16* fx_hi = nullptr;           // fragment-major split copies (FxSeg); lo = hi + fx_elems
+  __bf16* fx_lo = nullptr;
+  long long fx_elems = 0;
+  long long fx_version = 0;
   bool in_train_step = false;        // weight-operand GEMMs of a train step stay exact f32
   bool out_x3 = false;               // ... except the output layer's two GEMMs of a large-batch step (bf16x3)
   long long out_x3_rows = 8192;      // sample rows from which a train step takes that exception (0: never)
@@ -129,6 +137,7 @@ struct iwae_handle {
   float *logq = nullptr, *logp = nullptr, *lw = nullptr, *dlw = nullptr, *dpx = nullptr;
   float *dlw2 = nullptr, *dpx2 = nullptr, *contrib = nullptr, *part = nullptr, *part2 = nullptr;
   float *run_m = nullptr, *run_s = nullptr;
+  float* ebern = nullptr;            // engine: per-row Bernoulli log-likelihood, [rows][4] (cols 1-3 zero)
   int ldpart = 0, npart = 0;
   float* slabs = nullptr;
   float* fslab = nullptr;            // split-K partials of the first encoder layer (fused path)
@@ -142,6 +151,16 @@ struct iwae_handle {
   bool masked = false;               // active-unit masks in force (iwae_nll_masked only)
   long long n_mega = 0, n_mega_eps = 0;  // mega_fwd_kernel launches (all / injected noise), iwae_debug_count
   const float* mask[IWAE_MAX_LAYERS] = {};
+  // row-chain train engine plans (device resident, per shape; iwae_train.hip)
+  struct TcRec {
+    TcPlan* dev = nullptr;
+    int rt = 1, nb[kTcMaxJobs] = {0, 0};
+    size_t lds = 0;
+    double flop = 0.0;               // algorithmic FLOPs of one launch (weight products, no bias rows)
+  };
+  std::map<std::vector<long long>, TcRec> tc_plans;
+  int engine = 1;                    // train step on the row-chain engine when it applies (iwae_set_path)
+  bool adam_splits = false;          // the Adam launch being built also rewrites the split copies
   // graphs
   bool use_graphs = false;
   // a captured train step; its first kernel reads the caller's x directly
@@ -170,6 +189,10 @@ struct iwae_handle {
   GemmKind prof_k = GEMM_FWD; GemmEpi prof_e = EPI_STORE;
   int prof_tile = 0, prof_splits = 1; bool prof_ks = false;
   double prof_flop1 = 0.0;
+  bool prof_is_tc = false;             // the recorded launch is an engine launch (prof_kind 10 / 11)
+  TcArgs prof_tc{};
+  int prof_tc_rt = 1;
+  size_t prof_tc_lds = 0;
 };
 
 #define HIPCHK(expr)                                                           \
@@ -213,6 +236,7 @@ static StochL add_stoch(iwae_handle* h, int fin, int H, int d, int rows_kind) {
   s.l1 = add_dense(h, fin, H, rows_kind);
   s.l2 = add_dense(h, H, H, rows_kind);
   s.head = add_dense(h, H, 2 * d, rows_kind);   // [lmu | lstd] concatenated along N
+  h->dense[s.head].head_d = d;
   h->keras.push_back({s.l1, 0, H});
   h->keras.push_back({s.l2, 0, H});
   h->keras.push_back({s.head, 0, d});
@@ -230,6 +254,8 @@ static void destroy_graph(iwae_handle::GraphRec& g) {
 static void free_workspace(iwae_handle* h) {
   for (auto& kv : h->graphs) destroy_graph(kv.second);
   h->graphs.clear();
+  for (auto& kv : h->tc_plans) (void)hipFree(kv.second.dev);    // they point into the arena
+  h->tc_plans.clear();
   if (h->arena) (void)hipFree(h->arena);
   h->arena = nullptr;
   h->arena_bytes = 0;
@@ -316,6 +342,7 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
   vec(h->logq, rows); vec(h->logp, rows); vec(h->lw, rows);
   vec(h->dlw, rows); vec(h->dpx, rows); vec(h->dlw2, rows); vec(h->dpx2, rows);
   vec(h->contrib, Bimg); vec(h->run_m, Bimg); vec(h->run_s, Bimg);
+  vec(h->ebern, (size_t)rows * 4);
   h->fslab_S = (int)std::min<long long>(16, cdiv(h->xdim + 1, 64));
   vec(h->fslab, (size_t)h->fslab_S * Bimg * r4(h->enc[0].H + 1));
   if (train && rows <= 65536) {
@@ -634,7 +661,7 @@ static int forward_core(iwae_handle* h, const Plan& P, const EpsSet& E, bool tra
 }
 
 static int run_bound(iwae_handle* h, const Plan& P, bool train, float sign, float* value_out,
-                     bool adam_tick = false) {
+                     bool adam_tick = false, bool engine = false) {
   if (P.kl) {
     const int Lm1 = h->L - 1;
     const int rows = Lm1 == 0 ? P.Bimg : P.Bimg * P.kS;
@@ -644,6 +671,7 @@ static int run_bound(iwae_handle* h, const Plan& P, bool train, float sign, floa
   BoundArgs b{};
   b.part = h->part; b.part2 = P.need_bce ? h->part2 : nullptr; b.ldpart = h->ldpart; b.npart = h->npart;
   b.logp = h->logp; b.logq = h->logq;
+  if (engine) { b.part = h->ebern; b.ldpart = 4; b.npart = 1; b.part2 = nullptr; }   // row totals
   b.lw = h->lw; b.contrib = h->contrib;
   b.dlw = train ? h->dlw : nullptr; b.dpx = train ? h->dpx : nullptr;
   b.dlw2 = (train && P.piwae) ? h->dlw2 : nullptr; b.dpx2 = (train && P.piwae) ? h->dpx2 : nullptr;
@@ -762,6 +790,34 @@ static int ensure_wsplit(iwae_handle* h) {
   return IWAE_OK;
 }
 
+// refresh the fragment-major copies of every Dense layer but the first encoder
+// layer's (which never runs on the engine)
+static int run_fx(iwae_handle* h) {
+  FxArgs a{};
+  a.param = h->params; a.hi = h->fx_hi; a.lo = h->fx_lo;
+  long long tot = 0;
+  for (size_t i = 0; i < h->dense.size(); ++i) {
+    const DenseL& d = h->dense[i];
+    if (d.rows_kind == 0) continue;
+    FxSeg& g = a.seg[a.nseg++];
+    g.off = d.off; g.fin = d.fin; g.fout = d.fout; g.ldw = d.ldw;
+    g.fx_off = d.fx_off; g.fx_tiles = d.fx_tiles; g.fx_steps = d.fx_steps; g.head_d = d.head_d;
+    g.gx_off = d.gx_off; g.gx_tiles = d.gx_tiles; g.gx_steps = d.gx_steps;
+    g.start = tot;
+    tot += ((long long)d.fx_tiles * d.fx_steps + (long long)d.gx_tiles * d.gx_steps) * 64;
+  }
+  a.total = tot;
+  HIPCHK(launch_fx_refresh(h->stream, a));
+  return IWAE_OK;
+}
+
+static int ensure_fx(iwae_handle* h) {
+  if (h->fx_version == h->params_version) return IWAE_OK;
+  CHK(run_fx(h));
+  h->fx_version = h->params_version;
+  return IWAE_OK;
+}
+
 
 static int run_adam(iwae_handle* h, bool read_slabs, bool write_grad, bool do_adam, float scale_override,
                     bool tick, const float* scale_dev = nullptr, float* tail = nullptr) {
@@ -769,8 +825,12 @@ static int run_adam(iwae_handle* h, bool read_slabs, bool write_grad, bool do_ad
   a.scale_dev = scale_dev;
   a.tail = tail; a.tail_val = scale_override;
   a.param = h->params; a.m = h->adam_m; a.v = h->adam_v; a.grad = h->grad; a.slabs = h->slabs;
-  a.whi = nullptr; a.wlo = nullptr;          // split copies are refreshed lazily (ensure_wsplit)
+  // the engine reads the split copies: its steps rewrite them with every update,
+  // other paths refresh them lazily (ensure_wsplit)
+  const bool splits = do_adam && h->adam_splits;
+  a.whi = splits ? h->wsplit_hi : nullptr; a.wlo = splits ? h->wsplit_lo : nullptr;
   if (do_adam) h->params_version++;
+  if (splits) h->wsplit_version = h->params_version;
   long long mx = 0;
   for (size_t i = 0; i < h->dense.size(); ++i) {
     const DenseL& d = h->dense[i];
@@ -878,8 +938,9 @@ static bool smallm_ok(const iwae_handle* h, int rows) {
   return true;
 }
 
-static int fused_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool train) {
-  const int L = h->L, kS = P.kS, M = P.Bimg * kS;
+// First encoder layer on the images (Stochastic_layer 0, F:58): y1, y2 and
+// its head (mu | zs) P0, per image.
+static int enc0_forward(iwae_handle* h, const Plan& P) {
   if (smallm_ok(h, P.Bimg)) {
     // (1') first encoder layer on the images: three N-split few-row launches
     const StochL& S0 = h->enc[0];
@@ -963,6 +1024,12 @@ static int fused_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool tr
     Lf.njobs = 1;
     HIPCHK(launch_rb_fwd(h->stream, Lf));
   }
+  return IWAE_OK;
+}
+
+static int fused_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool train) {
+  const int L = h->L, kS = P.kS, M = P.Bimg * kS;
+  CHK(enc0_forward(h, P));
   // (3) encoder layers 1..L-1 (layer 1 samples h1 from P0 in its prologue)
   for (int i = 1; i < L; ++i) {
     RbFwdLaunch Lf{};
@@ -1134,9 +1201,10 @@ static int fused_decoder_bwd(iwae_handle* h, const Plan& P, const float* dlw, co
   return IWAE_OK;
 }
 
-static int fused_encoder_bwd(iwae_handle* h, const Plan& P, const float* dlw) {
+// encoder backward, layers top .. 0 (top < 0: all)
+static int fused_encoder_bwd(iwae_handle* h, const Plan& P, const float* dlw, int top = -1) {
   const int L = h->L, kS = P.kS, M = P.Bimg * kS;
-  for (int i = L - 1; i >= 0; --i) {
+  for (int i = top < 0 ? L - 1 : top; i >= 0; --i) {
     const StochL& S = h->enc[i];
     RbBwdLaunch Lb{};
     Lb.ld_lds = rb_ld(h, true);
@@ -1229,6 +1297,302 @@ static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const
   return IWAE_OK;
 }
 
+// ------------------------------------------------ row-chain train engine
+// Train step = first encoder layer (per image, enc0_forward) -> engine forward
+// (jobs E, O) -> bound -> engine backward (jobs O', E') -> first encoder layer
+// backward -> grouped weight gradients -> Adam (which also rewrites the split
+// copies the engine reads).  See iwae_train.hip.
+constexpr int kTcMaxLayers = 3;      // op-table capacity: 4 ops per stochastic layer and direction
+
+static bool use_engine(const iwae_handle* h, const Plan& P) {
+  if (!h->engine || !h->x3 || h->path == 1 || h->path == 2 || h->masked) return false;
+  if (P.need_bce || P.kl || P.piwae) return false;       // BCE / KL / two-weighting losses: fused row-block path
+  if (h->L > kTcMaxLayers) return false;
+  return (long long)P.Bimg * P.kS <= (1LL << 18);
+}
+
+struct TcBuild {
+  TcJob J;
+  std::vector<int> width;
+  TcBuild() : width(kTcMaxBufs, 0) { std::memset(&J, 0, sizeof(J)); }
+  void need(int b, int w) {
+    if (b >= 0) width[b] = std::max(width[b], w);
+  }
+  TcOp& add(int kind) {
+    TcOp& o = J.op[J.nop++];
+    std::memset(&o, 0, sizeof(o));
+    o.kind = kind;
+    o.in_buf = o.out_buf = -1;
+    return o;
+  }
+};
+
+static void tc_w(iwae_handle* h, TcOp& o, int di, bool bwd) {
+  const DenseL& d = h->dense[di];
+  const long long off = bwd ? d.gx_off : d.fx_off;
+  o.Whi = h->fx_hi + off;
+  o.Wlo = h->fx_lo + off;
+  o.W_bytes = (unsigned)((h->fx_elems - off) * (long long)sizeof(__bf16));
+  o.ldk = bwd ? d.ldG : d.ldF;
+  o.K = bwd ? d.fout : d.fin + 1;
+  o.N = bwd ? d.fin : d.fout;
+}
+// Dense op with an LDS output read by an op of padded width next_k
+static TcOp& tc_dense_op(iwae_handle* h, TcBuild& B, int kind, int di, bool bwd, int in, int out, int next_k) {
+  TcOp& o = B.add(kind);
+  tc_w(h, o, di, bwd);
+  o.in_buf = in; o.out_buf = out; o.next_k = next_k; o.ones = bwd ? 0 : 1;
+  B.need(in, o.ldk);
+  B.need(out, next_k);
+  return o;
+}
+static TcOp& tc_head_op(iwae_handle* h, TcBuild& B, int kind, int di, int in, int out, int d, int next_k) {
+  TcOp& o = tc_dense_op(h, B, kind, di, false, in, out, next_k);
+  o.d = d;
+  o.N = 8 * ((d + 3) / 4);                   // [mu quad | zs quad] groups of 8
+  B.need(out, 16 * ((o.N + 15) / 16) / 2);   // latent columns the epilogue writes
+  return o;
+}
+
+// LDS layout of one job for RT row tiles: every buffer = hi and lo planes of
+// [16 RT][ld] bf16 with a row stride of 8 mod 16 dwords (conflict-free
+// fragment reads), then the per-row accumulators.  Returns the bytes.
+static size_t tc_layout(TcBuild& B, int rt) {
+  const int R = 16 * rt;
+  int off = 0;
+  for (int b = 0; b < kTcMaxBufs; ++b) {
+    if (B.width[b] == 0) continue;
+    int sdw = (std::max(B.width[b], 32) + 1) / 2;
+    while (sdw % 16 != 8) ++sdw;
+    B.J.buf_ld[b] = 2 * sdw;
+    B.J.buf_off[b] = off;
+    off += 2 * R * B.J.buf_ld[b];
+  }
+  return (size_t)off * sizeof(__bf16);
+}
+
+static std::vector<long long> tc_key(const Plan& P, int which) {
+  return {which, P.Bimg, P.Bsplit, P.kS};
+}
+
+// forward (which = 0) or backward (1) plan of this shape: built once, uploaded
+static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
+  const auto key = tc_key(P, which);
+  if (h->tc_plans.count(key)) return IWAE_OK;
+  const int L = h->L, kS = P.kS;
+  auto r32 = [](int x) { return (x + 31) & ~31; };
+  std::vector<TcBuild> jobs;
+  auto ldF = [&](int di) { return h->dense[di].ldF; };
+  auto ldG = [&](int di) { return h->dense[di].ldG; };
+  if (which == 0) {
+    // job E: h1 (kept, buffer 0 .. L-2 hold h_0 .. h_{L-2}), P = L-1 (also h_{L-1}), Q = L
+    if (L >= 2) {
+      TcBuild B;
+      const int bP = L - 1, bQ = L;
+      auto hbuf = [&](int i) { return i == L - 1 ? bP : i; };
+      TcOp& s0 = B.add(TC_SAMPLE0);
+      s0.d = h->enc[0].d; s0.layer = 0; s0.acc = 1; s0.stdnormal = 0;
+      s0.P = h->eb[0].P.p; s0.ld_P = h->eb[0].P.ld; s0.P_div = kS;
+      s0.h = h->h[0].p; s0.ld_h = h->h[0].ld; s0.eps = h->eps_st[0].p; s0.ld_eps = h->eps_st[0].ld;
+      s0.out_buf = hbuf(0); s0.next_k = ldF(h->enc[1].l1);
+      B.need(s0.out_buf, s0.next_k);
+      for (int i = 1; i < L; ++i) {
+        const StochL& S = h->enc[i];
+        TcOp& a = tc_dense_op(h, B, TC_TANH, S.l1, false, hbuf(i - 1), bP, ldF(S.l2));
+        a.out = h->eb[i].y1.p; a.ld_out = h->eb[i].y1.ld;
+        TcOp& b = tc_dense_op(h, B, TC_TANH, S.l2, false, bP, bQ, ldF(S.head));
+        b.out = h->eb[i].y2.p; b.ld_out = h->eb[i].y2.ld;
+        const int nk = i < L - 1 ? ldF(h->enc[i + 1].l1) : ldF(h->dec[0].l1);
+        TcOp& c = tc_head_op(h, B, TC_SAMPLE, S.head, bQ, hbuf(i), S.d, nk);
+        c.layer = i; c.acc = 1; c.stdnormal = i == L - 1;
+        c.h = h->h[i].p; c.ld_h = h->h[i].ld; c.eps = h->eps_st[i].p; c.ld_eps = h->eps_st[i].ld;
+        c.out = h->eb[i].P.p; c.ld_out = h->eb[i].P.ld;
+      }
+      for (int j = 0; j < L - 1; ++j) {
+        const StochL& D = h->dec[j];
+        TcOp& a = tc_dense_op(h, B, TC_TANH, D.l1, false, hbuf(L - 1 - j), bQ, ldF(D.l2));
+        a.out = h->db[j].y1.p; a.ld_out = h->db[j].y1.ld;
+        TcOp& b = tc_dense_op(h, B, TC_TANH, D.l2, false, bQ, bP, ldF(D.head));
+        b.out = h->db[j].y2.p; b.ld_out = h->db[j].y2.ld;
+        TcOp& c = tc_head_op(h, B, TC_PRIOR, D.head, bP, -1, D.d, 0);
+        c.h = h->h[L - 2 - j].p; c.ld_h = h->h[L - 2 - j].ld;
+        c.out = h->db[j].P.p; c.ld_out = h->db[j].P.ld;
+      }
+      B.J.logq = h->logq; B.J.logp = h->logp;
+      jobs.push_back(B);
+    }
+    // job O: h1 again (same draw), output MLP, Bernoulli
+    {
+      TcBuild B;
+      TcOp& s0 = B.add(TC_SAMPLE0);
+      s0.d = h->enc[0].d; s0.layer = 0; s0.acc = L == 1; s0.stdnormal = L == 1;
+      s0.P = h->eb[0].P.p; s0.ld_P = h->eb[0].P.ld; s0.P_div = kS;
+      if (L == 1) { s0.h = h->h[0].p; s0.ld_h = h->h[0].ld; s0.eps = h->eps_st[0].p; s0.ld_eps = h->eps_st[0].ld; }
+      s0.out_buf = 0; s0.next_k = ldF(h->o1);
+      B.need(0, s0.next_k);
+      TcOp& a = tc_dense_op(h, B, TC_TANH, h->o1, false, 0, 1, ldF(h->o2));
+      a.out = h->ob.y1.p; a.ld_out = h->ob.y1.ld;
+      TcOp& b = tc_dense_op(h, B, TC_TANH, h->o2, false, 1, 2, ldF(h->o3));
+      b.out = h->ob.y2.p; b.ld_out = h->ob.y2.ld;
+      TcOp& c = tc_dense_op(h, B, TC_BERN, h->o3, false, 2, -1, 0);
+      c.out = h->ob.P.p; c.ld_out = h->ob.P.ld;
+      B.J.bern = h->ebern; B.J.ld_bern = 4;
+      if (L == 1) { B.J.logq = h->logq; B.J.logp = h->logp; }
+      jobs.push_back(B);
+    }
+  } else {
+    // job O': (dpx g) W3^T (1 - y2^2) -> W2^T (1 - y1^2) -> W1^T = dL/dh1 (output MLP part)
+    {
+      TcBuild B;
+      TcOp& g = B.add(TC_LOADG);
+      g.out_buf = 0; g.N = h->xdim; g.next_k = ldG(h->o3);
+      g.y = h->ob.P.p; g.ld_y = h->ob.P.ld;
+      B.need(0, g.next_k);
+      TcOp& a = tc_dense_op(h, B, TC_TGRAD, h->o3, true, 0, 1, ldG(h->o2));
+      a.y = h->ob.y2.p; a.ld_y = h->ob.y2.ld; a.out = h->ob.dY2.p; a.ld_out = h->ob.dY2.ld;
+      TcOp& b = tc_dense_op(h, B, TC_TGRAD, h->o2, true, 1, 2, ldG(h->o1));
+      b.y = h->ob.y1.p; b.ld_y = h->ob.y1.ld; b.out = h->ob.dY1.p; b.ld_out = h->ob.dY1.ld;
+      TcOp& c = tc_dense_op(h, B, TC_LIN, h->o1, true, 2, -1, 0);
+      c.out = h->dh_out[0].p; c.ld_out = h->dh_out[0].ld;
+      jobs.push_back(B);
+    }
+    // job E': decoder prior layers, then encoder layers L-1 .. 1 (row-local chain)
+    if (L >= 2) {
+      TcBuild B;
+      for (int j = 0; j < L - 1; ++j) {
+        const int t = L - 2 - j, src = L - 1 - j;
+        const StochL& D = h->dec[j];
+        TcOp& g = B.add(TC_GBWD_PRIOR);
+        g.d = D.d; g.out_buf = 0; g.next_k = ldG(D.head);
+        g.P = h->db[j].P.p; g.ld_P = h->db[j].P.ld;
+        g.h = h->h[t].p; g.ld_h = h->h[t].ld;
+        g.out = h->db[j].dP.p; g.ld_out = h->db[j].dP.ld;
+        g.dh = h->dh_prior[t].p; g.ld_dh = h->dh_prior[t].ld;
+        B.need(0, std::max(g.next_k, 2 * D.d));
+        TcOp& a = tc_dense_op(h, B, TC_TGRAD, D.head, true, 0, 1, ldG(D.l2));
+        a.y = h->db[j].y2.p; a.ld_y = h->db[j].y2.ld; a.out = h->db[j].dY2.p; a.ld_out = h->db[j].dY2.ld;
+        TcOp& b = tc_dense_op(h, B, TC_TGRAD, D.l2, true, 1, 0, ldG(D.l1));
+        b.y = h->db[j].y1.p; b.ld_y = h->db[j].y1.ld; b.out = h->db[j].dY1.p; b.ld_out = h->db[j].dY1.ld;
+        TcOp& c = tc_dense_op(h, B, TC_LIN, D.l1, true, 0, -1, 0);
+        c.out = h->dh_dec[src].p; c.ld_out = h->dh_dec[src].ld;
+      }
+      for (int i = L - 1; i >= 1; --i) {
+        const StochL& S = h->enc[i];
+        TcOp& g = B.add(TC_GBWD_ENC);
+        g.d = S.d; g.out_buf = 0; g.next_k = ldG(S.head); g.stdnormal = i == L - 1;
+        g.P = h->eb[i].P.p; g.ld_P = h->eb[i].P.ld;
+        g.h = h->h[i].p; g.ld_h = h->h[i].ld;
+        g.eps = h->eps_st[i].p; g.ld_eps = h->eps_st[i].ld;
+        int n = 0;
+        g.src[n] = h->dh_dec[i].p; g.ld_src[n++] = h->dh_dec[i].ld;
+        if (i <= L - 2) {
+          g.src[n] = h->dh_prior[i].p; g.ld_src[n++] = h->dh_prior[i].ld;
+          g.src[n] = h->dh_enc[i].p; g.ld_src[n++] = h->dh_enc[i].ld;
+        }
+        g.nsrc = n;
+        g.out = h->eb[i].dP.p; g.ld_out = h->eb[i].dP.ld;
+        B.need(0, std::max(g.next_k, 2 * S.d));
+        TcOp& a = tc_dense_op(h, B, TC_TGRAD, S.head, true, 0, 1, ldG(S.l2));
+        a.y = h->eb[i].y2.p; a.ld_y = h->eb[i].y2.ld; a.out = h->eb[i].dY2.p; a.ld_out = h->eb[i].dY2.ld;
+        TcOp& b = tc_dense_op(h, B, TC_TGRAD, S.l2, true, 1, 0, ldG(S.l1));
+        b.y = h->eb[i].y1.p; b.ld_y = h->eb[i].y1.ld; b.out = h->eb[i].dY1.p; b.ld_out = h->eb[i].dY1.ld;
+        TcOp& c = tc_dense_op(h, B, TC_LIN, S.l1, true, 0, -1, 0);
+        c.out = h->dh_enc[i - 1].p; c.ld_out = h->dh_enc[i - 1].ld;
+      }
+      jobs.push_back(B);
+    }
+  }
+  (void)r32;
+  if ((int)jobs.size() > kTcMaxJobs) return fail(h, IWAE_EINVAL, "engine: too many jobs");
+  // rows per workgroup: the largest tile count the LDS allows, fewer for small batches
+  const long long rows = (long long)P.Bimg * kS;
+  int want = 1;                         // (2 and 4 row tiles spill registers: knob only)
+  if (const char* e = std::getenv("IWAE_TC_RT")) want = std::atoi(e);   // tuning knob
+  iwae_handle::TcRec rec;
+  for (int rt : {4, 2, 1}) {
+    if (rt > want) continue;
+    size_t mx = 0;
+    int acc_off = 0;
+    for (auto& B : jobs) {
+      const size_t b = tc_layout(B, rt);
+      mx = std::max(mx, b);
+    }
+    acc_off = (int)((mx + 15) / 16 * 4);            // floats, 16-byte aligned
+    const size_t lds = (size_t)acc_off * sizeof(float) + (size_t)(2 + 3 * 8) * 16 * rt * sizeof(float);
+    if (lds <= 160 * 1024) {
+      rec.rt = rt;
+      rec.lds = lds;
+      TcPlan plan;
+      std::memset(&plan, 0, sizeof(plan));
+      plan.njobs = (int)jobs.size();
+      plan.acc_off = acc_off;
+      for (size_t j = 0; j < jobs.size(); ++j) plan.job[j] = jobs[j].J;
+      HIPCHK(hipMalloc(&rec.dev, sizeof(TcPlan)));
+      HIPCHK(hipMemcpy(rec.dev, &plan, sizeof(TcPlan), hipMemcpyHostToDevice));
+      const int nb = (int)cdiv(rows, 16 * rt);
+      for (size_t j = 0; j < jobs.size(); ++j) {
+        rec.nb[j] = nb;
+        for (int o = 0; o < jobs[j].J.nop; ++o) {
+          const TcOp& op = jobs[j].J.op[o];
+          if (op.kind > TC_LIN) continue;
+          const int kin = op.kind == TC_TGRAD || op.kind == TC_LIN ? op.K : op.K - 1;
+          const int nout = op.kind == TC_SAMPLE || op.kind == TC_PRIOR ? 2 * op.d : op.N;
+          rec.flop += 2.0 * (double)rows * kin * nout;
+        }
+      }
+      h->tc_plans[key] = rec;
+      return IWAE_OK;
+    }
+  }
+  return fail(h, IWAE_EINVAL, "engine: layer widths exceed the LDS");
+}
+
+static int tc_prepare(iwae_handle* h, const Plan& P) {
+  CHK(tc_prepare_one(h, P, 0));
+  return tc_prepare_one(h, P, 1);
+}
+
+static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which) {
+  auto it = h->tc_plans.find(tc_key(P, which));
+  if (it == h->tc_plans.end()) return fail(h, IWAE_EINVAL, "engine plan missing");
+  const iwae_handle::TcRec& rec = it->second;
+  TcArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.plan = rec.dev;
+  int tot = 0;
+  for (int j = 0; j < kTcMaxJobs; ++j) {
+    a.block_start[j] = tot;
+    tot += rec.nb[j];
+  }
+  a.block_start[kTcMaxJobs] = tot;
+  a.rows = P.Bimg * P.kS; a.kS = P.kS;
+  a.x = h->x_in.p; a.ldx = h->x_in.ld;
+  a.seed = h->seed; a.rng_base = &h->ds->rng[0];
+  for (int i = 0; i < h->L && i < 8; ++i) { a.eps_a[i] = E.a[i]; a.eps_b[i] = E.b[i]; }
+  a.Bsplit = P.Bsplit; a.Bimg = P.Bimg;
+  a.dlw = h->dlw; a.dpx = h->dpx; a.wa = P.wa;
+  const bool prof = h->prof_kind == 10 + which;
+  if (prof) {
+    if (h->prof_used + 2 > h->prof_ev.size()) {
+      for (int i = 0; i < 256; ++i) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        h->prof_ev.push_back(e);
+      }
+    }
+    HIPCHK(hipEventRecord(h->prof_ev[h->prof_used], h->stream));
+  }
+  HIPCHK(launch_tc(h->stream, a, rec.rt, rec.lds));
+  if (prof) {
+    HIPCHK(hipEventRecord(h->prof_ev[h->prof_used + 1], h->stream));
+    h->prof_used += 2;
+    h->prof_flop += rec.flop;
+    h->prof_have = true; h->prof_is_tc = true;
+    h->prof_tc = a; h->prof_tc_rt = rec.rt; h->prof_tc_lds = rec.lds; h->prof_flop1 = rec.flop;
+  }
+  return IWAE_OK;
+}
+
 static float* train_loss_ptr(iwae_handle* h) { return h->loss_out ? h->loss_out : &h->ds->scalars[0]; }
 
 // End of a train step / forward_backward: sum the weight-gradient slabs into the
@@ -1246,6 +1610,22 @@ static int finish_step(iwae_handle* h, const Plan& P, bool adam) {
       ncclSuccess)
     return fail(h, IWAE_EHIP, "ncclAllReduce of the gradient failed");
   return run_adam(h, false, true, true, 0.f, false, tail);
+}
+
+static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
+  CHK(enc0_forward(h, P));
+  CHK(tc_run(h, P, E, 0));
+  CHK(run_bound(h, P, true, -1.f, train_loss_ptr(h), adam, true));
+  CHK(tc_run(h, P, E, 1));
+  CHK(fused_encoder_bwd(h, P, h->dlw, 0));
+  CHK(weight_grads(h, P, true, true, h->dpx));
+  CHK(finish_step(h, P, adam));
+  if (adam) {
+    // the next step's engine reads the updated weights' fragment-major copies
+    CHK(run_fx(h));
+    h->fx_version = h->params_version;
+  }
+  return IWAE_OK;
 }
 
 static int fused_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
@@ -1267,6 +1647,7 @@ static int fused_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool
 
 // forward + backward (+ Adam) after x is staged
 static int train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
+  if (use_engine(h, P)) return engine_train_body(h, P, E, adam);
   // large batches: the output layer's forward (Bernoulli) and dX GEMMs on bf16x3
   // products of a split copy refreshed here, after the previous step's Adam
   h->out_x3 = h->x3 && h->out_x3_rows > 0 && (long long)P.Bimg * P.kS >= h->out_x3_rows;
@@ -1298,7 +1679,13 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
   CHK(ensure_capacity(h, P.Bimg, P.Bimg * P.kS, true));
   // the fused step's first kernel reads the caller's x itself (and fills x_in);
   // every other path stages x into x_in first
-  const bool direct = P.Bimg == P.B && use_fused(h, P) && smallm_ok(h, P.Bimg);
+  const bool engine = use_engine(h, P);
+  if (engine) {
+    // fragment-major copies current before the step; the step itself refreshes them after its Adam
+    CHK(ensure_fx(h));
+    CHK(tc_prepare(h, P));
+  }
+  const bool direct = P.Bimg == P.B && (engine || use_fused(h, P)) && smallm_ok(h, P.Bimg);
   if (!direct) CHK(copy_x(h, P, x));
   h->x_user = direct ? x : nullptr;
   const bool philox = (E.a[0] == nullptr);
@@ -1310,7 +1697,7 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
   } reset_flag{h};
   if (h->use_graphs && philox && h->prof_kind < 0) {
     std::vector<long long> key = {adam ? 1 : 0, lc->loss, B, lc->k, lc->k1, lc->k2, (long long)(uintptr_t)loss_dev,
-                                  direct ? 1 : 0};
+                                  direct ? 1 : 0, engine ? 1 : 0};
     float fk[3] = {lc->p, lc->alpha, lc->beta};
     for (float f : fk) {
       int bits;
@@ -1358,7 +1745,10 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
     HIPCHK(hipGraphLaunch(g.exec, h->stream));
     // the replayed Adam moved the parameters: the split (bf16x3) copies the
     // evaluation paths read are stale from here (run_adam's bump only ran at capture)
-    if (adam) h->params_version++;
+    if (adam) {
+      h->params_version++;
+      if (engine) h->fx_version = h->params_version;   // the replayed step refreshed the fragment-major copies
+    }
   } else {
     CHK(train_body(h, P, E, adam));
   }
@@ -1413,6 +1803,15 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   h->keras.push_back({h->o2, 0, Hd});
   h->keras.push_back({h->o3, 0, cfg->x_dim});
   for (auto& k : h->keras) h->nparam_keras += (long long)(h->dense[k.di].fin + 1) * k.width;
+  for (auto& d : h->dense) {
+    const int nf = d.head_d > 0 ? 8 * ((d.head_d + 3) / 4) : d.fout;
+    d.fx_tiles = (nf + 15) / 16; d.fx_steps = d.ldF / 32;
+    d.gx_tiles = (d.fin + 15) / 16; d.gx_steps = d.ldG / 32;
+    d.fx_off = h->fx_elems;
+    h->fx_elems += (long long)d.fx_tiles * d.fx_steps * 64 * 8;
+    d.gx_off = h->fx_elems;
+    h->fx_elems += (long long)d.gx_tiles * d.gx_steps * 64 * 8;
+  }
   hipError_t e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
   h->stream = h->own_stream;
   const size_t pb = (size_t)h->nparam_int * sizeof(float);
@@ -1427,6 +1826,8 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (e == hipSuccess) e = hipMalloc(&h->grad_own, pb + 4 * sizeof(float));   // + the DP batch-size tail
   if (e == hipSuccess) e = hipMalloc(&h->ds, sizeof(DevState));
   if (e == hipSuccess) e = hipMalloc(&h->wsplit_hi, (size_t)(2 * h->wsplit_elems) * sizeof(__bf16));
+  if (e == hipSuccess) e = hipMalloc(&h->fx_hi, (size_t)(2 * h->fx_elems) * sizeof(__bf16));
+  if (e == hipSuccess) e = hipMemset(h->fx_hi, 0, (size_t)(2 * h->fx_elems) * sizeof(__bf16));
   if (e == hipSuccess) e = hipMemset(h->wsplit_hi, 0, (size_t)(2 * h->wsplit_elems) * sizeof(__bf16));
   if (e == hipSuccess) e = hipMemset(h->params, 0, h->params_bytes);
   if (e == hipSuccess) e = hipMemset(h->adam_m, 0, pb);
@@ -1445,11 +1846,14 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   }
   h->grad = h->grad_own;
   h->wsplit_lo = h->wsplit_hi + h->wsplit_elems;
+  h->fx_lo = h->fx_hi + h->fx_elems;
   e = rb_setup_attributes();
   if (e == hipSuccess) e = mega_setup_attributes();
   if (const char* w = std::getenv("IWAE_TRAIN_OUT_X3_ROWS")) h->out_x3_rows = std::atoll(w);   // tuning knob
   if (const char* w = std::getenv("IWAE_MG_WAVES")) h->mg_waves = std::atoi(w) == 4 ? 4 : 8;   // tuning knob
   if (e == hipSuccess) e = smallm_setup_attributes();
+  if (e == hipSuccess) e = tc_setup_attributes();
+  if (const char* w = std::getenv("IWAE_ENGINE")) h->engine = std::atoi(w) != 0;   // A/B switch
   if (e != hipSuccess) {
     g_create_error = std::string("hipFuncSetAttribute failed: ") + hipGetErrorString(e);
     iwae_destroy(h);
@@ -1473,6 +1877,7 @@ void iwae_destroy(iwae_handle* h) {
   if (h->grad_own) (void)hipFree(h->grad_own);
   if (h->ds) (void)hipFree(h->ds);
   if (h->wsplit_hi) (void)hipFree(h->wsplit_hi);
+  if (h->fx_hi) (void)hipFree(h->fx_hi);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
   delete h;
 }
@@ -1519,7 +1924,8 @@ int iwae_set_seed(iwae_handle* h, unsigned long long seed) {
 
 int iwae_set_path(iwae_handle* h, int path) {
   if (!h) return IWAE_EINVAL;
-  if (path < 0 || path > 2) return fail(h, IWAE_EINVAL, "path must be 0 (auto), 1 (layer-wise) or 2 (fused)");
+  if (path < 0 || path > 3)
+    return fail(h, IWAE_EINVAL, "path must be 0 (auto), 1 (layer-wise), 2 (fused row-block) or 3 (engine)");
   h->path = path;
   h->nll_fused = path != 1;             // layer-wise everywhere when asked for
   for (auto& kv : h->graphs) destroy_graph(kv.second);
@@ -2140,6 +2546,7 @@ int iwae_profile_gemm(iwae_handle* h, int kind, int epi) {
   h->prof_used = 0;
   h->prof_flop = 0.0;
   h->prof_have = false;
+  h->prof_is_tc = false;
   return IWAE_OK;
 }
 
@@ -2151,8 +2558,10 @@ int iwae_profile_replay(iwae_handle* h, int n, double* total_ms, double* total_f
   HIPCHK(hipEventCreate(&e1));
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipEventRecord(e0, h->stream));
-  for (int i = 0; i < n; ++i)
-    HIPCHK(launch_gemm(h->stream, h->prof_k, h->prof_e, h->prof_tile, h->prof_splits, h->prof_ks, h->prof_args));
+  for (int i = 0; i < n; ++i) {
+    if (h->prof_is_tc) HIPCHK(launch_tc(h->stream, h->prof_tc, h->prof_tc_rt, h->prof_tc_lds));
+    else HIPCHK(launch_gemm(h->stream, h->prof_k, h->prof_e, h->prof_tile, h->prof_splits, h->prof_ks, h->prof_args));
+  }
   HIPCHK(hipEventRecord(e1, h->stream));
   HIPCHK(hipEventSynchronize(e1));
   float ms = 0.f;

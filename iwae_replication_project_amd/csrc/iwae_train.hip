@@ -1,0 +1,833 @@
+// Row-chain train engine (gfx950): the train step's per-sample-row work as
+// chains of Dense layers and Gaussian / Bernoulli ops run by one workgroup on
+// 16*RT sample rows, activations resident in LDS.
+//
+// Forward (Flexible_Model.train_step F:221 -> get_log_weights F:327-F:351):
+//   job E: sample h1 from the image's (mu, zs) (F:58-F:60), every later encoder
+//          layer (F:66-F:73: tanh, tanh, head -> sample h_i, log q), log N(h_L;
+//          0, 1) (F:135-F:136), the decoder prior layers (F:138-F:141);
+//   job O: sample h1 again (same Philox draw), the output MLP tanh, tanh,
+//          Dense(784) -> sigmoid, clamp, Bernoulli log-prob row sum and the
+//          dLoss/dlogit factor g (F:92-F:96, F:123-F:129).
+// Backward (tape.gradient, F:243), after the bound kernel's dL/dlw:
+//   job O': (dpx * g) -> W3^T (1 - y2^2) -> W2^T (1 - y1^2) -> W1^T: dL/dh1;
+//   job E': per decoder prior layer: dP of its head -> W^T chain -> dL/dh of
+//           its input; per encoder layer (top down): dP of its sampling head
+//           from the dL/dh sources -> W^T chain -> dL/dh of its input.
+// Every f32 tensor the weight gradients need (y, P, dZ, g, h, eps) is written
+// by the epilogues; the first encoder layer (per image) and the weight
+// gradients run as separate launches.
+//
+// Products: bf16x3 on v_mfma_f32_16x16x32_bf16 (w_lo a_hi + w_hi a_lo + w_hi
+// a_hi, f32 accumulate; ~2^-16 relative per product).  The weights are the
+// MFMA A operand: each lane streams one output feature's pre-split row of the
+// layer's F copy (forward, k = fin + 1 incl. the bias) or G copy (backward,
+// k = fout), 16-byte buffer loads, k contiguous; the fragments of the wave's
+// next column tile are requested during the current tile's MFMAs.  The
+// activations are the B operand, kept in LDS as split bf16 planes (hi, lo) so
+// a fragment is two ds_read_b128; each value is split once, by its producer.
+// A lane's four accumulators are four consecutive output features of one
+// sample row: epilogues store them as one 16-byte f32 store and one 8-byte
+// store per LDS plane.
+#include "iwae_kernels.h"
+
+namespace iwae {
+
+typedef float tc_f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 tc_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 tc_bf16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned tc_u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int TC_NW = 8;      // waves per workgroup
+constexpr int TC_KS = 4;      // k steps of 32 per weight fetch unit (128 k)
+constexpr float kBernOff0T = 9.1327896e-7f;   // 1 - 0.999999f - 1e-7f (F:126 constants in f32)
+
+extern __shared__ __attribute__((aligned(16))) float tcs[];
+
+#ifdef IWAE_TC_TRACE
+// Debug build only (-DIWAE_TC_TRACE): 100 MHz timestamps of the first
+// workgroup of every job: [rec][0] = job, [1] = entry, then per op its start
+// and wave 0's end (before the barrier); and of wave 0's first-tile MFMA start.
+__device__ unsigned long long g_tc_trace[256 * 64];
+__device__ unsigned g_tc_trace_n;
+// per-unit stamps of wave 0 of the traced workgroups: [rec][op < 8][unit < 16][3]
+__device__ unsigned long long g_tc_utrace[256 * 8 * 16 * 3];
+__device__ int tc_tr_rec = -1, tc_tr_op = 0;   // (set per workgroup in registers; see tc_kernel)
+#endif
+
+// The plan is read through the constant address space: its fields are
+// wave-uniform, so they become scalar loads (s_load, scalar cache).  Through a
+// generic pointer the compiler has to assume the kernel's own global stores may
+// alias them and emits vector loads, each followed by a vmcnt(0) that drains
+// every outstanding weight fetch.
+#define TC_CONST __attribute__((address_space(4)))
+typedef const TC_CONST TcOp COp;
+typedef const TC_CONST TcJob CJob;
+typedef const TC_CONST TcPlan CPlan;
+
+struct TcBuf {
+  __bf16* hi; __bf16* lo; int ld;
+};
+template <int RT>
+__device__ __forceinline__ TcBuf tc_buf(CJob& J, int b) {
+  __bf16* base = reinterpret_cast<__bf16*>(tcs);
+  TcBuf B;
+  B.ld = J.buf_ld[b];
+  B.hi = base + J.buf_off[b];
+  B.lo = B.hi + 16 * RT * B.ld;
+  return B;
+}
+
+__device__ __forceinline__ tc_bf16x8 tc_as_bf16x8(tc_u32x4 v) { return __builtin_bit_cast(tc_bf16x8, v); }
+
+// four f32 -> hi / lo planes at element offset o (o % 4 == 0)
+__device__ __forceinline__ void tc_put4(const TcBuf& B, int o, const float (&v)[4]) {
+  tc_bf16x4 vh, vl;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    vh[i] = (__bf16)v[i];
+    vl[i] = (__bf16)(v[i] - (float)vh[i]);
+  }
+  *reinterpret_cast<tc_bf16x4*>(B.hi + o) = vh;
+  *reinterpret_cast<tc_bf16x4*>(B.lo + o) = vl;
+}
+__device__ __forceinline__ void tc_put1(const TcBuf& B, int o, float v) {
+  const __bf16 h = (__bf16)v;
+  B.hi[o] = h;
+  B.lo[o] = (__bf16)(v - (float)h);
+}
+
+// zero padding [width, next_k) of every row of B (ones column at width if asked)
+template <int RT>
+__device__ __forceinline__ void tc_pad(const TcBuf& B, int width, int next_k, bool ones) {
+  constexpr int R = 16 * RT, TPR = (TC_NW * 64) / R;
+  const int row = threadIdx.x / TPR;
+  for (int col = width + threadIdx.x % TPR; col < next_k; col += TPR) {
+    B.hi[row * B.ld + col] = (__bf16)((ones && col == width) ? 1.f : 0.f);
+    B.lo[row * B.ld + col] = (__bf16)0.f;
+  }
+}
+
+struct TcFrag {
+  tc_bf16x8 h[TC_KS], l[TC_KS];
+};
+
+// source row of output feature f (head stages: features permuted into groups
+// of 8, [mu 4q..4q+3 | zs 4q..4q+3]); -1: none
+__device__ __forceinline__ int tc_src_row(COp& S, int f) {
+  if (S.kind != TC_SAMPLE && S.kind != TC_PRIOR) return f < S.N ? f : -1;
+  const int q = f >> 3, w = f & 7, j = 4 * q + (w & 3);
+  if (j >= S.d) return -1;
+  return w < 4 ? j : S.d + j;
+}
+// byte offset (both planes) of this lane's fragment of column tile t at k0 in
+// the fragment-major copy (FX / GX: [tile][k step][64 lanes][8]), or kOOB
+__device__ __forceinline__ unsigned tc_frag_base(COp& S, int t, int k0) {
+  const int lane = threadIdx.x & 63;
+  const int ntile = (S.N + 15) >> 4;
+  return t < ntile ? (unsigned)(((t * (S.ldk >> 5) + (k0 >> 5)) * 64 + lane) * 16) : kOOB;
+}
+__device__ __forceinline__ void tc_fetch_step(__amdgpu_buffer_rsrc_t rh, __amdgpu_buffer_rsrc_t rl, unsigned vb,
+                                              int u, int ns, TcFrag& f) {
+  if (u >= ns) return;
+  f.h[u] = tc_as_bf16x8(__builtin_amdgcn_raw_buffer_load_b128(rh, vb, 1024 * u, 0));
+  f.l[u] = tc_as_bf16x8(__builtin_amdgcn_raw_buffer_load_b128(rl, vb, 1024 * u, 0));
+}
+
+// acc[rt] += W-tile . IN[rows of rt][k0 .. k0 + 32 ns) (bf16x3)
+template <int RT>
+__device__ __forceinline__ void tc_mma(const TcBuf& IN, int k0, int ns, const TcFrag& f, tc_f32x4 (&acc)[RT]) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  constexpr int RH = RT < 2 ? RT : 2;
+  constexpr int NP = RT / RH;
+  constexpr int NC = TC_KS * NP;
+  tc_bf16x8 ah[2][RH], al[2][RH];
+  auto rd = [&](int c, int b) {
+    const int u = c / NP, p = c % NP;
+#pragma unroll
+    for (int i = 0; i < RH; ++i) {
+      const int ao = ((p * RH + i) * 16 + r) * IN.ld + k0 + 32 * u + 8 * g;
+      ah[b][i] = *reinterpret_cast<const tc_bf16x8*>(IN.hi + ao);
+      al[b][i] = *reinterpret_cast<const tc_bf16x8*>(IN.lo + ao);
+    }
+  };
+  rd(0, 0);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int u = c / NP, p = c % NP, b = c & 1;
+    if (u >= ns) break;
+    if (c + 1 < NC && (c + 1) / NP < ns) rd(c + 1, b ^ 1);
+#pragma unroll
+    for (int i = 0; i < RH; ++i)
+      acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.l[u], ah[b][i], acc[p * RH + i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < RH; ++i)
+      acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], al[b][i], acc[p * RH + i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < RH; ++i)
+      acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], ah[b][i], acc[p * RH + i], 0, 0, 0);
+  }
+}
+
+// per-lane row state: log q / log p partial sums (natural log), the Bernoulli
+// log2 sum, and the pixel offset of the row's image
+template <int RT>
+struct TcRows {
+  float q[RT], p[RT], l2[RT];
+  unsigned xoff[RT];
+};
+
+// injected noise of latent columns j, j+1 of global row grow (0 past d)
+__device__ __forceinline__ float2 tc_eps2(const TcArgs& A, int layer, int d, int grow, int j) {
+  const int bi = grow / A.kS, s = grow - bi * A.kS;
+  const float* src = bi < A.Bsplit ? A.eps_a[layer] + ((size_t)s * A.Bsplit + bi) * d
+                                   : A.eps_b[layer] + ((size_t)s * (A.Bimg - A.Bsplit) + (bi - A.Bsplit)) * d;
+  return make_float2(j < d ? src[j] : 0.f, j + 1 < d ? src[j + 1] : 0.f);
+}
+
+// ------------------------------------------------------------ epilogues
+// TANH / TGRAD / LIN: features f0..f0+3 of row rt*16 + r
+template <int RT, int KIND>
+__device__ __forceinline__ void tc_store_act(COp& S, const TcBuf& OUT, int t, const tc_f32x4 (&acc)[RT],
+                                             const float4 (&yv)[RT], int row0, int nrows) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  const int f0 = t * 16 + 4 * g;
+  if (f0 >= S.N) return;
+  const bool full = f0 + 3 < S.N;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float a = acc[rt][i];
+      if (KIND == TC_TANH) {
+        v[i] = ftanh(a);
+      } else if (KIND == TC_TGRAD) {
+        const float y = i == 0 ? yv[rt].x : i == 1 ? yv[rt].y : i == 2 ? yv[rt].z : yv[rt].w;
+        v[i] = a * (1.f - y * y);
+      } else {
+        v[i] = a;
+      }
+    }
+    const int row = rt * 16 + r;
+    if (S.out_buf >= 0) {
+      const int o = row * OUT.ld + f0;
+      if (full) {
+        tc_put4(OUT, o, v);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (f0 + i < S.N) tc_put1(OUT, o + i, v[i]);
+      }
+    }
+#ifdef IWAE_TC_NOSTORE
+    if (false) {
+#else
+    if (S.out && row < nrows) {
+#endif
+      float* dst = S.out + (size_t)(row0 + row) * S.ld_out + f0;
+      if (full) {
+        *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (f0 + i < S.N) dst[i] = v[i];
+      }
+    }
+  }
+}
+
+// Head epilogue (SAMPLE / PRIOR).  Lane groups g hold, for quad q = 2t + (g >> 1),
+// the mu quad (g even) or the zs quad (g odd); two v_permlane16_swap leave every
+// lane (mu, zs) of its own two latent columns j0, j0 + 1.
+template <int RT, int KIND>
+__device__ __forceinline__ void tc_head(const TcArgs& A, COp& S, const TcBuf& H, int t, uint64_t base,
+                                        const tc_f32x4 (&acc)[RT], const float2 (&tv)[RT], TcRows<RT>& R, int row0,
+                                        int nrows) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  const int q = 2 * t + (g >> 1);
+  const int j0 = 4 * q + 2 * (g & 1);
+  const int d = S.d;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const auto p0 = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[rt][0]), __float_as_uint(acc[rt][2]),
+                                                     false, false);
+    const auto p1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[rt][1]), __float_as_uint(acc[rt][3]),
+                                                     false, false);
+    const float mu[2] = {__uint_as_float(p0[0]), __uint_as_float(p1[0])};
+    const float zs[2] = {__uint_as_float(p0[1]), __uint_as_float(p1[1])};
+    const int row = rt * 16 + r;
+    const int grow = row0 + min(row, nrows - 1);
+    const bool st = row < nrows;
+    float* Pr = S.out ? S.out + (size_t)grow * S.ld_out : nullptr;
+    if (KIND == TC_SAMPLE) {
+      float2 e;
+      if (A.eps_a[S.layer]) e = tc_eps2(A, S.layer, d, grow, j0);
+      else e = philox_normal2(A.seed, base, (unsigned)grow, (unsigned)S.layer, (unsigned)q, (g & 1) != 0);
+      float hv[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int j = j0 + c;
+        const float sc = fexp(zs[c]) + kScaleEps;
+        const float ec = c == 0 ? e.x : e.y;
+        const float h = ec * sc + mu[c];
+        if (j < d) {
+          if (S.acc) R.q[rt] += normal_logp(h, mu[c], sc);
+          if (S.stdnormal) R.p[rt] += -0.5f * (h * h) - kHalfLog2Pi;
+          if (st) {
+            S.h[(size_t)grow * S.ld_h + j] = h;
+            S.eps[(size_t)grow * S.ld_eps + j] = ec;
+            Pr[j] = mu[c];
+            Pr[d + j] = zs[c];
+          }
+        }
+        hv[c] = j < d ? h : (j == d ? 1.f : 0.f);
+      }
+      tc_put1(H, row * H.ld + j0, hv[0]);
+      tc_put1(H, row * H.ld + j0 + 1, hv[1]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int j = j0 + c;
+        if (j < d) {
+          const float sc = fexp(zs[c]) + kScaleEps;
+          R.p[rt] += normal_logp(c == 0 ? tv[rt].x : tv[rt].y, mu[c], sc);
+          if (st && Pr) {
+            Pr[j] = mu[c];
+            Pr[d + j] = zs[c];
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);     // one row tile at a time (register pressure)
+  }
+}
+
+// Output layer: TFP Bernoulli(probs = sigmoid(l)*(1-1e-6)+1e-7).log_prob(x)
+// summed over the row (F:126-F:128) and g = wa * dlog p / dlogit stored for the
+// backward pass.  Binarised pixels: the selected probability is
+// sigmoid(+-l) * c + (x ? 1e-7 : 1 - c - 1e-7) (no f32 cancellation), four of
+// them multiplied before one log2.
+template <int RT>
+__device__ __forceinline__ void tc_bern(const TcArgs& A, COp& S, int t, const tc_f32x4 (&acc)[RT],
+                                        const float4 (&xv)[RT], TcRows<RT>& R, int row0, int nrows) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  const int f0 = t * 16 + 4 * g;
+  bool bin = true;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+    bin = bin && (xv[rt].x == 0.f || xv[rt].x == 1.f) && (xv[rt].y == 0.f || xv[rt].y == 1.f) &&
+          (xv[rt].z == 0.f || xv[rt].z == 1.f) && (xv[rt].w == 0.f || xv[rt].w == 1.f);
+  const bool allbin = __all(bin);
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    float gv[4];
+    if (allbin) {
+      float prod = 1.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float x = f4_at(xv[rt], i);
+        const bool one = x != 0.f;
+        const float z = one ? acc[rt][i] : -acc[rt][i];
+        const float s = frcp(1.f + fexp(-z));
+        const float sel = __builtin_fmaf(s, kProbScale, one ? kProbShift : kBernOff0T);
+        prod *= (f0 + i < S.N) ? sel : 1.f;
+        const float dsg = kProbScale * (s * (1.f - s));
+        gv[i] = A.wa * ((one ? dsg : -dsg) * frcp(sel));
+      }
+      R.l2[rt] += __builtin_amdgcn_logf(prod);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float x = f4_at(xv[rt], i);
+        const float e = fexp(-acc[rt][i]);
+        const float sp = frcp(1.f + e);
+        const float p1 = __builtin_fmaf(sp, kProbScale, kProbShift);
+        const float p0 = __builtin_fmaf(e * sp, kProbScale, kBernOff0T);
+        const float v = x * __builtin_amdgcn_logf(p1) + (1.f - x) * __builtin_amdgcn_logf(p0);
+        R.l2[rt] += (f0 + i < S.N) ? v : 0.f;
+        const float dsg = kProbScale * (sp * (1.f - sp));
+        gv[i] = A.wa * ((x * frcp(p1) - (1.f - x) * frcp(p0)) * dsg);
+      }
+    }
+    const int row = rt * 16 + r;
+#ifdef IWAE_TC_NOSTORE
+    if (false) {
+#else
+    if (row < nrows && f0 < S.N) {
+#endif
+      float* dst = S.out + (size_t)(row0 + row) * S.ld_out + f0;
+      if (f0 + 3 < S.N) {
+        *reinterpret_cast<float4*>(dst) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (f0 + i < S.N) dst[i] = gv[i];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------- dense op
+// A wave's work in one Dense op is a sequence of fetch units: (column tile t,
+// k chunk c) for t = wave, wave + 8, ... and c over ceil(ldk / 224) chunks.
+// Units are double-buffered in two register sets: the next unit's weight
+// fragments (all its k steps, both planes) are requested before the current
+// unit's MFMAs, so each unit's L2 round trip overlaps the previous unit's
+// MFMAs and epilogue.  A tile's epilogue operands are requested at its first
+// unit, ahead of the next unit's fragments (in-order vmcnt: the epilogue then
+// does not wait for them).
+struct TcUnit {
+  int t, k0, ns;
+  bool first, last;
+};
+__device__ __forceinline__ TcUnit tc_unit(COp& S, int u, int nch) {
+  const int wave = threadIdx.x >> 6;
+  TcUnit x;
+  const int c = u % nch;
+  x.t = wave + TC_NW * (u / nch);
+  x.k0 = 32 * TC_KS * c;
+  x.ns = min(TC_KS, (S.ldk - x.k0) >> 5);
+  x.first = c == 0;
+  x.last = c == nch - 1;
+  return x;
+}
+__device__ __forceinline__ void tc_issue(COp& S, __amdgpu_buffer_rsrc_t rh, __amdgpu_buffer_rsrc_t rl,
+                                         const TcUnit& x, TcFrag& f) {
+  const unsigned vb = tc_frag_base(S, x.t, x.k0);
+#pragma unroll
+  for (int u = 0; u < TC_KS; ++u) tc_fetch_step(rh, rl, vb, u, x.ns, f);
+}
+
+// epilogue operands of tile t: pixels (BERN), forward tanh output (TGRAD),
+// target h of the lane's two latent columns (PRIOR)
+template <int RT, int KIND>
+__device__ __forceinline__ void tc_epi_loads(const TcArgs& A, COp& S, int t, const TcRows<RT>& R, int row0,
+                                             int nrows, float4 (&ov)[RT], float2 (&tv)[RT]) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  const int f0 = t * 16 + 4 * g;
+  if (KIND == TC_BERN) {
+    const __amdgpu_buffer_rsrc_t rx = buf_rsrc(A.x);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) ov[rt] = bld4(rx, f0 < S.N ? R.xoff[rt] + (unsigned)f0 * 4u : kOOB);
+  }
+  if (KIND == TC_TGRAD) {
+    const __amdgpu_buffer_rsrc_t ry = buf_rsrc(S.y);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int row = min(rt * 16 + r, nrows - 1);
+      ov[rt] = bld4(ry, f0 < S.N ? (unsigned)((row0 + row) * S.ld_y + f0) * 4u : kOOB);
+    }
+  }
+  if (KIND == TC_PRIOR) {
+    const __amdgpu_buffer_rsrc_t rh = buf_rsrc(S.h);
+    const int j0 = 4 * (2 * t + (g >> 1)) + 2 * (g & 1);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int row = row0 + min(rt * 16 + r, nrows - 1);
+      tv[rt].x = bld1(rh, j0 < S.d ? (unsigned)(row * S.ld_h + j0) * 4u : kOOB);
+      tv[rt].y = bld1(rh, j0 + 1 < S.d ? (unsigned)(row * S.ld_h + j0 + 1) * 4u : kOOB);
+    }
+  }
+}
+
+template <int RT, int KIND>
+__device__ __forceinline__ void tc_epilogue(const TcArgs& A, COp& S, const TcBuf& OUT, int t, uint64_t base,
+                                            const tc_f32x4 (&acc)[RT], const float4 (&ov)[RT],
+                                            const float2 (&tv)[RT], TcRows<RT>& R, int row0, int nrows) {
+  if (KIND == TC_TANH || KIND == TC_TGRAD || KIND == TC_LIN) tc_store_act<RT, KIND>(S, OUT, t, acc, ov, row0, nrows);
+  else if (KIND == TC_BERN) tc_bern<RT>(A, S, t, acc, ov, R, row0, nrows);
+  else tc_head<RT, KIND>(A, S, OUT, t, base, acc, tv, R, row0, nrows);
+}
+
+// request the first unit of this wave in Dense op S (ahead of the barrier before it)
+__device__ __forceinline__ bool tc_prefetch(COp& S, TcFrag& fa) {
+  const int wave = threadIdx.x >> 6;
+  if (S.kind > TC_LIN || wave >= ((S.N + 15) >> 4)) return false;
+  const __amdgpu_buffer_rsrc_t rh = buf_rsrc(S.Whi, S.W_bytes), rl = buf_rsrc(S.Wlo, S.W_bytes);
+  tc_issue(S, rh, rl, tc_unit(S, 0, (S.ldk + 32 * TC_KS - 1) / (32 * TC_KS)), fa);
+  return true;
+}
+
+// fa: the first unit's register set; pre: its fragments were already requested
+// (by the previous op, tc_prefetch).  Sn: the next op when it is a Dense op
+// whose first unit this op requests -- at its last unit, before that unit's
+// MFMAs and epilogue stores (in-order vmcnt: the next op's wait for them then
+// does not include this op's stores) -- into fa; returns whether it did.
+template <int RT, int KIND>
+__device__ __forceinline__ bool tc_dense(const TcArgs& A, CJob& J, COp& S, uint64_t base,
+                                         TcRows<RT>& R, int row0, int nrows, TcFrag& fa, bool pre, COp* Sn,
+                                         int utr = -1) {
+  const int wave = threadIdx.x >> 6;
+  const int ntile = (S.N + 15) >> 4;
+  if (wave >= ntile) return Sn ? tc_prefetch(*Sn, fa) : false;
+  const int nch = (S.ldk + 32 * TC_KS - 1) / (32 * TC_KS);
+  const int U = ((ntile - 1 - wave) / TC_NW + 1) * nch;
+  const TcBuf IN = tc_buf<RT>(J, S.in_buf);
+  const TcBuf OUT = tc_buf<RT>(J, S.out_buf >= 0 ? S.out_buf : S.in_buf);
+  const __amdgpu_buffer_rsrc_t rh = buf_rsrc(S.Whi, S.W_bytes), rl = buf_rsrc(S.Wlo, S.W_bytes);
+  TcFrag fb;
+  float4 ov[RT];
+  float2 tv[RT];
+  tc_f32x4 acc[RT];
+  bool pn = false;
+  auto step = [&](int u, const TcFrag& cur, TcFrag& nxt) {
+    const TcUnit x = tc_unit(S, u, nch);
+#ifdef IWAE_TC_TRACE
+    const bool st = utr >= 0 && (threadIdx.x & 63) == 0 && u < 16;
+    if (st) g_tc_utrace[(utr * 16 + u) * 3] = wall_clock64();
+#endif
+    if (x.first) {
+      tc_epi_loads<RT, KIND>(A, S, x.t, R, row0, nrows, ov, tv);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt] = (tc_f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    if (u + 1 < U) tc_issue(S, rh, rl, tc_unit(S, u + 1, nch), nxt);
+    else if (Sn) pn = tc_prefetch(*Sn, nxt);
+    tc_mma<RT>(IN, x.k0, x.ns, cur, acc);
+#ifdef IWAE_TC_TRACE
+    if (st) {
+      asm volatile("" ::"v"(acc[0][0]) : "memory");
+      g_tc_utrace[(utr * 16 + u) * 3 + 1] = wall_clock64();
+    }
+#endif
+    if (x.last) tc_epilogue<RT, KIND>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows);
+#ifdef IWAE_TC_TRACE
+    if (st) {
+      asm volatile("" ::"v"(R.l2[0]) : "memory");
+      g_tc_utrace[(utr * 16 + u) * 3 + 2] = wall_clock64();
+    }
+#endif
+  };
+  if (!pre) tc_issue(S, rh, rl, tc_unit(S, 0, nch), fa);
+  for (int u = 0; u < U; u += 2) {
+    step(u, fa, fb);
+    if (u + 1 >= U) break;
+    step(u + 1, fb, fa);
+  }
+  if (pn && (U & 1)) fa = fb;       // the next op's first unit landed in fb
+  return pn;
+}
+
+// Barrier between ops.  LDS only: global stores (activations for the weight
+// gradients, read by later launches) and the next op's prefetched weights stay
+// in flight.  Ops that read global data written earlier in this launch by this
+// workgroup (the prior head's target h, the encoder head's dL/dh sources) get
+// the full __syncthreads (every store of every wave completed first).
+__device__ __forceinline__ bool tc_needs_global(int kind) { return kind == TC_PRIOR || kind == TC_GBWD_ENC; }
+__device__ __forceinline__ void tc_lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// ------------------------------------------------------- elementwise ops
+// Thread t works on row t / TPR, column quads t % TPR, t % TPR + TPR, ...
+
+// h1 = eps * scale + mu of the row's image (Encoder.call F:58-F:60), log q(h1|x)
+// and log N(h1; 0, 1) into the row accumulators, h1 into out_buf (ones column
+// at d, zeros to next_k); h1 / eps stored when S.h is set.
+template <int RT>
+__device__ __forceinline__ void tc_sample0(const TcArgs& A, CJob& J, COp& S, uint64_t base, int row0,
+                                           int nrows, float* rq, float* rp) {
+  constexpr int R = 16 * RT, TPR = (TC_NW * 64) / R;
+  const int t = threadIdx.x, rr = t / TPR, sub = t - rr * TPR;
+  const int d = S.d;
+  const TcBuf H = tc_buf<RT>(J, S.out_buf);
+  const int rg = row0 + min(rr, nrows - 1);
+  const bool st = S.h != nullptr && rr < nrows;
+  const float* Pp = S.P + (size_t)(rg / S.P_div) * S.ld_P;
+  float aq = 0.f, ap = 0.f;
+  for (int gq = sub; 4 * gq < S.next_k; gq += TPR) {
+    float mu[4], zs[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int jc = min(4 * gq + q, d - 1);
+      mu[q] = Pp[jc];
+      zs[q] = Pp[d + jc];
+    }
+    float4 e4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (A.eps_a[S.layer]) {
+      const float2 a = tc_eps2(A, S.layer, d, rg, 4 * gq), b = tc_eps2(A, S.layer, d, rg, 4 * gq + 2);
+      e4 = make_float4(a.x, a.y, b.x, b.y);
+    } else if (4 * gq < d) {
+      e4 = philox_normal4(A.seed, base, (unsigned)rg, (unsigned)S.layer, (unsigned)gq);
+    }
+    float hv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = 4 * gq + q;
+      hv[q] = 0.f;
+      if (j < d) {
+        const float sc = fexp(zs[q]) + kScaleEps;
+        const float e = f4_at(e4, q);
+        hv[q] = e * sc + mu[q];
+        aq += normal_logp(hv[q], mu[q], sc);
+        ap += -0.5f * (hv[q] * hv[q]) - kHalfLog2Pi;
+        if (st) {
+          S.h[(size_t)rg * S.ld_h + j] = hv[q];
+          S.eps[(size_t)rg * S.ld_eps + j] = e;
+        }
+      } else if (j == d) {
+        hv[q] = 1.f;
+      }
+    }
+    tc_put4(H, rr * H.ld + 4 * gq, hv);
+  }
+  for (int o = TPR >> 1; o > 0; o >>= 1) {
+    aq += __shfl_xor(aq, o);
+    ap += __shfl_xor(ap, o);
+  }
+  if (sub == 0 && S.acc) {
+    rq[rr] += aq;
+    if (S.stdnormal) rp[rr] += ap;
+  }
+}
+
+// output-layer backward operand: dpx[row] * g[row][k] for k < N, zero to next_k
+template <int RT>
+__device__ __forceinline__ void tc_loadg(const TcArgs& A, CJob& J, COp& S, int row0, int nrows) {
+  constexpr int R = 16 * RT, TPR = (TC_NW * 64) / R;
+  const int t = threadIdx.x, rr = t / TPR, sub = t - rr * TPR;
+  const TcBuf B = tc_buf<RT>(J, S.out_buf);
+  const int rg = row0 + min(rr, nrows - 1);
+  const float dp = A.dpx[rg];
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(S.y);
+  for (int c4 = sub; 4 * c4 < S.next_k; c4 += TPR) {
+    const int k = 4 * c4;
+    const float4 gv = bld4(rs, k < S.N ? (unsigned)(rg * S.ld_y + k) * 4u : kOOB);
+    float v[4] = {gv.x * dp, gv.y * dp, gv.z * dp, gv.w * dp};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (k + i >= S.N) v[i] = 0.f;
+    tc_put4(B, rr * B.ld + k, v);
+  }
+}
+
+// dP = (dmu | dzs) of a Gaussian head (F:37: scale = exp(zs) + 1e-6) into
+// out_buf (natural order, zeros to next_k) and S.out.
+//   GBWD_PRIOR: log p(h_t | .) with dL/dlogp = dlw: dmu = dl z / s,
+//               dscale = dl (z^2 - 1) / s, and dL/dh_t = -dl z / s (S.dh);
+//   GBWD_ENC:   sampled h = eps s + mu, dL/dlogq = -dlw, G = sum of the dL/dh
+//               sources (+ dlw * d log N(h; 0, 1)/dh for the top layer):
+//               dmu = G + dlq z / s, dscale = G eps + dlq (z^2 - 1) / s.
+template <int RT, int KIND>
+__device__ __forceinline__ void tc_gbwd(const TcArgs& A, CJob& J, COp& S, int row0, int nrows) {
+  constexpr int R = 16 * RT, TPR = (TC_NW * 64) / R;
+  const int t = threadIdx.x, rr = t / TPR, sub = t - rr * TPR;
+  const TcBuf B = tc_buf<RT>(J, S.out_buf);
+  const int d = S.d;
+  for (int c = 2 * d + sub; c < S.next_k; c += TPR) {
+    B.hi[rr * B.ld + c] = (__bf16)0.f;
+    B.lo[rr * B.ld + c] = (__bf16)0.f;
+  }
+  const int rg = row0 + min(rr, nrows - 1);
+  const bool st = rr < nrows;
+  const float dl = A.dlw[rg];
+  const float* Pr = S.P + (size_t)rg * S.ld_P;
+  const float* Hr = S.h + (size_t)rg * S.ld_h;
+  __amdgpu_buffer_rsrc_t rsrc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) rsrc[u] = buf_rsrc(S.src[u]);
+  const __amdgpu_buffer_rsrc_t reps = buf_rsrc(S.eps);
+  for (int gq = sub; 4 * gq < d; gq += TPR) {
+    float mu[4], zs[4], hv[4], ev[4], G[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = min(4 * gq + q, d - 1);
+      mu[q] = Pr[c];
+      zs[q] = Pr[d + c];
+      hv[q] = Hr[c];
+      ev[q] = KIND == TC_GBWD_ENC ? bld1(reps, (unsigned)(rg * S.ld_eps + c) * 4u) : 0.f;
+      G[q] = 0.f;
+      if (KIND == TC_GBWD_ENC) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          G[q] += bld1(rsrc[u], u < S.nsrc ? (unsigned)(rg * S.ld_src[u] + c) * 4u : kOOB);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = 4 * gq + q;
+      if (c >= d) break;
+      const float ez = fexp(zs[q]);
+      const float sc = ez + kScaleEps;
+      const float rs = frcp(sc);
+      const float z = hv[q] * rs - mu[q] * rs;
+      float dmu, dsc;
+      if (KIND == TC_GBWD_PRIOR) {
+        if (st) S.dh[(size_t)rg * S.ld_dh + c] = dl * (-z * rs);
+        dmu = dl * (z * rs);
+        dsc = dl * ((z * z - 1.f) * rs);
+      } else {
+        const float dlq = -dl;
+        float Gq = G[q];
+        if (S.stdnormal) Gq += dl * (-hv[q]);
+        Gq += dlq * (-z * rs);
+        dmu = Gq + dlq * (z * rs);
+        dsc = Gq * ev[q] + dlq * ((z * z - 1.f) * rs);
+      }
+      const float dzs = dsc * ez;
+      tc_put1(B, rr * B.ld + c, dmu);
+      tc_put1(B, rr * B.ld + d + c, dzs);
+      if (st) {
+        S.out[(size_t)rg * S.ld_out + c] = dmu;
+        S.out[(size_t)rg * S.ld_out + d + c] = dzs;
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------- kernel
+template <int RT>
+__global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
+  constexpr int R = 16 * RT;
+  CPlan* plan = (CPlan*)A.plan;
+  int jb = 0;
+  while (jb + 1 < plan->njobs && (int)blockIdx.x >= A.block_start[jb + 1]) ++jb;
+  CJob& J = plan->job[jb];
+  const int row0 = ((int)blockIdx.x - A.block_start[jb]) * R;
+  const int nrows = min(R, A.rows - row0);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  float* rq = tcs + plan->acc_off;
+  float* rp = rq + R;
+  float* red = rp + R;                  // [3][NW][R]
+  if (t < R) { rq[t] = 0.f; rp[t] = 0.f; }
+  const uint64_t base = A.rng_base ? *A.rng_base : 0ull;
+  TcRows<RT> Rw;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int row = min(rt * 16 + (lane & 15), nrows - 1);
+    Rw.q[rt] = 0.f; Rw.p[rt] = 0.f; Rw.l2[rt] = 0.f;
+    Rw.xoff[rt] = (unsigned)((row0 + row) / A.kS) * (unsigned)A.ldx * 4u;
+  }
+#ifdef IWAE_TC_TRACE
+  int tr = -1;
+  if ((int)blockIdx.x == A.block_start[jb] && t == 0) {
+    tr = (int)atomicAdd(&g_tc_trace_n, 1u);
+    if (tr >= 256) tr = -1;
+    else { g_tc_trace[tr * 64] = jb; g_tc_trace[tr * 64 + 1] = wall_clock64(); }
+  }
+#endif
+  __syncthreads();
+  TcFrag fa;              // first-unit fragments of the next Dense op (prefetched across the barrier)
+  bool pre = false, pnext = false;
+#ifdef IWAE_TC_TRACE
+  const int trw = __shfl(tr, 0);       // the traced record, on every lane of wave 0
+#endif
+  for (int s = 0; s < J.nop; ++s) {
+    COp& S = J.op[s];
+    const int kind = S.kind;
+#ifdef IWAE_TC_TRACE
+#define UTR ((trw >= 0 && wave == 0 && s < 8) ? trw * 8 + s : -1)
+#else
+#define UTR -1
+#endif
+#ifdef IWAE_TC_TRACE
+    if (tr >= 0 && 3 + 2 * s < 64) g_tc_trace[tr * 64 + 2 + 2 * s] = wall_clock64();
+#endif
+    // the next op's first weight unit is requested by this op (see tc_dense)
+    COp* Sn = nullptr;
+    if (s + 1 < J.nop && J.op[s + 1].kind <= TC_LIN && !tc_needs_global(J.op[s + 1].kind)) Sn = &J.op[s + 1];
+    pnext = false;
+    if (kind > TC_LIN && Sn) pnext = tc_prefetch(*Sn, fa);   // elementwise op: before its own memory traffic
+    if (kind <= TC_LIN && S.out_buf >= 0) {
+      const int width = kind == TC_SAMPLE ? S.d : S.N;
+      tc_pad<RT>(tc_buf<RT>(J, S.out_buf), width, S.next_k, S.ones != 0);
+    }
+    switch (kind) {      // one instantiation per kind: one epilogue per tile loop
+      case TC_TANH: pnext = tc_dense<RT, TC_TANH>(A, J, S, base, Rw, row0, nrows, fa, pre, Sn, UTR); break;
+      case TC_SAMPLE: pnext = tc_dense<RT, TC_SAMPLE>(A, J, S, base, Rw, row0, nrows, fa, pre, Sn, UTR); break;
+      case TC_PRIOR: pnext = tc_dense<RT, TC_PRIOR>(A, J, S, base, Rw, row0, nrows, fa, pre, Sn, UTR); break;
+      case TC_BERN: pnext = tc_dense<RT, TC_BERN>(A, J, S, base, Rw, row0, nrows, fa, pre, Sn, UTR); break;
+      case TC_TGRAD: pnext = tc_dense<RT, TC_TGRAD>(A, J, S, base, Rw, row0, nrows, fa, pre, Sn, UTR); break;
+      case TC_LIN: pnext = tc_dense<RT, TC_LIN>(A, J, S, base, Rw, row0, nrows, fa, pre, Sn, UTR); break;
+      case TC_SAMPLE0: tc_sample0<RT>(A, J, S, base, row0, nrows, rq, rp); break;
+      case TC_GBWD_PRIOR: tc_gbwd<RT, TC_GBWD_PRIOR>(A, J, S, row0, nrows); break;
+      case TC_GBWD_ENC: tc_gbwd<RT, TC_GBWD_ENC>(A, J, S, row0, nrows); break;
+      default: tc_loadg<RT>(A, J, S, row0, nrows); break;
+    }
+#ifdef IWAE_TC_TRACE
+    if (tr >= 0 && 3 + 2 * s < 64) g_tc_trace[tr * 64 + 3 + 2 * s] = wall_clock64();
+#endif
+    pre = pnext;
+    if (s + 1 < J.nop && !tc_needs_global(J.op[s + 1].kind)) tc_lds_barrier();
+    else __syncthreads();
+  }
+  if (!J.logq && !J.logp && !J.bern) return;
+  // per-row sums: over the 4 lane groups, then over the waves (fixed order)
+  {
+    const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      float v[3] = {Rw.q[rt], Rw.p[rt], Rw.l2[rt]};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        v[k] += __shfl_xor(v[k], 16);
+        v[k] += __shfl_xor(v[k], 32);
+        if (g == 0) red[(k * TC_NW + wave) * R + rt * 16 + r] = v[k];
+      }
+    }
+  }
+  __syncthreads();
+  if (t < nrows) {
+    float s3[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int w = 0; w < TC_NW; ++w) s3[k] += red[(k * TC_NW + w) * R + t];
+    const int rg = row0 + t;
+    if (J.logq) J.logq[rg] = rq[t] + s3[0];
+    if (J.logp) J.logp[rg] = rp[t] + s3[1];
+    if (J.bern) *reinterpret_cast<float4*>(J.bern + (size_t)rg * J.ld_bern) = make_float4(kLn2 * s3[2], 0.f, 0.f, 0.f);
+  }
+}
+
+hipError_t launch_tc(hipStream_t st, const TcArgs& a, int rt, size_t lds_bytes) {
+  const int nb = a.block_start[kTcMaxJobs];
+  if (nb <= 0) return hipSuccess;
+  switch (rt) {
+    case 1: hipLaunchKernelGGL((tc_kernel<1>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a); break;
+    case 2: hipLaunchKernelGGL((tc_kernel<2>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a); break;
+    case 4: hipLaunchKernelGGL((tc_kernel<4>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t tc_setup_attributes() {
+  const void* fns[] = {(const void*)tc_kernel<1>, (const void*)tc_kernel<2>, (const void*)tc_kernel<4>};
+  for (const void* f : fns) {
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace iwae
+
+#ifdef IWAE_TC_TRACE
+extern "C" int iwae_tc_utrace_dump(unsigned long long* out, int cap) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  const int n = 256 * 8 * 16 * 3 < cap ? 256 * 8 * 16 * 3 : cap;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(iwae::g_tc_utrace), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+  return n;
+}
+extern "C" int iwae_tc_trace_dump(unsigned long long* out, int cap) {
+  unsigned n = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(iwae::g_tc_trace_n), sizeof(n)) != hipSuccess) return -1;
+  n = n > 256u ? 256u : n;
+  const int m = (int)n * 64 < cap ? (int)n * 64 : cap;
+  if (m > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(iwae::g_tc_trace), m * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  unsigned zero = 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(iwae::g_tc_trace_n), &zero, sizeof(zero));
+  return m;
+}
+#endif

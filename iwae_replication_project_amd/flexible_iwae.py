@@ -202,7 +202,7 @@ class Flexible_Model:
             seed = int.from_bytes(os.urandom(8), "little")
         self._call(self._lib.iwae_set_seed(h, int(seed) & ((1 << 64) - 1)))
         self._call(self._lib.iwae_set_graphs(h, 1 if use_graphs else 0))
-        paths = {"auto": 0, "layerwise": 1, "fused": 2}
+        paths = {"auto": 0, "layerwise": 1, "fused": 2, "engine": 3}
         if kernel_path not in paths:
             raise ValueError(f"kernel_path must be one of {tuple(paths)}")
         self._call(self._lib.iwae_set_path(h, paths[kernel_path]))

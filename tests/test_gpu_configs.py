@@ -61,15 +61,20 @@ def _run(arch, loss, B, k, seed, **kw):
         okw["eps2"] = draws[1]
     opt = O.Adam(1e-3, 0.9, 0.999, 1e-4)
     ref_loss, ref_new, ref_g = O.train_step(params, spec, x, draws[0], loss, k, opt, **okw)
-    return loss_gpu, ref_loss, _flat(m.get_gradients()), ref_g, _flat(m.get_weights()), \
-        O.flatten_params(spec, ref_new)
+    g = _flat(m.get_gradients())
+    w0 = O.flatten_params(spec, params)
+    return loss_gpu, ref_loss, g, ref_g, _flat(m.get_weights()), O.flatten_params(spec, ref_new), \
+        O.Adam(1e-3, 0.9, 0.999, 1e-4).apply(w0, g)
 
 
-def _check(res, wtol=ADAM_ATOL):
-    loss, ref_loss, g, ref_g, w, ref_w = res
+def _check(res):
+    loss, ref_loss, g, ref_g, w, ref_w, w_from_g = res
     assert abs(loss - ref_loss) <= REL * abs(ref_loss), (loss, ref_loss)
     assert _rel_l2(g, ref_g) <= REL, _rel_l2(g, ref_g)
-    np.testing.assert_allclose(w, ref_w, atol=wtol)
+    # Adam on the device == Adam applied to the device gradient; against the oracle's
+    # weights within 10x the gradient error (lr/eps = 10 amplification at step 1)
+    np.testing.assert_allclose(w, w_from_g, atol=2e-6)
+    np.testing.assert_allclose(w, ref_w, atol=max(ADAM_ATOL, 10 * np.abs(g - ref_g).max()))
 
 
 C0_LOSSES = [("VAE", {}), ("IWAE", {}), ("VAE_V1", {}), ("L_alpha", dict(alpha=0.5)),

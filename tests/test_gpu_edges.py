@@ -56,8 +56,15 @@ def test_ragged_batches_match_oracle(B, k):
     opt = O.Adam(1e-3, 0.9, 0.999, 1e-4)
     ref_loss, ref_new, ref_g = O.train_step(params, spec, x, eps, "IWAE", k, opt)
     assert abs(loss - ref_loss) <= REL * abs(ref_loss), (loss, ref_loss)
-    assert _rel_l2(_flat(m.get_gradients()), ref_g) <= REL
-    np.testing.assert_allclose(_flat(m.get_weights()), O.flatten_params(spec, ref_new), atol=ADAM_ATOL)
+    g = _flat(m.get_gradients())
+    assert _rel_l2(g, ref_g) <= REL
+    # the device Adam step is exactly Adam (E:36-E:40) applied to the device gradient; the
+    # weights then follow the oracle's within 10x the gradient error (lr/eps = 10 bounds
+    # d(update)/dg at step 1: near-zero gradient elements amplify their rounding)
+    w0 = O.flatten_params(spec, params)
+    np.testing.assert_allclose(_flat(m.get_weights()), O.Adam(1e-3, 0.9, 0.999, 1e-4).apply(w0, g), atol=2e-6)
+    np.testing.assert_allclose(_flat(m.get_weights()), O.flatten_params(spec, ref_new),
+                               atol=max(ADAM_ATOL, 10 * np.abs(g - ref_g).max()))
 
 
 def test_k1_iwae_equals_vae():

@@ -170,18 +170,24 @@ def test_c2_full_size_iwae_train_step_matches_oracle():
     np.testing.assert_allclose(flat(m.get_weights()), O.flatten_params(spec, ref_new), atol=ADAM_ATOL)
 
 
-@pytest.mark.parametrize("loss", ["IWAE", "CIWAE", "PIWAE", "VAE_V1", "L_alpha", "L_median"])
+@pytest.mark.parametrize("path", ["fused", "engine"])
+@pytest.mark.parametrize("loss", ["IWAE", "VAE", "CIWAE", "PIWAE", "VAE_V1", "L_alpha", "L_median", "MIWAE",
+                                  "L_power_p"])
 @pytest.mark.parametrize("arch", [([64], [64], [16], [784]), ([64, 32], [32, 64], [32, 16], [32, 784]),
                                   ([48, 32, 24], [24, 32, 48], [20, 12, 8], [12, 20, 784])])
-def test_fused_and_layerwise_paths_agree(arch, loss):
-    """The fused row-block kernels and the layer-wise GEMM kernels compute the
-    same train step (same Philox noise): loss, gradients and updated weights."""
+def test_fused_and_layerwise_paths_agree(arch, loss, path):
+    """The fused row-block kernels / the bf16x3 row-chain engine and the
+    layer-wise GEMM kernels compute the same train step (same Philox noise):
+    loss, gradients and updated weights.  (The engine runs every loss but
+    VAE_V1 / L_alpha / PIWAE; those take the fused kernels under "engine".)"""
     he, hd, le, ld = arch
     rng = np.random.default_rng(19)
     x = (rng.random((9, 784)) < 0.2).astype(np.float32)
-    kw = dict(k1=3, k2=2) if loss == "PIWAE" else {}
+    kw = dict(k1=3, k2=2) if loss in ("PIWAE", "MIWAE") else {}
+    if loss == "L_power_p":
+        kw["p"] = 2.0
     outs = []
-    for path in ("layerwise", "fused"):
+    for path in ("layerwise", path):
         from iwae_replication_project_amd import Adam
         m = make_model(he, hd, le, ld, loss=loss, k=6, seed=77, kernel_path=path, alpha=0.4, beta=0.3, **kw)
         m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
