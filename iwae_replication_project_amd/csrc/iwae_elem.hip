@@ -344,21 +344,26 @@ __device__ ImgBound image_bound(const BoundArgs& a, int mode, const LwView& lw) 
   return o;
 }
 
-// coef * dBound/dlw written to out[row0 + q]
+// coef * dBound/dlw written to out[row0 + q] (and to out2 when given: no
+// store-then-reload of out)
 __device__ __forceinline__ void image_grad(const BoundArgs& a, int mode, int row0, const ImgBound& ib,
-                                           float coef, const LwView& lw, float* out) {
+                                           float coef, const LwView& lw, float* out, float* out2 = nullptr) {
   const int lane = threadIdx.x & 63;
   const int kS = a.kS;
+  auto put = [&](int i, float v) {
+    out[i] = v;
+    if (out2) out2[i] = v;
+  };
   if (mode == BM_NONE) {
-    for (int q = lane; q < kS; q += 64) out[row0 + q] = 0.f;
+    for (int q = lane; q < kS; q += 64) put(row0 + q, 0.f);
   } else if (mode == BM_VAE) {
-    for (int q = lane; q < kS; q += 64) out[row0 + q] = coef / (float)kS;
+    for (int q = lane; q < kS; q += 64) put(row0 + q, coef / (float)kS);
   } else if (mode == BM_IWAE || mode == BM_POWER) {
     const float pp = mode == BM_POWER ? a.p : 1.f;
-    for (int q = lane; q < kS; q += 64) out[row0 + q] = coef * (expf((lw(q) - ib.mx) * pp) / ib.se);
+    for (int q = lane; q < kS; q += 64) put(row0 + q, coef * (expf((lw(q) - ib.mx) * pp) / ib.se));
   } else if (mode == BM_MEDIAN) {
     for (int q = lane; q < kS; q += 64)
-      out[row0 + q] = coef * (0.5f * (q == ib.lo) + 0.5f * (q == ib.hi));
+      put(row0 + q, coef * (0.5f * (q == ib.lo) + 0.5f * (q == ib.hi)));
   } else {  // MIWAE
     for (int j = 0; j < a.k2; ++j) {
       const int g0 = j * a.k1;
@@ -369,7 +374,7 @@ __device__ __forceinline__ void image_grad(const BoundArgs& a, int mode, int row
       for (int i = lane; i < a.k1; i += 64) se += expf(lw.sh[g0 + i] - mx);
       se = wave_sum(se);
       for (int i = lane; i < a.k1; i += 64)
-        out[row0 + g0 + i] = coef * (expf(lw.sh[g0 + i] - mx) / se) / (float)a.k2;
+        put(row0 + g0 + i, coef * (expf(lw.sh[g0 + i] - mx) / se) / (float)a.k2);
     }
   }
 }
@@ -413,19 +418,13 @@ __global__ __launch_bounds__(kBoundWaves * 64) void bound_kernel(BoundArgs a) {
     }
     if (a.dlw) {
       // loss = -objective: dL/dlw = -(w/Bg) * dBound/dlw
-      image_grad(a, mode, row0, ib, -w / (float)Bg, lwv, a.dlw);
-      if (a.dpx) {
-        for (int q = lane; q < a.kS; q += 64) {
-          const int r = row0 + q;
-          a.dpx[r] = a.dpx_is_const ? a.dpx_const : a.dlw[r];
-        }
-      }
+      image_grad(a, mode, row0, ib, -w / (float)Bg, lwv, a.dlw, a.dpx_is_const ? nullptr : a.dpx);
+      if (a.dpx && a.dpx_is_const)
+        for (int q = lane; q < a.kS; q += 64) a.dpx[row0 + q] = a.dpx_const;
     }
     if (a.dlw2) {
       const ImgBound ib2 = image_bound(a, a.mode2, lwv);
-      image_grad(a, a.mode2, row0, ib2, -w / (float)Bg, lwv, a.dlw2);
-      if (a.dpx2)
-        for (int q = lane; q < a.kS; q += 64) a.dpx2[row0 + q] = a.dlw2[row0 + q];
+      image_grad(a, a.mode2, row0, ib2, -w / (float)Bg, lwv, a.dlw2, a.dpx2);
     }
   }
   bool finalize;
@@ -721,14 +720,18 @@ hipError_t launch_wsplit(hipStream_t st, const WSplitArgs& a, long long max_seg_
 // One thread = one lane's 8 consecutive k of one fragment (see FxSeg):
 // 8 f32 parameters in, 16 bytes per plane out (consecutive threads write
 // consecutive 16-byte chunks).
+// Segments start at multiples of 256 threads: the segment is found per
+// workgroup with scalar loads (a per-lane search would be a chain of dependent
+// vector loads of the argument table).
 __global__ __launch_bounds__(256) void fx_refresh_kernel(FxArgs a) {
-  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.total) return;
+  const long long c0 = (long long)blockIdx.x * blockDim.x;
   int s = 0;
-  while (s + 1 < a.nseg && c >= a.seg[s + 1].start) ++s;
+  while (s + 1 < a.nseg && c0 >= a.seg[s + 1].start) ++s;
   const FxSeg& g = a.seg[s];
-  long long q = c - g.start;
+  long long q = c0 + threadIdx.x - g.start;
   const long long nfx = (long long)g.fx_tiles * g.fx_steps * 64;
+  const long long ngx = (long long)g.gx_tiles * g.gx_steps * 64;
+  if (q >= nfx + ngx) return;       // the segment's alignment pad
   const bool fwd = q < nfx;
   if (!fwd) q -= nfx;
   const int steps = fwd ? g.fx_steps : g.gx_steps;

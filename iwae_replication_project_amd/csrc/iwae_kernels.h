@@ -462,7 +462,7 @@ enum TcKind {
   TC_GBWD_ENC = 8,   // dP of an encoder sampling head from the dL/dh sources
   TC_LOADG = 9       // B operand = dpx[row] * g[row][:] (output layer backward)
 };
-constexpr int kTcMaxOps = 20, kTcMaxBufs = 12, kTcMaxJobs = 2;
+constexpr int kTcMaxOps = 20, kTcMaxBufs = 12, kTcMaxJobs = 3;
 struct TcOp {
   int kind;
   const __bf16* Whi; const __bf16* Wlo; unsigned W_bytes; int ldk, K, N;   // dense ops: split rows [.][ldk]
@@ -478,11 +478,12 @@ struct TcOp {
   const float* P; int ld_P; int P_div;   // SAMPLE0: image P0 (row / P_div); GBWD_*: head P
   const float* src[4]; int ld_src[4]; int nsrc;   // GBWD_ENC: dL/dh sources summed
   float* dh; int ld_dh;       // GBWD_PRIOR: dL/dh of the target h
+  int t0;                     // dense ops: first column tile (a job may run a column range [16 t0, N))
 };
 struct TcJob {
   TcOp op[kTcMaxOps]; int nop;
   int buf_off[kTcMaxBufs], buf_ld[kTcMaxBufs];   // bf16 offset of the hi plane / row stride
-  float* logq; float* logp; float* bern; int ld_bern;   // per-row sums this job writes (null: none)
+  float* logq; float* logp; float* bern; int ld_bern, bern_col;   // per-row sums this job writes (null: none)
 };
 struct TcPlan {              // device resident (built once per shape)
   TcJob job[kTcMaxJobs]; int njobs;

@@ -154,7 +154,7 @@ struct iwae_handle {
   // row-chain train engine plans (device resident, per shape; iwae_train.hip)
   struct TcRec {
     TcPlan* dev = nullptr;
-    int rt = 1, nb[kTcMaxJobs] = {0, 0};
+    int rt = 1, nb[kTcMaxJobs] = {};
     size_t lds = 0;
     double flop = 0.0;               // algorithmic FLOPs of one launch (weight products, no bias rows)
   };
@@ -671,7 +671,7 @@ static int run_bound(iwae_handle* h, const Plan& P, bool train, float sign, floa
   BoundArgs b{};
   b.part = h->part; b.part2 = P.need_bce ? h->part2 : nullptr; b.ldpart = h->ldpart; b.npart = h->npart;
   b.logp = h->logp; b.logq = h->logq;
-  if (engine) { b.part = h->ebern; b.ldpart = 4; b.npart = 1; b.part2 = nullptr; }   // row totals
+  if (engine) { b.part = h->ebern; b.ldpart = 4; b.npart = 1; b.part2 = nullptr; }   // row totals (cols 0-1 summed)
   b.lw = h->lw; b.contrib = h->contrib;
   b.dlw = train ? h->dlw : nullptr; b.dpx = train ? h->dpx : nullptr;
   b.dlw2 = (train && P.piwae) ? h->dlw2 : nullptr; b.dpx2 = (train && P.piwae) ? h->dpx2 : nullptr;
@@ -803,8 +803,8 @@ static int run_fx(iwae_handle* h) {
     g.off = d.off; g.fin = d.fin; g.fout = d.fout; g.ldw = d.ldw;
     g.fx_off = d.fx_off; g.fx_tiles = d.fx_tiles; g.fx_steps = d.fx_steps; g.head_d = d.head_d;
     g.gx_off = d.gx_off; g.gx_tiles = d.gx_tiles; g.gx_steps = d.gx_steps;
-    g.start = tot;
-    tot += ((long long)d.fx_tiles * d.fx_steps + (long long)d.gx_tiles * d.gx_steps) * 64;
+    g.start = tot;      // block aligned: a workgroup never straddles two segments
+    tot += ((((long long)d.fx_tiles * d.fx_steps + (long long)d.gx_tiles * d.gx_steps) * 64 + 255) / 256) * 256;
   }
   a.total = tot;
   HIPCHK(launch_fx_refresh(h->stream, a));
@@ -1421,23 +1421,34 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
       B.J.logq = h->logq; B.J.logp = h->logp;
       jobs.push_back(B);
     }
-    // job O: h1 again (same draw), output MLP, Bernoulli
-    {
+    // jobs O1, O2: h1 again (same draw), output MLP, Bernoulli over a column
+    // range each (the 784-wide output layer is the chain's longest op: both jobs
+    // recompute the two 200-wide layers, O1 alone stores them)
+    const int ntile = (h->dense[h->o3].fout + 15) / 16;
+    const int nsplit = ntile >= 16 ? 2 : 1;
+    for (int part = 0; part < nsplit; ++part) {
+      const bool first = part == 0;
       TcBuild B;
       TcOp& s0 = B.add(TC_SAMPLE0);
-      s0.d = h->enc[0].d; s0.layer = 0; s0.acc = L == 1; s0.stdnormal = L == 1;
+      s0.d = h->enc[0].d; s0.layer = 0; s0.acc = L == 1 && first; s0.stdnormal = L == 1;
       s0.P = h->eb[0].P.p; s0.ld_P = h->eb[0].P.ld; s0.P_div = kS;
-      if (L == 1) { s0.h = h->h[0].p; s0.ld_h = h->h[0].ld; s0.eps = h->eps_st[0].p; s0.ld_eps = h->eps_st[0].ld; }
+      if (L == 1 && first) {
+        s0.h = h->h[0].p; s0.ld_h = h->h[0].ld; s0.eps = h->eps_st[0].p; s0.ld_eps = h->eps_st[0].ld;
+      }
       s0.out_buf = 0; s0.next_k = ldF(h->o1);
       B.need(0, s0.next_k);
       TcOp& a = tc_dense_op(h, B, TC_TANH, h->o1, false, 0, 1, ldF(h->o2));
-      a.out = h->ob.y1.p; a.ld_out = h->ob.y1.ld;
+      if (first) { a.out = h->ob.y1.p; a.ld_out = h->ob.y1.ld; }
       TcOp& b = tc_dense_op(h, B, TC_TANH, h->o2, false, 1, 2, ldF(h->o3));
-      b.out = h->ob.y2.p; b.ld_out = h->ob.y2.ld;
+      if (first) { b.out = h->ob.y2.p; b.ld_out = h->ob.y2.ld; }
       TcOp& c = tc_dense_op(h, B, TC_BERN, h->o3, false, 2, -1, 0);
       c.out = h->ob.P.p; c.ld_out = h->ob.P.ld;
-      B.J.bern = h->ebern; B.J.ld_bern = 4;
-      if (L == 1) { B.J.logq = h->logq; B.J.logp = h->logp; }
+      // tiles [t0, t1): t1 caps N (whole tiles), t0 offsets each wave's first tile
+      const int t0 = part * (ntile / nsplit), t1 = part + 1 == nsplit ? ntile : (part + 1) * (ntile / nsplit);
+      c.t0 = t0;
+      if (t1 < ntile) c.N = 16 * t1;
+      B.J.bern = h->ebern; B.J.ld_bern = 4; B.J.bern_col = part;
+      if (L == 1 && first) { B.J.logq = h->logq; B.J.logp = h->logp; }
       jobs.push_back(B);
     }
   } else {
@@ -1617,6 +1628,8 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   CHK(tc_run(h, P, E, 0));
   CHK(run_bound(h, P, true, -1.f, train_loss_ptr(h), adam, true));
   CHK(tc_run(h, P, E, 1));
+  // (a second stream for the first encoder layer's backward beside the other
+  // weight gradients measured slower inside the captured graph: sequential)
   CHK(fused_encoder_bwd(h, P, h->dlw, 0));
   CHK(weight_grads(h, P, true, true, h->dpx));
   CHK(finish_step(h, P, adam));

@@ -52,6 +52,7 @@ __device__ unsigned long long g_tc_trace[256 * 64];
 __device__ unsigned g_tc_trace_n;
 // per-unit stamps of wave 0 of the traced workgroups: [rec][op < 8][unit < 16][3]
 __device__ unsigned long long g_tc_utrace[256 * 8 * 16 * 3];
+__device__ unsigned long long g_tc_ptrace[256 * 32 * 4];     // per op: kind read, after pad, dense entry
 __device__ int tc_tr_rec = -1, tc_tr_op = 0;   // (set per workgroup in registers; see tc_kernel)
 #endif
 
@@ -64,6 +65,19 @@ __device__ int tc_tr_rec = -1, tc_tr_op = 0;   // (set per workgroup in register
 typedef const TC_CONST TcOp COp;
 typedef const TC_CONST TcJob CJob;
 typedef const TC_CONST TcPlan CPlan;
+typedef const TC_CONST uint32_t CU32;
+
+// Touch every 64-byte line of the job's descriptors once at kernel start: the
+// scalar-cache misses then overlap each other instead of stalling each op's
+// prologue on its own descriptor lines (one L2 round trip per op otherwise).
+__device__ __forceinline__ void tc_warm_descriptors(CJob& J) {
+  constexpr int kLines = (int)(sizeof(TcJob) / 64);
+  CU32* p = (CU32*)&J;
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < kLines; ++i) x ^= p[16 * i];
+  asm volatile("" ::"s"(x));
+}
 
 struct TcBuf {
   __bf16* hi; __bf16* lo; int ld;
@@ -108,6 +122,9 @@ __device__ __forceinline__ void tc_pad(const TcBuf& B, int width, int next_k, bo
   }
 }
 
+// wave index as a scalar (wave-uniform branches stay scalar branches)
+__device__ __forceinline__ int tc_wave() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 struct TcFrag {
   tc_bf16x8 h[TC_KS], l[TC_KS];
 };
@@ -127,22 +144,38 @@ __device__ __forceinline__ unsigned tc_frag_base(COp& S, int t, int k0) {
   const int ntile = (S.N + 15) >> 4;
   return t < ntile ? (unsigned)(((t * (S.ldk >> 5) + (k0 >> 5)) * 64 + lane) * 16) : kOOB;
 }
+// every register of the set is written (k steps past ns read zeros out of
+// range): a set is never partially live across units
 __device__ __forceinline__ void tc_fetch_step(__amdgpu_buffer_rsrc_t rh, __amdgpu_buffer_rsrc_t rl, unsigned vb,
                                               int u, int ns, TcFrag& f) {
-  if (u >= ns) return;
-  f.h[u] = tc_as_bf16x8(__builtin_amdgcn_raw_buffer_load_b128(rh, vb, 1024 * u, 0));
-  f.l[u] = tc_as_bf16x8(__builtin_amdgcn_raw_buffer_load_b128(rl, vb, 1024 * u, 0));
+  const unsigned v = u < ns ? vb : kOOB;
+#ifdef IWAE_TC_NOLOAD      // timing experiment only: no weight traffic
+  f.h[u] = tc_as_bf16x8((tc_u32x4){v, 0u, 0u, 0u});
+  f.l[u] = tc_as_bf16x8((tc_u32x4){0u, v, 0u, 0u});
+#else
+  f.h[u] = tc_as_bf16x8(__builtin_amdgcn_raw_buffer_load_b128(rh, v, 1024 * u, 0));
+  f.l[u] = tc_as_bf16x8(__builtin_amdgcn_raw_buffer_load_b128(rl, v, 1024 * u, 0));
+#endif
 }
 
 // acc[rt] += W-tile . IN[rows of rt][k0 .. k0 + 32 ns) (bf16x3)
 template <int RT>
 __device__ __forceinline__ void tc_mma(const TcBuf& IN, int k0, int ns, const TcFrag& f, tc_f32x4 (&acc)[RT]) {
+#ifdef IWAE_TC_NOMMA       // timing experiment only
+  acc[0][0] += (float)f.h[0][0] + (float)f.l[TC_KS - 1][7];
+  return;
+#endif
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
   constexpr int RH = RT < 2 ? RT : 2;
   constexpr int NP = RT / RH;
   constexpr int NC = TC_KS * NP;
   tc_bf16x8 ah[2][RH], al[2][RH];
+  // two accumulator chains (the hi x hi products; the two cross terms): the
+  // dependent MFMA chain of a unit is half as long
+  tc_f32x4 lo[RT];
+#pragma unroll
+  for (int i = 0; i < RT; ++i) lo[i] = (tc_f32x4){0.f, 0.f, 0.f, 0.f};
   auto rd = [&](int c, int b) {
     const int u = c / NP, p = c % NP;
 #pragma unroll
@@ -160,14 +193,16 @@ __device__ __forceinline__ void tc_mma(const TcBuf& IN, int k0, int ns, const Tc
     if (c + 1 < NC && (c + 1) / NP < ns) rd(c + 1, b ^ 1);
 #pragma unroll
     for (int i = 0; i < RH; ++i)
-      acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.l[u], ah[b][i], acc[p * RH + i], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < RH; ++i)
-      acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], al[b][i], acc[p * RH + i], 0, 0, 0);
+      lo[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.l[u], ah[b][i], lo[p * RH + i], 0, 0, 0);
 #pragma unroll
     for (int i = 0; i < RH; ++i)
       acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], ah[b][i], acc[p * RH + i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < RH; ++i)
+      lo[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], al[b][i], lo[p * RH + i], 0, 0, 0);
   }
+#pragma unroll
+  for (int i = 0; i < RT; ++i) acc[i] += lo[i];
 }
 
 // per-lane row state: log q / log p partial sums (natural log), the Bernoulli
@@ -386,10 +421,10 @@ struct TcUnit {
   bool first, last;
 };
 __device__ __forceinline__ TcUnit tc_unit(COp& S, int u, int nch) {
-  const int wave = threadIdx.x >> 6;
+  const int wave = tc_wave();
   TcUnit x;
   const int c = u % nch;
-  x.t = wave + TC_NW * (u / nch);
+  x.t = S.t0 + wave + TC_NW * (u / nch);
   x.k0 = 32 * TC_KS * c;
   x.ns = min(TC_KS, (S.ldk - x.k0) >> 5);
   x.first = c == 0;
@@ -445,58 +480,115 @@ __device__ __forceinline__ void tc_epilogue(const TcArgs& A, COp& S, const TcBuf
   else tc_head<RT, KIND>(A, S, OUT, t, base, acc, tv, R, row0, nrows);
 }
 
-// request the first unit of this wave in Dense op S (ahead of the barrier before it)
-__device__ __forceinline__ bool tc_prefetch(COp& S, TcFrag& fa) {
-  const int wave = threadIdx.x >> 6;
-  if (S.kind > TC_LIN || wave >= ((S.N + 15) >> 4)) return false;
-  const __amdgpu_buffer_rsrc_t rh = buf_rsrc(S.Whi, S.W_bytes), rl = buf_rsrc(S.Wlo, S.W_bytes);
-  tc_issue(S, rh, rl, tc_unit(S, 0, (S.ldk + 32 * TC_KS - 1) / (32 * TC_KS)), fa);
-  return true;
+// Weight-fragment pipeline.  Four register sets with fixed roles: X holds
+// unit 0 of a Dense op, Y unit 1, A / B units 2, 3, 4, ... alternately.  Unit
+// u + 2 is requested at unit u; once unit 0 (1) has been multiplied, X (Y)
+// receives the next Dense op's unit 0 (1), so the next op's first units are in
+// flight for nearly the whole of this op, its epilogues and the barrier.
+// Every set is addressed statically and always rewritten whole: no register
+// copy of a set with loads in flight (that would wait for every outstanding
+// load and store of the wave).
+struct TcSets {
+  TcFrag X, Y, A, B;
+};
+struct TcStream {          // the units of one Dense op for this wave
+  __amdgpu_buffer_rsrc_t rh, rl;
+  int nch, U;
+};
+__device__ __forceinline__ TcStream tc_stream(COp& S) {
+  const int wave = tc_wave();
+  TcStream q;
+  const int ntile = (S.N + 15) >> 4;
+  q.nch = (S.ldk + 32 * TC_KS - 1) / (32 * TC_KS);
+  q.U = S.t0 + wave < ntile ? ((ntile - 1 - S.t0 - wave) / TC_NW + 1) * q.nch : 0;
+  q.rh = buf_rsrc(S.Whi, S.W_bytes);
+  q.rl = buf_rsrc(S.Wlo, S.W_bytes);
+  return q;
+}
+// request unit u of op S (past its end: out-of-range loads, the set is still
+// rewritten whole)
+__device__ __forceinline__ void tc_issue_u(COp& S, const TcStream& q, int u, TcFrag& f) {
+  const bool own = u < q.U;
+  const TcUnit x = tc_unit(S, own ? u : 0, q.nch);
+  const unsigned vb = own ? tc_frag_base(S, x.t, x.k0) : kOOB;
+#pragma unroll
+  for (int k = 0; k < TC_KS; ++k) tc_fetch_step(q.rh, q.rl, vb, k, own ? x.ns : 0, f);
+}
+// an elementwise op requests the first two units of the next Dense op Sn
+__device__ __forceinline__ int tc_prefetch(COp& Sn, TcSets& F) {
+  const TcStream qn = tc_stream(Sn);
+  if (qn.U > 0) tc_issue_u(Sn, qn, 0, F.X);
+  if (qn.U > 1) tc_issue_u(Sn, qn, 1, F.Y);
+  return min(2, qn.U);
 }
 
-// fa: the first unit's register set; pre: its fragments were already requested
-// (by the previous op, tc_prefetch).  Sn: the next op when it is a Dense op
-// whose first unit this op requests -- at its last unit, before that unit's
-// MFMAs and epilogue stores (in-order vmcnt: the next op's wait for them then
-// does not include this op's stores) -- into fa; returns whether it did.
-template <int RT, int KIND>
-__device__ __forceinline__ bool tc_dense(const TcArgs& A, CJob& J, COp& S, uint64_t base,
-                                         TcRows<RT>& R, int row0, int nrows, TcFrag& fa, bool pre, COp* Sn,
-                                         int utr = -1) {
-  const int wave = threadIdx.x >> 6;
-  const int ntile = (S.N + 15) >> 4;
-  if (wave >= ntile) return Sn ? tc_prefetch(*Sn, fa) : false;
-  const int nch = (S.ldk + 32 * TC_KS - 1) / (32 * TC_KS);
-  const int U = ((ntile - 1 - wave) / TC_NW + 1) * nch;
+// One Dense op (any kind: the fragment pipeline is one piece of code, only the
+// epilogue switches on the kind).  npre: how many of the op's first units (in
+// X, Y) the previous op already requested; Sn: the next op when it is a Dense
+// op whose first units this op requests.  Returns the next op's npre.
+template <int RT>
+__device__ __forceinline__ int tc_dense(const TcArgs& A, CJob& J, COp& S, const int kind, uint64_t base,
+                                        TcRows<RT>& R, int row0, int nrows, TcSets& F, int npre, COp* Sn,
+                                        int utr = -1) {
+#ifdef IWAE_TC_SKIPDENSE  // timing experiment only
+  return 0;
+#endif
+  const TcStream q = tc_stream(S);
+  TcStream qn;
+  if (Sn) qn = tc_stream(*Sn);
+  else { qn.U = 0; qn.nch = 1; qn.rh = qn.rl = q.rh; }
+  const int U = q.U, Un = min(2, qn.U);
   const TcBuf IN = tc_buf<RT>(J, S.in_buf);
   const TcBuf OUT = tc_buf<RT>(J, S.out_buf >= 0 ? S.out_buf : S.in_buf);
-  const __amdgpu_buffer_rsrc_t rh = buf_rsrc(S.Whi, S.W_bytes), rl = buf_rsrc(S.Wlo, S.W_bytes);
-  TcFrag fb;
+  if (npre < 1 && U > 0) tc_issue_u(S, q, 0, F.X);
+  if (npre < 2 && U > 1) tc_issue_u(S, q, 1, F.Y);
+  if (U <= 1 && Un > 1) tc_issue_u(*Sn, qn, 1, F.Y);     // Y is not used by this op
+  if (U == 0 && Un > 0) tc_issue_u(*Sn, qn, 0, F.X);
   float4 ov[RT];
   float2 tv[RT];
   tc_f32x4 acc[RT];
-  bool pn = false;
-  auto step = [&](int u, const TcFrag& cur, TcFrag& nxt) {
-    const TcUnit x = tc_unit(S, u, nch);
+#ifdef IWAE_TC_TRACE
+  if (utr >= 0 && (threadIdx.x & 63) == 0) g_tc_ptrace[((utr >> 3) * 32 + (utr & 7)) * 4 + 2] = wall_clock64();
+#endif
+  // step u < 2: request unit u + 2 (into A / B), multiply unit u (in X / Y),
+  // hand X / Y over to the next op's unit u.  Step u >= 2: multiply unit u (in
+  // A / B), then request unit u + 2 into the same set.
+  auto step = [&](int u, TcFrag& cur, TcFrag& nxt, bool handover) {
+    const TcUnit x = tc_unit(S, u, q.nch);
 #ifdef IWAE_TC_TRACE
     const bool st = utr >= 0 && (threadIdx.x & 63) == 0 && u < 16;
     if (st) g_tc_utrace[(utr * 16 + u) * 3] = wall_clock64();
 #endif
     if (x.first) {
-      tc_epi_loads<RT, KIND>(A, S, x.t, R, row0, nrows, ov, tv);
+      switch (kind) {
+        case TC_BERN: tc_epi_loads<RT, TC_BERN>(A, S, x.t, R, row0, nrows, ov, tv); break;
+        case TC_TGRAD: tc_epi_loads<RT, TC_TGRAD>(A, S, x.t, R, row0, nrows, ov, tv); break;
+        case TC_PRIOR: tc_epi_loads<RT, TC_PRIOR>(A, S, x.t, R, row0, nrows, ov, tv); break;
+        default: break;
+      }
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) acc[rt] = (tc_f32x4){0.f, 0.f, 0.f, 0.f};
     }
-    if (u + 1 < U) tc_issue(S, rh, rl, tc_unit(S, u + 1, nch), nxt);
-    else if (Sn) pn = tc_prefetch(*Sn, nxt);
+    if (handover && u + 2 < U) tc_issue_u(S, q, u + 2, nxt);
     tc_mma<RT>(IN, x.k0, x.ns, cur, acc);
+    if (handover && u < Un) tc_issue_u(*Sn, qn, u, cur);
+    if (!handover && u + 2 < U) tc_issue_u(S, q, u + 2, cur);
 #ifdef IWAE_TC_TRACE
     if (st) {
       asm volatile("" ::"v"(acc[0][0]) : "memory");
       g_tc_utrace[(utr * 16 + u) * 3 + 1] = wall_clock64();
     }
 #endif
-    if (x.last) tc_epilogue<RT, KIND>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows);
+    if (x.last) {
+      switch (kind) {
+        case TC_TANH: tc_epilogue<RT, TC_TANH>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_TGRAD: tc_epilogue<RT, TC_TGRAD>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_LIN: tc_epilogue<RT, TC_LIN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_BERN: tc_epilogue<RT, TC_BERN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_SAMPLE: tc_epilogue<RT, TC_SAMPLE>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        default: tc_epilogue<RT, TC_PRIOR>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+      }
+    }
 #ifdef IWAE_TC_TRACE
     if (st) {
       asm volatile("" ::"v"(R.l2[0]) : "memory");
@@ -504,14 +596,14 @@ __device__ __forceinline__ bool tc_dense(const TcArgs& A, CJob& J, COp& S, uint6
     }
 #endif
   };
-  if (!pre) tc_issue(S, rh, rl, tc_unit(S, 0, nch), fa);
-  for (int u = 0; u < U; u += 2) {
-    step(u, fa, fb);
+  if (U > 0) step(0, F.X, F.A, true);
+  if (U > 1) step(1, F.Y, F.B, true);
+  for (int u = 2; u < U; u += 2) {
+    step(u, F.A, F.A, false);
     if (u + 1 >= U) break;
-    step(u + 1, fb, fa);
+    step(u + 1, F.B, F.B, false);
   }
-  if (pn && (U & 1)) fa = fb;       // the next op's first unit landed in fb
-  return pn;
+  return Un;
 }
 
 // Barrier between ops.  LDS only: global stores (activations for the weight
@@ -691,6 +783,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
   int jb = 0;
   while (jb + 1 < plan->njobs && (int)blockIdx.x >= A.block_start[jb + 1]) ++jb;
   CJob& J = plan->job[jb];
+  tc_warm_descriptors(J);
   const int row0 = ((int)blockIdx.x - A.block_start[jb]) * R;
   const int nrows = min(R, A.rows - row0);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -715,8 +808,8 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
   }
 #endif
   __syncthreads();
-  TcFrag fa;              // first-unit fragments of the next Dense op (prefetched across the barrier)
-  bool pre = false, pnext = false;
+  TcSets F;               // the weight-fragment pipeline's register sets
+  int npre = 0;           // units of the next Dense op already requested (in F.X, F.Y)
 #ifdef IWAE_TC_TRACE
   const int trw = __shfl(tr, 0);       // the traced record, on every lane of wave 0
 #endif
@@ -732,30 +825,43 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
     if (tr >= 0 && 3 + 2 * s < 64) g_tc_trace[tr * 64 + 2 + 2 * s] = wall_clock64();
 #endif
     // the next op's first weight unit is requested by this op (see tc_dense)
+#ifdef IWAE_TC_TRACE
+    if (tr >= 0 && s < 32) {
+      asm volatile("" ::"s"(kind) : "memory");
+      g_tc_ptrace[(tr * 32 + s) * 4] = wall_clock64();
+    }
+#endif
     COp* Sn = nullptr;
     if (s + 1 < J.nop && J.op[s + 1].kind <= TC_LIN && !tc_needs_global(J.op[s + 1].kind)) Sn = &J.op[s + 1];
-    pnext = false;
-    if (kind > TC_LIN && Sn) pnext = tc_prefetch(*Sn, fa);   // elementwise op: before its own memory traffic
+    int nx = 0;             // elementwise op: requests the next op's first units
+    if (kind > TC_LIN && Sn) nx = tc_prefetch(*Sn, F);
     if (kind <= TC_LIN && S.out_buf >= 0) {
       const int width = kind == TC_SAMPLE ? S.d : S.N;
       tc_pad<RT>(tc_buf<RT>(J, S.out_buf), width, S.next_k, S.ones != 0);
     }
-    switch (kind) {      // one instantiation per kind: one epilogue per tile loop
-      case TC_TANH: pnext = tc_dense<RT, TC_TANH>(A, J, S, base, Rw, row0, nrows, fa, pre, Sn, UTR); break;
-      case TC_SAMPLE: pnext = tc_dense<RT, TC_SAMPLE>(A, J, S, base, Rw, row0, nrows, fa, pre, Sn, UTR); break;
-      case TC_PRIOR: pnext = tc_dense<RT, TC_PRIOR>(A, J, S, base, Rw, row0, nrows, fa, pre, Sn, UTR); break;
-      case TC_BERN: pnext = tc_dense<RT, TC_BERN>(A, J, S, base, Rw, row0, nrows, fa, pre, Sn, UTR); break;
-      case TC_TGRAD: pnext = tc_dense<RT, TC_TGRAD>(A, J, S, base, Rw, row0, nrows, fa, pre, Sn, UTR); break;
-      case TC_LIN: pnext = tc_dense<RT, TC_LIN>(A, J, S, base, Rw, row0, nrows, fa, pre, Sn, UTR); break;
+#ifdef IWAE_TC_TRACE
+    if (tr >= 0 && s < 32) g_tc_ptrace[(tr * 32 + s) * 4 + 1] = wall_clock64();
+#endif
+    switch (kind) {
+      case TC_TANH:
+      case TC_SAMPLE:
+      case TC_PRIOR:
+      case TC_BERN:
+      case TC_TGRAD:
+      case TC_LIN: nx = tc_dense<RT>(A, J, S, kind, base, Rw, row0, nrows, F, npre, Sn, UTR); break;
+#ifdef IWAE_TC_SKIPELEM    // timing experiment only
+      default: break;
+#else
       case TC_SAMPLE0: tc_sample0<RT>(A, J, S, base, row0, nrows, rq, rp); break;
       case TC_GBWD_PRIOR: tc_gbwd<RT, TC_GBWD_PRIOR>(A, J, S, row0, nrows); break;
       case TC_GBWD_ENC: tc_gbwd<RT, TC_GBWD_ENC>(A, J, S, row0, nrows); break;
       default: tc_loadg<RT>(A, J, S, row0, nrows); break;
+#endif
     }
 #ifdef IWAE_TC_TRACE
     if (tr >= 0 && 3 + 2 * s < 64) g_tc_trace[tr * 64 + 3 + 2 * s] = wall_clock64();
 #endif
-    pre = pnext;
+    npre = nx;
     if (s + 1 < J.nop && !tc_needs_global(J.op[s + 1].kind)) tc_lds_barrier();
     else __syncthreads();
   }
@@ -784,7 +890,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
     const int rg = row0 + t;
     if (J.logq) J.logq[rg] = rq[t] + s3[0];
     if (J.logp) J.logp[rg] = rp[t] + s3[1];
-    if (J.bern) *reinterpret_cast<float4*>(J.bern + (size_t)rg * J.ld_bern) = make_float4(kLn2 * s3[2], 0.f, 0.f, 0.f);
+    if (J.bern) J.bern[(size_t)rg * J.ld_bern + J.bern_col] = kLn2 * s3[2];
   }
 }
 
@@ -812,6 +918,10 @@ hipError_t tc_setup_attributes() {
 }  // namespace iwae
 
 #ifdef IWAE_TC_TRACE
+extern "C" int iwae_tc_ptrace_dump(unsigned long long* out, int cap) {
+  const int n = std::min(cap, 256 * 32 * 4);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(iwae::g_tc_ptrace), n * sizeof(unsigned long long)) == hipSuccess ? n : -1;
+}
 extern "C" int iwae_tc_utrace_dump(unsigned long long* out, int cap) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   const int n = 256 * 8 * 16 * 3 < cap ? 256 * 8 * 16 * 3 : cap;

@@ -51,3 +51,22 @@ for rec in range(nrec):
             continue
         print(f"  rec{rec} job{int(a[rec, 0])} op{op}: " + " ".join(
             f"u{u}[{(v[0] - t0) / 100:.2f} mma+{(v[1] - v[0]) / 100:.2f} epi+{(v[2] - v[1]) / 100:.2f}]" for u, v in us))
+# per op: kind read (descriptor loads), after the LDS padding, dense-op entry (wave 0)
+pdump = getattr(m._lib, "iwae_tc_ptrace_dump", None)
+if pdump is not None:
+    pdump.restype = ctypes.c_int
+    pdump.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    pbuf = (ctypes.c_ulonglong * (256 * 32 * 4))()
+    pdump(pbuf, 256 * 32 * 4)
+    P = np.array(pbuf[:], dtype=np.int64).reshape(256, 32, 4)
+    for rec in range(nrec):
+        t0 = int(a[rec, 1])
+        parts = []
+        for s in range(31):
+            b = int(a[rec, 2 + 2 * s])
+            if b == 0:
+                break
+            k, pd, de = (int(v) for v in P[rec, s, :3])
+            f = lambda v: f"{(v - b) / 100:.2f}" if v > 0 else "-"
+            parts.append(f"op{s}[kind+{f(k)} pad+{f(pd)} dense+{f(de)}]")
+        print(f"  prologue rec{rec} job{int(a[rec, 0])}: " + " ".join(parts))
