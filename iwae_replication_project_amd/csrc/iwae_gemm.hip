@@ -640,6 +640,12 @@ constexpr int SM_WAVES = 8;
 constexpr int SM_MAXU = 8;          // 16-deep k groups per wave (K <= 8 * 16 * 8 = 1024)
 constexpr int SM_MAX_ASLABS = 4;    // partial slabs a reader sums while staging A
 
+// Every load of a phase is issued before the first wait: the weight fragments
+// (bt is a template parameter, so no branch joins a set of loads), then the
+// activation rows in batches of SM_STAGE quads per thread.
+constexpr int SM_STAGE = 4;
+
+template <bool BT>
 __global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm_lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -663,7 +669,7 @@ __global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
   for (int u = 0; u < SM_MAXU; ++u) {
     const int k0 = kb + 16 * u + 4 * g;
     const bool ok = u < nu && n < a.N;
-    if (a.bt) {
+    if (BT) {
       // W[n][k0..k0+3]: one 16-byte load (k beyond K reads the row's zero padding or 0)
       bq[u] = bld4(rW, (ok && k0 < Kb) ? (unsigned)(n * a.ldw + kb0 + k0) * 4u : kOOB);
     } else {
@@ -677,57 +683,72 @@ __global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
   // activations -> LDS (rows >= M and k >= K zero)
   const __amdgpu_buffer_rsrc_t rA = a.a_bytes ? buf_rsrc(a.A, a.a_bytes) : buf_rsrc(a.A);
   const int q4 = Kp >> 2;
+  const int nq = 32 * q4;
   const bool write_a = a.a_out != nullptr && blockIdx.x == 0 && ks == 0;
-  for (int e = threadIdx.x; e < 32 * q4; e += blockDim.x) {
-    const int row = e / q4, kq = e - row * q4;
-    const int k = 4 * kq, gk = kb0 + k;
-    float4 v;
-    if (a.a_slabs > 0) {
-      // sum of the producer's partial slabs, activation, ones column at K - 1
-      // (all slab loads in flight at once: up to SM_MAX_ASLABS, slabs past a_slabs read 0)
-      float4 w[SM_MAX_ASLABS];
+  const int nsl = a.a_slabs;
+  for (int e0 = threadIdx.x; e0 < nq; e0 += SM_STAGE * blockDim.x) {
+    // the batch's loads (every slab of every quad) first
+    float4 w[SM_STAGE][SM_MAX_ASLABS];
 #pragma unroll
-      for (int sl = 0; sl < SM_MAX_ASLABS; ++sl)
-        w[sl] = bld4(rA, (sl < a.a_slabs && row < a.M && k < Kb)
-                             ? (unsigned)(sl * a.a_slab + row * a.lda + gk) * 4u : kOOB);
-      float4 sacc = w[0];
+    for (int i = 0; i < SM_STAGE; ++i) {
+      const int e = e0 + i * blockDim.x;
+      const int row = e / q4, kq = e - row * q4;
+      const int k = 4 * kq, gk = kb0 + k;
+      const bool in = e < nq && row < a.M && k < Kb;
 #pragma unroll
-      for (int sl = 1; sl < SM_MAX_ASLABS; ++sl) {
-        sacc.x += w[sl].x; sacc.y += w[sl].y; sacc.z += w[sl].z; sacc.w += w[sl].w;
-      }
-      float vv[4] = {sacc.x, sacc.y, sacc.z, sacc.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int col = gk + q;
-        float y = a.a_act ? ftanh(vv[q]) : vv[q];
-        if (write_a && row < a.M && col < a.K - 1) a.a_out[(size_t)row * a.a_ldo + col] = y;
-        vv[q] = (row < a.M && k + q < Kb) ? (col < a.K - 1 ? y : 1.f) : 0.f;
-      }
-      v = make_float4(vv[0], vv[1], vv[2], vv[3]);
-    } else {
-      v = bld4(rA, (row < a.M && k < Kb) ? (unsigned)(row * a.lda + gk) * 4u : kOOB);
-      if (a.a_ones > 0 && gk + 3 >= a.a_ones) {
-        // caller's rows end at a_ones: the ones column there, zeros after
-        float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (gk + q >= a.a_ones) vv[q] = (gk + q == a.a_ones && row < a.M) ? 1.f : 0.f;
-        v = make_float4(vv[0], vv[1], vv[2], vv[3]);
-      }
-      if (k + 3 >= Kb) {          // zero the part of the last quad past K (the row's padding may hold the ones column)
-        if (k + 1 >= Kb) v.y = 0.f;
-        if (k + 2 >= Kb) v.z = 0.f;
-        if (k + 3 >= Kb) v.w = 0.f;
-      }
-      if (a.a_copy && blockIdx.x == 0 && row < a.M && k < Kb) {
-        float* dst = a.a_copy + (size_t)row * a.a_copy_ld + gk;
-        const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (k + q < Kb) dst[q] = vv[q];
+      for (int sl = 0; sl < SM_MAX_ASLABS; ++sl) {
+        const bool used = nsl > 0 ? sl < nsl : sl == 0;
+        w[i][sl] = bld4(rA, (used && in) ? (unsigned)(sl * a.a_slab + row * a.lda + gk) * 4u : kOOB);
       }
     }
-    *reinterpret_cast<float4*>(&As[row * lds_ld + k]) = v;
+#pragma unroll
+    for (int i = 0; i < SM_STAGE; ++i) {
+      const int e = e0 + i * blockDim.x;
+      if (e >= nq) break;
+      const int row = e / q4, kq = e - row * q4;
+      const int k = 4 * kq, gk = kb0 + k;
+      float4 v;
+      if (nsl > 0) {
+        // sum of the producer's partial slabs, activation, ones column at K - 1
+        float4 sacc = w[i][0];
+#pragma unroll
+        for (int sl = 1; sl < SM_MAX_ASLABS; ++sl) {
+          sacc.x += w[i][sl].x; sacc.y += w[i][sl].y; sacc.z += w[i][sl].z; sacc.w += w[i][sl].w;
+        }
+        float vv[4] = {sacc.x, sacc.y, sacc.z, sacc.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int col = gk + q;
+          float y = a.a_act ? ftanh(vv[q]) : vv[q];
+          if (write_a && row < a.M && col < a.K - 1) a.a_out[(size_t)row * a.a_ldo + col] = y;
+          vv[q] = (row < a.M && k + q < Kb) ? (col < a.K - 1 ? y : 1.f) : 0.f;
+        }
+        v = make_float4(vv[0], vv[1], vv[2], vv[3]);
+      } else {
+        v = w[i][0];
+        if (a.a_ones > 0 && gk + 3 >= a.a_ones) {
+          // caller's rows end at a_ones: the ones column there, zeros after
+          float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (gk + q >= a.a_ones) vv[q] = (gk + q == a.a_ones && row < a.M) ? 1.f : 0.f;
+          v = make_float4(vv[0], vv[1], vv[2], vv[3]);
+        }
+        if (k + 3 >= Kb) {          // zero the part of the last quad past K (the row's padding may hold the ones column)
+          if (k + 1 >= Kb) v.y = 0.f;
+          if (k + 2 >= Kb) v.z = 0.f;
+          if (k + 3 >= Kb) v.w = 0.f;
+        }
+        if (a.a_copy && blockIdx.x == 0 && row < a.M && k < Kb) {
+          float* dst = a.a_copy + (size_t)row * a.a_copy_ld + gk;
+          const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (k + q < Kb) dst[q] = vv[q];
+        }
+      }
+      *reinterpret_cast<float4*>(&As[row * lds_ld + k]) = v;
+    }
   }
   __syncthreads();
   typedef float f4v __attribute__((ext_vector_type(4)));
@@ -783,12 +804,19 @@ hipError_t launch_smallm(hipStream_t st, const SmArgs& a) {
   if (a.M > 32 || KC > SM_WAVES * 16 * SM_MAXU || a.a_slabs > SM_MAX_ASLABS) return hipErrorInvalidValue;
   const int Kp = (KC + 15) & ~15;
   const size_t lds = (size_t)(32 * (Kp + 4) + SM_WAVES * 2 * 4 * 64) * sizeof(float);
-  hipLaunchKernelGGL(smallm_kernel, dim3((a.N + 15) / 16, ksl), dim3(SM_WAVES * 64), lds, st, a);
+  if (a.bt)
+    hipLaunchKernelGGL(smallm_kernel<true>, dim3((a.N + 15) / 16, ksl), dim3(SM_WAVES * 64), lds, st, a);
+  else
+    hipLaunchKernelGGL(smallm_kernel<false>, dim3((a.N + 15) / 16, ksl), dim3(SM_WAVES * 64), lds, st, a);
   return hipGetLastError();
 }
 
 hipError_t smallm_setup_attributes() {
-  return hipFuncSetAttribute((const void*)smallm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipError_t e = hipFuncSetAttribute((const void*)smallm_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)smallm_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             160 * 1024);
 }
 
 hipError_t launch_gemm(hipStream_t st, GemmKind kind, GemmEpi epi, int tile, int splits, bool ks,

@@ -109,29 +109,21 @@ struct MgFrag {
   mg_bf16x8 h[MG_KS], l[MG_KS];
 };
 
-// F row of output feature f (head stages: the permuted [mu | zs] quads); -1: none
-__device__ __forceinline__ int mg_src_row(const MgStage& S, int f) {
-  if (S.act != MG_SAMPLE && S.act != MG_PRIOR) return f < S.N ? f : -1;
-  const int q = f >> 3, w = f & 7, j = 4 * q + (w & 3);
-  if (j >= S.d) return -1;
-  return w < 4 ? j : S.d + j;
-}
-
-// Weight row offset (bytes, hi and lo planes alike) of this lane's output
-// feature in column tile t at k0, or kOOB
+// Byte offset (hi and lo planes alike) of this lane's fragment of column tile
+// t at k0 in the fragment-major copy (FX: [tile][k step][64 lanes][8], head
+// rows already permuted, padding rows zero), or kOOB
 __device__ __forceinline__ unsigned mg_frag_base(const MgStage& S, int t, int k0) {
   const int lane = threadIdx.x & 63;
-  const int r = lane & 15, g = lane >> 4;
   const int ntile = (S.N + 15) >> 4;
-  const int n = t < ntile ? mg_src_row(S, t * 16 + r) : -1;
-  return n >= 0 ? (unsigned)(n * S.ldk + k0 + 8 * g) * 2u : kOOB;
+  return t < ntile ? (unsigned)(((t * (S.ldk >> 5) + (k0 >> 5)) * 64 + lane) * 16) : kOOB;
 }
-// (an invalid lane's kOOB + 64u stays beyond the buffer: it reads 0)
+// k step u of the fragment: 1 KiB further (an invalid tile's kOOB + 1024 u
+// stays beyond the buffer: it reads 0)
 __device__ __forceinline__ void mg_fetch_step(__amdgpu_buffer_rsrc_t rh, __amdgpu_buffer_rsrc_t rl, unsigned vb,
                                               int u, int ns, MgFrag& f) {
   if (u >= ns) return;
-  f.h[u] = mg_as_bf16x8(__builtin_amdgcn_raw_buffer_load_b128(rh, vb, 64 * u, 0));
-  f.l[u] = mg_as_bf16x8(__builtin_amdgcn_raw_buffer_load_b128(rl, vb, 64 * u, 0));
+  f.h[u] = mg_as_bf16x8(__builtin_amdgcn_raw_buffer_load_b128(rh, vb, 1024 * u, 0));
+  f.l[u] = mg_as_bf16x8(__builtin_amdgcn_raw_buffer_load_b128(rl, vb, 1024 * u, 0));
 }
 // A fragments of column tile t over k in [k0, k0 + 256): 8 steps of 32, hi and lo
 __device__ __forceinline__ void mg_fetch(const MgStage& S, __amdgpu_buffer_rsrc_t rh, __amdgpu_buffer_rsrc_t rl,

@@ -932,7 +932,11 @@ static int smallm(iwae_handle* h, const Mat& A, int rows, const DenseL& d, bool 
   return IWAE_OK;
 }
 static bool smallm_ok(const iwae_handle* h, int rows) {
-  if (rows > 32) return false;
+  static const int max_rows = [] {      // tuning knob (0: never the few-row launches)
+    const char* e = std::getenv("IWAE_SMALLM_ROWS");
+    return e ? std::atoi(e) : 32;
+  }();
+  if (rows > std::min(max_rows, 32)) return false;
   for (int di : {h->enc[0].l1, h->enc[0].l2, h->enc[0].head})
     if (h->dense[di].fin + 1 > 1024 || h->dense[di].fout > 1024) return false;
   return true;
@@ -1424,8 +1428,10 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
     // jobs O1, O2: h1 again (same draw), output MLP, Bernoulli over a column
     // range each (the 784-wide output layer is the chain's longest op: both jobs
     // recompute the two 200-wide layers, O1 alone stores them)
+    // (only while the launch leaves CUs idle: at large batch the recomputed
+    // 200-wide layers cost more than the split saves)
     const int ntile = (h->dense[h->o3].fout + 15) / 16;
-    const int nsplit = ntile >= 16 ? 2 : 1;
+    const int nsplit = ntile >= 16 && (long long)P.Bimg * kS <= 2048 ? 2 : 1;
     for (int part = 0; part < nsplit; ++part) {
       const bool first = part == 0;
       TcBuild B;
@@ -2242,8 +2248,10 @@ static bool mega_plan(iwae_handle* h, MgLaunch& M, int& rt, int& waves, size_t& 
   auto stage = [&](int di, int in, int out, int act, int next_k) {
     const DenseL& d = h->dense[di];
     MgStage S{};
-    S.Whi = h->wsplit_hi + d.f_off; S.Wlo = h->wsplit_lo + d.f_off;
-    S.W_bytes = (unsigned)((h->wsplit_elems - d.f_off) * (long long)sizeof(__bf16));
+    // fragment-major split copies (FX, the train engine's): one 16-byte load
+    // per lane reads 1 KiB contiguous per wave
+    S.Whi = h->fx_hi + d.fx_off; S.Wlo = h->fx_lo + d.fx_off;
+    S.W_bytes = (unsigned)((h->fx_elems - d.fx_off) * (long long)sizeof(__bf16));
     S.ldk = d.ldF; S.K = d.fin + 1; S.N = d.fout;
     S.in_buf = in; S.out_buf = out; S.act = act; S.next_k = next_k;
     width[in] = std::max(width[in], S.ldk);
@@ -2338,6 +2346,7 @@ static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, flo
   int mg_rt = 0, mg_waves = 8;
   size_t mg_lds = 0;
   const bool mega = h->x3 && h->nll_fused && !h->masked && mega_plan(h, MG, mg_rt, mg_waves, mg_lds);
+  if (mega) CHK(ensure_fx(h));
   if (eps && !mega) return fail(h, IWAE_EINVAL, "injected-noise NLL chunks need the fused kernel");
   for (int i = 0; i < 8; ++i) MG.eps[i] = (eps && i < h->L) ? eps[i] : nullptr;
   MG.eps_N = N;

@@ -579,7 +579,12 @@ __device__ __forceinline__ int tc_dense(const TcArgs& A, CJob& J, COp& S, const 
       g_tc_utrace[(utr * 16 + u) * 3 + 1] = wall_clock64();
     }
 #endif
+#ifdef IWAE_TC_NOEPI       // timing experiment only
+    if (x.last) R.l2[0] += acc[0][0];
+    if (false) {
+#else
     if (x.last) {
+#endif
       switch (kind) {
         case TC_TANH: tc_epilogue<RT, TC_TANH>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
         case TC_TGRAD: tc_epilogue<RT, TC_TGRAD>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
