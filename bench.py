@@ -255,8 +255,8 @@ def main():
     pmc = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
-            rec = json.load(f)
-        if rec.get("kernel_label") == dom:
+            rec = json.load(f).get(dom)          # records keyed by the kernel label used here
+        if rec:
             traffic = round(rec["traffic_bytes"] / 1e6, 3)
             traffic_src = f"profiles/r02_pmc_traffic.json (MB per launch: fetch {rec['fetch_bytes'] / 1e6:.2f} + " \
                           f"write {rec['write_bytes'] / 1e6:.2f})"
@@ -268,6 +268,19 @@ def main():
                                 else "f32 MFMA 157.3 TFLOP/s"),
                     frac_of_bf16_dense_peak=round(achieved / BF16_PEAK_TFLOPS, 4),
                     kernels=kern, step_tflops=round(TRAIN_FLOP_PER_ROW * rows / el / 1e12, 3))
+
+    # ---- the train step's memory-bound launches (Adam, bound, FX refresh), same
+    # replay timing: algorithmic HBM bytes per launch / duration vs HBM peak
+    mem = {}
+    for kind, name in ((12, "adam_kernel"), (13, "bound_kernel"), (14, "fx_refresh_kernel")):
+        v = live(kind, 0)
+        if v is not None:
+            ms1, by = v
+            mem[name] = dict(avg_us=round(ms1 * 1e3, 3), bytes_per_launch=int(by),
+                             gbps=round(by / (ms1 * 1e-3) / 1e9, 1),
+                             frac_of_hbm_peak=round(by / (ms1 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+    roofline["memory_kernels"] = dict(peak_gbps=HBM_PEAK_GBS, kernels=mem,
+                                      note="bytes: algorithmic (each operand once); launches replayed back to back")
 
     # ---- configs[4] per-GPU share: B=512 images per GPU, k=50, same model and
     # step (RCCL gradient all-reduce for N > 1)

@@ -237,7 +237,9 @@ long long iwae_debug_count(const iwae_handle* h, int what);
 /* Live kernel timing: bracket every launch of one kernel class with HIP events
  * on the handle's stream -- a GEMM class (kind: 0 forward, 1 backward-data,
  * 2 backward-weight; epi: 0 store, 1 tanh, 2 Bernoulli, 3 tanh-grad) or the
- * train engine's forward (kind 10) / backward (kind 11) launch (epi ignored);
+ * train engine's forward (kind 10) / backward (kind 11) launch (epi ignored),
+ * or a memory-bound launch of the train step: 12 Adam, 13 bound, 14 FX refresh
+ * (replay only; their "FLOP" outputs are the launch's algorithmic HBM bytes);
  * kind = -1 disables.
  * Disables hipGraph replay while active.  iwae_profile_read synchronizes and
  * returns the summed kernel milliseconds, the algorithmic FLOPs of those

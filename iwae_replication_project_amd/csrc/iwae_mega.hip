@@ -350,6 +350,16 @@ __device__ __forceinline__ void mg_store_tanh(const MgBuf& OUT, const MgStage& S
   }
 }
 
+// Barrier between stages.  The stages exchange data through LDS only (global
+// memory: read-only inputs, and the log weights stored after the last stage),
+// so the release / acquire cover LDS alone: requested weight fragments and
+// pixels stay in flight across it (a full __syncthreads would wait for them).
+__device__ __forceinline__ void mg_lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // One column tile: x operands (Bernoulli stage) requested first, MFMAs over
 // the whole K, epilogue.
 template <int RT, int ACT>
@@ -500,7 +510,7 @@ __global__ __launch_bounds__(NW * 64) void mega_fwd_kernel(MgLaunch L) {
     Rw.l2[rt] = 0.f;
     Rw.xoff[rt] = (unsigned)((row0 + row) / L.kS) * (unsigned)L.ldx * 4u;
   }
-  __syncthreads();
+  mg_lds_barrier();
   MG_TRACE(1)
 
   for (int s = 0; s < L.nst; ++s) {
@@ -515,7 +525,7 @@ __global__ __launch_bounds__(NW * 64) void mega_fwd_kernel(MgLaunch L) {
       default: mg_dense<RT, MG_BERN, NW>(L, S, base, Rw); break;
     }
     MG_TRACE(3 + 3 * s)
-    __syncthreads();
+    mg_lds_barrier();
     MG_TRACE(4 + 3 * s)
   }
 

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <functional>
 #include <map>
 #include <string>
 #include <tuple>
@@ -190,6 +191,10 @@ struct iwae_handle {
   int prof_tile = 0, prof_splits = 1; bool prof_ks = false;
   double prof_flop1 = 0.0;
   bool prof_is_tc = false;             // the recorded launch is an engine launch (prof_kind 10 / 11)
+  // memory-bound launches (prof_kind 12 Adam, 13 bound, 14 FX refresh): the
+  // launch as a closure and its algorithmic bytes (reported in place of FLOP)
+  std::function<hipError_t(hipStream_t)> prof_mem;
+  float* prof_scratch = nullptr;       // side-effect targets of a replayed bound launch
   TcArgs prof_tc{};
   int prof_tc_rt = 1;
   size_t prof_tc_lds = 0;
@@ -689,6 +694,21 @@ static int run_bound(iwae_handle* h, const Plan& P, bool train, float sign, floa
   b.ticket = &h->ds->tickets[0]; b.rng_base = &h->ds->rng[0];
   b.adam_step = adam_tick ? &h->ds->adam.t : nullptr;
   HIPCHK(launch_bound(h->stream, b));
+  if (h->prof_kind == 13 && !h->prof_have) {
+    // replays write the loss, Philox base and Adam step into scratch instead
+    if (!h->prof_scratch) HIPCHK(hipMalloc(&h->prof_scratch, 64 * sizeof(float)));
+    HIPCHK(hipMemsetAsync(h->prof_scratch, 0, 64 * sizeof(float), h->stream));
+    BoundArgs r = b;
+    r.loss = h->prof_scratch;
+    r.rng_base = reinterpret_cast<uint64_t*>(h->prof_scratch + 8);
+    r.adam_step = b.adam_step ? reinterpret_cast<decltype(b.adam_step)>(h->prof_scratch + 16) : nullptr;
+    r.ticket = reinterpret_cast<unsigned*>(h->prof_scratch + 24);
+    h->prof_mem = [r](hipStream_t st) { return launch_bound(st, r); };
+    const double rows = (double)P.Bimg * P.kS;
+    // logq, logp, the row's 4 partial-sum floats in; lw, dlw, dpx out; contrib per image
+    h->prof_flop1 = rows * (2 + 4 + 1 + (b.dlw ? 1 : 0) + (b.dpx ? 1 : 0)) * 4.0 + (double)P.Bimg * 4.0;
+    h->prof_have = true;
+  }
   return IWAE_OK;
 }
 
@@ -808,6 +828,14 @@ static int run_fx(iwae_handle* h) {
   }
   a.total = tot;
   HIPCHK(launch_fx_refresh(h->stream, a));
+  if (h->prof_kind == 14 && !h->prof_have) {
+    h->prof_mem = [a](hipStream_t st) { return launch_fx_refresh(st, a); };
+    double chunks = 0.0;                  // 8 parameters in, 8 bf16 per plane out
+    for (int i = 0; i < a.nseg; ++i)
+      chunks += ((double)a.seg[i].fx_tiles * a.seg[i].fx_steps + (double)a.seg[i].gx_tiles * a.seg[i].gx_steps) * 64;
+    h->prof_flop1 = chunks * (8 * 4.0 + 2 * 16.0);
+    h->prof_have = true;
+  }
   return IWAE_OK;
 }
 
@@ -846,6 +874,16 @@ static int run_adam(iwae_handle* h, bool read_slabs, bool write_grad, bool do_ad
   a.grad_scale_override = scale_override;
   a.tick = tick;
   HIPCHK(launch_adam(h->stream, a, mx));
+  if (h->prof_kind == 12 && do_adam && !h->prof_have) {
+    AdamArgs r = a;
+    r.tick = false;                  // replays repeat this step's update (same t)
+    h->prof_mem = [r, mx](hipStream_t st) { return launch_adam(st, r, mx); };
+    double bytes = 0.0;
+    for (int i = 0; i < a.nseg; ++i)      // p, m, v in; p, m, v (+ g) out; the slabs in
+      bytes += (double)a.seg[i].n * 4.0 * (6 + (write_grad ? 1 : 0) + (read_slabs ? a.seg[i].splits : 1));
+    h->prof_flop1 = bytes;
+    h->prof_have = true;
+  }
   return IWAE_OK;
 }
 
@@ -1897,6 +1935,7 @@ void iwae_destroy(iwae_handle* h) {
   if (h->ds) (void)hipFree(h->ds);
   if (h->wsplit_hi) (void)hipFree(h->wsplit_hi);
   if (h->fx_hi) (void)hipFree(h->fx_hi);
+  if (h->prof_scratch) (void)hipFree(h->prof_scratch);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
   delete h;
 }
@@ -2569,6 +2608,7 @@ int iwae_profile_gemm(iwae_handle* h, int kind, int epi) {
   h->prof_flop = 0.0;
   h->prof_have = false;
   h->prof_is_tc = false;
+  h->prof_mem = nullptr;
   return IWAE_OK;
 }
 
@@ -2582,6 +2622,7 @@ int iwae_profile_replay(iwae_handle* h, int n, double* total_ms, double* total_f
   HIPCHK(hipEventRecord(e0, h->stream));
   for (int i = 0; i < n; ++i) {
     if (h->prof_is_tc) HIPCHK(launch_tc(h->stream, h->prof_tc, h->prof_tc_rt, h->prof_tc_lds));
+    else if (h->prof_kind >= 12) HIPCHK(h->prof_mem(h->stream));
     else HIPCHK(launch_gemm(h->stream, h->prof_k, h->prof_e, h->prof_tile, h->prof_splits, h->prof_ks, h->prof_args));
   }
   HIPCHK(hipEventRecord(e1, h->stream));
