@@ -457,41 +457,59 @@ __global__ __launch_bounds__(NW * 64) void mega_fwd_kernel(MgLaunch L) {
     float aq = 0.f, ap = 0.f;
     const int rg = row0 + min(rr, nrows - 1);
     const float* Pp = L.P0 + (size_t)(rg / L.kS) * L.ldP0;
-    for (int gq = sub; 4 * gq < L.h0_next_k; gq += TPR) {
-      float mu[4], zs[4];
+    // batches of 4 column quads per thread: every load of a batch (the image's
+    // mu / zs, injected eps) is issued before the first is used -- one memory
+    // round trip per batch instead of one per quad
+    const float* ep = L.eps[0] ? L.eps[0] + ((size_t)(L.eps_s0 + rg % L.kS) * L.eps_N + (L.eps_i0 + rg / L.kS)) * d
+                               : nullptr;
+    for (int gq0 = sub; 4 * gq0 < L.h0_next_k; gq0 += 4 * TPR) {
+      float mu[4][4], zs[4][4], ev[4][4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int jc = min(4 * gq + q, d - 1);
-        mu[q] = Pp[jc];
-        zs[q] = Pp[d + jc];
-      }
-      float4 e4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (L.eps[0]) {
-        const float* ep = L.eps[0] + ((size_t)(L.eps_s0 + rg % L.kS) * L.eps_N + (L.eps_i0 + rg / L.kS)) * d;
-        const int j = 4 * gq;
-        e4 = make_float4(j < d ? ep[j] : 0.f, j + 1 < d ? ep[j + 1] : 0.f, j + 2 < d ? ep[j + 2] : 0.f,
-                         j + 3 < d ? ep[j + 3] : 0.f);
-      } else if (4 * gq < d) {
-        e4 = philox_normal4(L.seed, base, (unsigned)rg, 0u, (unsigned)gq);
-      }
-      mg_bf16x4 vh, vl;
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = 4 * gq + q;
-        float hv = 0.f;
-        if (j < d) {
-          const float sc = fexp(zs[q]) + kScaleEps;
-          hv = f4_at(e4, q) * sc + mu[q];
-          aq += mg_normal_logp(hv, mu[q], sc);
-          ap += -0.5f * (hv * hv) - kHalfLog2Pi;
-        } else if (j == d) {
-          hv = 1.f;
+        for (int q = 0; q < 4; ++q) {
+          const int jc = min(4 * (gq0 + i * TPR) + q, d - 1);      // clamped: always a valid address
+          mu[i][q] = Pp[jc];
+          zs[i][q] = Pp[d + jc];
+          ev[i][q] = 0.f;
         }
-        vh[q] = (__bf16)hv;
-        vl[q] = (__bf16)(hv - (float)vh[q]);
+      if (L.eps[0]) {                 // uniform: injected noise (parity runs)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ev[i][q] = ep[min(4 * (gq0 + i * TPR) + q, d - 1)];
       }
-      *reinterpret_cast<mg_bf16x4*>(H.hi + rr * H.ld + 4 * gq) = vh;
-      *reinterpret_cast<mg_bf16x4*>(H.lo + rr * H.ld + 4 * gq) = vl;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int gq = gq0 + i * TPR;
+        if (4 * gq >= L.h0_next_k) break;
+        float4 e4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (L.eps[0]) {
+          const int j = 4 * gq;
+          e4 = make_float4(j < d ? ev[i][0] : 0.f, j + 1 < d ? ev[i][1] : 0.f, j + 2 < d ? ev[i][2] : 0.f,
+                           j + 3 < d ? ev[i][3] : 0.f);
+        } else if (4 * gq < d) {
+          e4 = philox_normal4(L.seed, base, (unsigned)rg, 0u, (unsigned)gq);
+        }
+        mg_bf16x4 vh, vl;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = 4 * gq + q;
+          float hv = 0.f;
+          if (j < d) {
+            const float sc = fexp(zs[i][q]) + kScaleEps;
+            hv = f4_at(e4, q) * sc + mu[i][q];
+            aq += mg_normal_logp(hv, mu[i][q], sc);
+            ap += -0.5f * (hv * hv) - kHalfLog2Pi;
+          } else if (j == d) {
+            hv = 1.f;
+          }
+          vh[q] = (__bf16)hv;
+          vl[q] = (__bf16)(hv - (float)vh[q]);
+        }
+        *reinterpret_cast<mg_bf16x4*>(H.hi + rr * H.ld + 4 * gq) = vh;
+        *reinterpret_cast<mg_bf16x4*>(H.lo + rr * H.ld + 4 * gq) = vl;
+      }
     }
     for (int o = TPR >> 1; o > 0; o >>= 1) {
       aq += __shfl_xor(aq, o);

@@ -195,6 +195,8 @@ struct iwae_handle {
   // launch as a closure and its algorithmic bytes (reported in place of FLOP)
   std::function<hipError_t(hipStream_t)> prof_mem;
   float* prof_scratch = nullptr;       // side-effect targets of a replayed bound launch
+  float* prof_adam = nullptr;          // parameters / m / v copies a replayed Adam launch updates
+  size_t prof_adam_bytes = 0;
   TcArgs prof_tc{};
   int prof_tc_rt = 1;
   size_t prof_tc_lds = 0;
@@ -877,6 +879,19 @@ static int run_adam(iwae_handle* h, bool read_slabs, bool write_grad, bool do_ad
   if (h->prof_kind == 12 && do_adam && !h->prof_have) {
     AdamArgs r = a;
     r.tick = false;                  // replays repeat this step's update (same t)
+    // ... on scratch copies of the parameters and moments: the model is untouched
+    const size_t pb = (size_t)h->nparam_int * sizeof(float);
+    if (h->prof_adam_bytes < 3 * pb) {
+      if (h->prof_adam) HIPCHK(hipFree(h->prof_adam));
+      h->prof_adam = nullptr;
+      HIPCHK(hipMalloc(&h->prof_adam, 3 * pb));
+      h->prof_adam_bytes = 3 * pb;
+    }
+    HIPCHK(hipMemcpyAsync(h->prof_adam, h->params, pb, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->prof_adam + h->nparam_int, h->adam_m, pb, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->prof_adam + 2 * h->nparam_int, h->adam_v, pb, hipMemcpyDeviceToDevice, h->stream));
+    r.param = h->prof_adam; r.m = h->prof_adam + h->nparam_int; r.v = h->prof_adam + 2 * h->nparam_int;
+    // (the gradient buffer is rewritten with the same values)
     h->prof_mem = [r, mx](hipStream_t st) { return launch_adam(st, r, mx); };
     double bytes = 0.0;
     for (int i = 0; i < a.nseg; ++i)      // p, m, v in; p, m, v (+ g) out; the slabs in
@@ -1936,6 +1951,7 @@ void iwae_destroy(iwae_handle* h) {
   if (h->wsplit_hi) (void)hipFree(h->wsplit_hi);
   if (h->fx_hi) (void)hipFree(h->fx_hi);
   if (h->prof_scratch) (void)hipFree(h->prof_scratch);
+  if (h->prof_adam) (void)hipFree(h->prof_adam);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
   delete h;
 }
