@@ -469,29 +469,52 @@ hipError_t launch_bound(hipStream_t st, const BoundArgs& a) {
 }
 
 // ---------------------------------------------------------- NLL: LSE merge
-__global__ __launch_bounds__(256) void lse_kernel(LseArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b < a.Bimg) {
-    const int row0 = b * a.kS;
-    float m = -INFINITY, s = 0.f;
-    for (int q = lane; q < a.kS; q += 64) {
-      const int r = row0 + q;
-      const float v = a.lw ? a.lw[r]
-                           : __fsub_rn(__fadd_rn(a.logp[r], row_sum_parts(a.part, a.ldpart, a.npart, r)), a.logq[r]);
-      if (v > m) { s = s * fexp(m - v) + 1.f; m = v; }
-      else s += fexp(v - m);
+// One 256-thread workgroup per image: each thread keeps a running (max, sum)
+// over its rows, reading them 8 at a time (all 8 loads in flight before the
+// first is used), then a fixed-order reduction over the lanes and the waves,
+// merged into the image's running (m, s) across chunks.  HBM-bound: 4 B per
+// row (fused path) or logq, logp and the partial sums (layer-wise path).
+constexpr int kLseThreads = 256, kLseBatch = 8;
+
+__device__ __forceinline__ float lse_row(const LseArgs& a, int r) {
+  return a.lw ? a.lw[r] : __fsub_rn(__fadd_rn(a.logp[r], row_sum_parts(a.part, a.ldpart, a.npart, r)), a.logq[r]);
+}
+
+__global__ __launch_bounds__(kLseThreads) void lse_kernel(LseArgs a) {
+  __shared__ float sm[kLseThreads / 64], ss[kLseThreads / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int b = blockIdx.x;
+  const int row0 = b * a.kS;
+  float m = -INFINITY, s = 0.f;
+  for (int q0 = threadIdx.x; q0 < a.kS; q0 += kLseBatch * kLseThreads) {
+    float v[kLseBatch];
+#pragma unroll
+    for (int i = 0; i < kLseBatch; ++i) {
+      const int q = min(q0 + i * kLseThreads, a.kS - 1);     // clamped: always a valid row
+      v[i] = lse_row(a, row0 + q);
     }
-    const float M = wave_max(m);
-    s = wave_sum(m == -INFINITY ? 0.f : s * expf(m - M));
-    if (lane == 0) {
-      if (a.init) { a.run_m[b] = M; a.run_s[b] = s; }
-      else {
-        const float m0 = a.run_m[b], s0 = a.run_s[b];
-        const float MM = fmaxf(m0, M);
-        a.run_s[b] = s0 * expf(m0 - MM) + s * expf(M - MM);
-        a.run_m[b] = MM;
-      }
+#pragma unroll
+    for (int i = 0; i < kLseBatch; ++i) {
+      if (q0 + i * kLseThreads >= a.kS) break;
+      if (v[i] > m) { s = s * fexp(m - v[i]) + 1.f; m = v[i]; }
+      else s += fexp(v[i] - m);
+    }
+  }
+  const float M = wave_max(m);
+  s = wave_sum(m == -INFINITY ? 0.f : s * expf(m - M));
+  if (lane == 0) { sm[wave] = M; ss[wave] = s; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float MM = sm[0];
+    for (int w = 1; w < kLseThreads / 64; ++w) MM = fmaxf(MM, sm[w]);
+    float S = 0.f;
+    for (int w = 0; w < kLseThreads / 64; ++w) S += sm[w] == -INFINITY ? 0.f : ss[w] * expf(sm[w] - MM);
+    if (a.init) { a.run_m[b] = MM; a.run_s[b] = S; }
+    else {
+      const float m0 = a.run_m[b], s0 = a.run_s[b];
+      const float T = fmaxf(m0, MM);
+      a.run_s[b] = s0 * expf(m0 - T) + S * expf(MM - T);
+      a.run_m[b] = T;
     }
   }
   if (a.ticket && last_block_arrive(a.ticket)) {
@@ -504,7 +527,7 @@ __global__ __launch_bounds__(256) void lse_kernel(LseArgs a) {
 
 hipError_t launch_lse(hipStream_t st, const LseArgs& a) {
   if (a.Bimg <= 0) return hipSuccess;
-  hipLaunchKernelGGL(lse_kernel, dim3((a.Bimg + 3) / 4), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(lse_kernel, dim3(a.Bimg), dim3(kLseThreads), 0, st, a);
   return hipGetLastError();
 }
 
