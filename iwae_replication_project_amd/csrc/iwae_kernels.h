@@ -451,16 +451,22 @@ hipError_t mega_setup_attributes();
 // gradients and later ops read.  A launch runs up to kTcMaxJobs independent
 // chains (workgroups [block_start[j], block_start[j+1]) run job j).
 enum TcKind {
+  // Dense ops (kind <= TC_LAST_DENSE): MFMA tile loop + epilogue
   TC_TANH = 0,       // out = tanh(acc)                                   Dense(tanh) F:26-F:27, F:92-F:93
   TC_SAMPLE = 1,     // encoder head: h = eps*scale + mu, log q (+ log N(h;0,1))   F:37, F:68-F:73
   TC_PRIOR = 2,      // decoder head: log N(h_t; mu, scale), h_t read (f32)       F:138-F:141
   TC_BERN = 3,       // output Dense(784): Bernoulli log-prob row sum + dLoss/dlogit factor g   F:123-F:128
   TC_TGRAD = 4,      // backward dX = dZ W^T (1 - y^2)  (tanh of the forward layer below)
   TC_LIN = 5,        // backward dX = dZ W^T (no activation): dL/dh contribution
-  TC_SAMPLE0 = 6,    // sample h1 from the image's first-layer (mu | zs)         F:58-F:60
-  TC_GBWD_PRIOR = 7, // dP of a decoder head (+ dL/dh of its target)
-  TC_GBWD_ENC = 8,   // dP of an encoder sampling head from the dL/dh sources
-  TC_LOADG = 9       // B operand = dpx[row] * g[row][:] (output layer backward)
+  TC_HEADP = 6,      // first encoder layer's head on image rows: stores P = (mu | zs) only   F:37
+  TC_LAST_DENSE = 6,
+  // elementwise ops
+  TC_SAMPLE0 = 7,    // sample h1 from the image's first-layer (mu | zs)         F:58-F:60
+  TC_GBWD_PRIOR = 8, // dP of a decoder head (+ dL/dh of its target)
+  TC_GBWD_ENC = 9,   // dP of an encoder sampling head from the dL/dh sources
+  TC_LOADG = 10,     // B operand = dpx[row] * g[row][:] (output layer backward)
+  TC_LOADSLAB = 11,  // image rows: y1 = tanh(sum of the input layer's split-K slabs)   F:26
+  TC_GBWD0 = 12      // image rows: dP0 = sum over the image's k samples of the h1 Gaussian backward
 };
 constexpr int kTcMaxOps = 20, kTcMaxBufs = 12, kTcMaxJobs = 3;
 struct TcOp {
@@ -479,6 +485,7 @@ struct TcOp {
   const float* src[4]; int ld_src[4]; int nsrc;   // GBWD_ENC: dL/dh sources summed
   float* dh; int ld_dh;       // GBWD_PRIOR: dL/dh of the target h
   int t0;                     // dense ops: first column tile (a job may run a column range [16 t0, N))
+  int nslab; long long slab_stride;   // LOADSLAB: partial slabs at y + i * slab_stride ([rows][ld_y] each)
 };
 struct TcJob {
   TcOp op[kTcMaxOps]; int nop;
@@ -493,6 +500,7 @@ struct TcArgs {
   const TcPlan* plan;
   int block_start[kTcMaxJobs + 1];
   int rows, kS;
+  int row_step;                             // rows per workgroup (0: 16 * RT; image-row launches: 1)
   const float* x; int ldx;                  // pixels by image
   uint64_t seed; const uint64_t* rng_base;
   const float* eps_a[8]; const float* eps_b[8]; int Bsplit, Bimg;   // injected noise ([k][B][d]) or null

@@ -156,11 +156,13 @@ struct iwae_handle {
   struct TcRec {
     TcPlan* dev = nullptr;
     int rt = 1, nb[kTcMaxJobs] = {};
+    int row_step = 0;                  // rows per workgroup (image-row launches; 0: 16 rt)
     size_t lds = 0;
     double flop = 0.0;               // algorithmic FLOPs of one launch (weight products, no bias rows)
   };
   std::map<std::vector<long long>, TcRec> tc_plans;
   int engine = 1;                    // train step on the row-chain engine when it applies (iwae_set_path)
+  int engine_img = 1;                // ... with the first encoder layer's l2 / head on its image-row jobs
   bool adam_splits = false;          // the Adam launch being built also rewrites the split copies
   // graphs
   bool use_graphs = false;
@@ -812,15 +814,16 @@ static int ensure_wsplit(iwae_handle* h) {
   return IWAE_OK;
 }
 
-// refresh the fragment-major copies of every Dense layer but the first encoder
-// layer's (which never runs on the engine)
+// refresh the fragment-major copies of every Dense layer but the input layer
+// (the engine runs every other layer, the first encoder layer's l2 and head on
+// image rows)
 static int run_fx(iwae_handle* h) {
   FxArgs a{};
   a.param = h->params; a.hi = h->fx_hi; a.lo = h->fx_lo;
   long long tot = 0;
   for (size_t i = 0; i < h->dense.size(); ++i) {
     const DenseL& d = h->dense[i];
-    if (d.rows_kind == 0) continue;
+    if ((int)i == h->enc[0].l1) continue;      // the 785-wide input layer: few-row f32 path only
     FxSeg& g = a.seg[a.nseg++];
     g.off = d.off; g.fin = d.fin; g.fout = d.fout; g.ldw = d.ldw;
     g.fx_off = d.fx_off; g.fx_tiles = d.fx_tiles; g.fx_steps = d.fx_steps; g.head_d = d.head_d;
@@ -995,9 +998,20 @@ static bool smallm_ok(const iwae_handle* h, int rows) {
   return true;
 }
 
+// Number of partial slabs the first encoder Dense writes into fslab when only
+// that launch runs (enc0_forward(l1_only), the train engine's image-row job
+// sums them).
+static int enc0_nslab(const iwae_handle* h, int Bimg) {
+  const DenseL& d1 = h->dense[h->enc[0].l1];
+  if (smallm_ok(h, Bimg)) return (int)std::min<long long>(std::min(4, h->fslab_S), cdiv(d1.fin + 1, 128));
+  const long long K = d1.fin + 1, kchunk = cdiv(cdiv(K, h->fslab_S), 64) * 64;
+  return (int)cdiv(K, kchunk);
+}
+
 // First encoder layer on the images (Stochastic_layer 0, F:58): y1, y2 and
-// its head (mu | zs) P0, per image.
-static int enc0_forward(iwae_handle* h, const Plan& P) {
+// its head (mu | zs) P0, per image.  l1_only: just the input Dense, as
+// pre-activation partial slabs in fslab (enc0_nslab of them).
+static int enc0_forward(iwae_handle* h, const Plan& P, bool l1_only = false) {
   if (smallm_ok(h, P.Bimg)) {
     // (1') first encoder layer on the images: three N-split few-row launches
     const StochL& S0 = h->enc[0];
@@ -1015,7 +1029,7 @@ static int enc0_forward(iwae_handle* h, const Plan& P) {
     }
     a.W = h->params + d1.off; a.ldw = d1.ldw;
     a.M = P.Bimg; a.N = d1.fout; a.K = d1.fin + 1;
-    if (ksl > 1) {
+    if (ksl > 1 || l1_only) {
       // the wide input layer split over K into partial slabs (more workgroups);
       // the second layer sums them, applies tanh and stores y1 while staging
       a.C = h->fslab; a.ldc = h->eb[0].y1.ld;
@@ -1036,6 +1050,7 @@ static int enc0_forward(iwae_handle* h, const Plan& P) {
       h->cap_x_node = nd == 1 ? deps[0] : nullptr;
       h->cap_x_args = a;
     }
+    if (l1_only) return IWAE_OK;
     if (ksl > 1) {
       const DenseL& d2 = h->dense[S0.l2];
       SmArgs b{};
@@ -1067,6 +1082,7 @@ static int enc0_forward(iwae_handle* h, const Plan& P) {
     CHK(prof_begin(h, GEMM_FWD, EPI_STORE, 2.0 * P.Bimg * d.fout * d.fin));
     HIPCHK(launch_gemm(h->stream, GEMM_FWD, EPI_STORE, 0, S, false, a));
     CHK(prof_end(h, GEMM_FWD, EPI_STORE));
+    if (l1_only) return IWAE_OK;
     // (2) rest of encoder layer 0 on the images: tanh(sum) -> l2 -> head (P0)
     RbFwdLaunch Lf{};
     Lf.ld_lds = rb_ld(h, false);
@@ -1432,7 +1448,9 @@ static std::vector<long long> tc_key(const Plan& P, int which) {
   return {which, P.Bimg, P.Bsplit, P.kS};
 }
 
-// forward (which = 0) or backward (1) plan of this shape: built once, uploaded
+// Plans of this shape, built once and uploaded: which = 0 the sample-row
+// forward launch, 1 the sample-row backward launch, 2 / 3 the first encoder
+// layer's image-row forward (after its input Dense) / backward launch.
 static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
   const auto key = tc_key(P, which);
   if (h->tc_plans.count(key)) return IWAE_OK;
@@ -1510,6 +1528,45 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
       if (L == 1 && first) { B.J.logq = h->logq; B.J.logp = h->logp; }
       jobs.push_back(B);
     }
+  } else if (which == 2) {
+    // job I: y1 = tanh(sum of the input Dense's slabs) -> l2 tanh -> head: P0 = (mu | zs)
+    TcBuild B;
+    const StochL& S0 = h->enc[0];
+    TcOp& ls = B.add(TC_LOADSLAB);
+    ls.N = h->dense[S0.l1].fout; ls.out_buf = 0; ls.next_k = ldF(S0.l2);
+    ls.y = h->fslab; ls.ld_y = h->eb[0].y1.ld;
+    ls.nslab = enc0_nslab(h, P.Bimg); ls.slab_stride = (long long)P.Bimg * h->eb[0].y1.ld;
+    ls.out = h->eb[0].y1.p; ls.ld_out = h->eb[0].y1.ld;
+    B.need(0, ls.next_k);
+    TcOp& a = tc_dense_op(h, B, TC_TANH, S0.l2, false, 0, 1, ldF(S0.head));
+    a.out = h->eb[0].y2.p; a.ld_out = h->eb[0].y2.ld;
+    TcOp& c = tc_head_op(h, B, TC_HEADP, S0.head, 1, -1, S0.d, 0);
+    c.out = h->eb[0].P.p; c.ld_out = h->eb[0].P.ld;
+    jobs.push_back(B);
+  } else if (which == 3) {
+    // job I': dP0 summed over each image's samples -> head^T (1 - y2^2) -> l2^T (1 - y1^2)
+    TcBuild B;
+    const StochL& S0 = h->enc[0];
+    TcOp& g = B.add(TC_GBWD0);
+    g.d = S0.d; g.out_buf = 0; g.in_buf = 2; g.next_k = ldG(S0.head); g.stdnormal = L == 1;
+    g.P = h->eb[0].P.p; g.ld_P = h->eb[0].P.ld;
+    g.h = h->h[0].p; g.ld_h = h->h[0].ld;
+    g.eps = h->eps_st[0].p; g.ld_eps = h->eps_st[0].ld;
+    int n = 0;
+    g.src[n] = h->dh_out[0].p; g.ld_src[n++] = h->dh_out[0].ld;
+    if (L >= 2) {
+      g.src[n] = h->dh_prior[0].p; g.ld_src[n++] = h->dh_prior[0].ld;
+      g.src[n] = h->dh_enc[0].p; g.ld_src[n++] = h->dh_enc[0].ld;
+    }
+    g.nsrc = n;
+    g.out = h->eb[0].dP.p; g.ld_out = h->eb[0].dP.ld;
+    B.need(0, std::max(g.next_k, 2 * S0.d));
+    B.need(2, 256);                            // reduction scratch: [16][32][8] floats
+    TcOp& a = tc_dense_op(h, B, TC_TGRAD, S0.head, true, 0, 1, ldG(S0.l2));
+    a.y = h->eb[0].y2.p; a.ld_y = h->eb[0].y2.ld; a.out = h->eb[0].dY2.p; a.ld_out = h->eb[0].dY2.ld;
+    TcOp& b = tc_dense_op(h, B, TC_TGRAD, S0.l2, true, 1, -1, 0);
+    b.y = h->eb[0].y1.p; b.ld_y = h->eb[0].y1.ld; b.out = h->eb[0].dY1.p; b.ld_out = h->eb[0].dY1.ld;
+    jobs.push_back(B);
   } else {
     // job O': (dpx g) W3^T (1 - y2^2) -> W2^T (1 - y1^2) -> W1^T = dL/dh1 (output MLP part)
     {
@@ -1575,7 +1632,10 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
   (void)r32;
   if ((int)jobs.size() > kTcMaxJobs) return fail(h, IWAE_EINVAL, "engine: too many jobs");
   // rows per workgroup: the largest tile count the LDS allows, fewer for small batches
-  const long long rows = (long long)P.Bimg * kS;
+  const bool img = which >= 2;
+  const long long rows = img ? (long long)P.Bimg : (long long)P.Bimg * kS;
+  // image rows: one image per workgroup (latency-bound chains of a few rows), up to 256 workgroups
+  const int row_step = img ? (int)std::max<long long>(1, cdiv(P.Bimg, 256)) : 0;
   int want = 1;                         // (2 and 4 row tiles spill registers: knob only)
   if (const char* e = std::getenv("IWAE_TC_RT")) want = std::atoi(e);   // tuning knob
   iwae_handle::TcRec rec;
@@ -1599,12 +1659,13 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
       for (size_t j = 0; j < jobs.size(); ++j) plan.job[j] = jobs[j].J;
       HIPCHK(hipMalloc(&rec.dev, sizeof(TcPlan)));
       HIPCHK(hipMemcpy(rec.dev, &plan, sizeof(TcPlan), hipMemcpyHostToDevice));
-      const int nb = (int)cdiv(rows, 16 * rt);
+      const int nb = (int)cdiv(rows, row_step > 0 ? row_step : 16 * rt);
+      rec.row_step = row_step;
       for (size_t j = 0; j < jobs.size(); ++j) {
         rec.nb[j] = nb;
         for (int o = 0; o < jobs[j].J.nop; ++o) {
           const TcOp& op = jobs[j].J.op[o];
-          if (op.kind > TC_LIN) continue;
+          if (op.kind > TC_LAST_DENSE) continue;
           const int kin = op.kind == TC_TGRAD || op.kind == TC_LIN ? op.K : op.K - 1;
           const int nout = op.kind == TC_SAMPLE || op.kind == TC_PRIOR ? 2 * op.d : op.N;
           rec.flop += 2.0 * (double)rows * kin * nout;
@@ -1618,6 +1679,8 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
 }
 
 static int tc_prepare(iwae_handle* h, const Plan& P) {
+  CHK(tc_prepare_one(h, P, 2));
+  CHK(tc_prepare_one(h, P, 3));
   CHK(tc_prepare_one(h, P, 0));
   return tc_prepare_one(h, P, 1);
 }
@@ -1635,7 +1698,8 @@ static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which) {
     tot += rec.nb[j];
   }
   a.block_start[kTcMaxJobs] = tot;
-  a.rows = P.Bimg * P.kS; a.kS = P.kS;
+  a.rows = which >= 2 ? P.Bimg : P.Bimg * P.kS; a.kS = P.kS;
+  a.row_step = rec.row_step;
   a.x = h->x_in.p; a.ldx = h->x_in.ld;
   a.seed = h->seed; a.rng_base = &h->ds->rng[0];
   for (int i = 0; i < h->L && i < 8; ++i) { a.eps_a[i] = E.a[i]; a.eps_b[i] = E.b[i]; }
@@ -1683,13 +1747,27 @@ static int finish_step(iwae_handle* h, const Plan& P, bool adam) {
 }
 
 static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
-  CHK(enc0_forward(h, P));
+  // The first encoder layer's l2 / head: up to 32 images the few-row N-split
+  // launches (one 16-column tile per workgroup; at B = 20 the image-row jobs,
+  // one image per workgroup streaming both layers' weights, took 18.2 + 18.4
+  // us against 12 + 21 us and the step 142.4 vs 139.9 us), above that the
+  // image-row engine jobs (B = 512: 0.954 vs 0.985 ms per step against the
+  // split-K GEMM + row-block kernels)
+  const bool img = h->engine_img && !smallm_ok(h, P.Bimg);
+  if (img) {
+    // first encoder layer: input Dense (few-row / split-K), then its image-row engine job
+    CHK(enc0_forward(h, P, true));
+    CHK(tc_run(h, P, E, 2));
+  } else {
+    CHK(enc0_forward(h, P));
+  }
   CHK(tc_run(h, P, E, 0));
   CHK(run_bound(h, P, true, -1.f, train_loss_ptr(h), adam, true));
   CHK(tc_run(h, P, E, 1));
   // (a second stream for the first encoder layer's backward beside the other
   // weight gradients measured slower inside the captured graph: sequential)
-  CHK(fused_encoder_bwd(h, P, h->dlw, 0));
+  if (img) CHK(tc_run(h, P, E, 3));
+  else CHK(fused_encoder_bwd(h, P, h->dlw, 0));
   CHK(weight_grads(h, P, true, true, h->dpx));
   CHK(finish_step(h, P, adam));
   if (adam) {
@@ -1926,6 +2004,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (e == hipSuccess) e = smallm_setup_attributes();
   if (e == hipSuccess) e = tc_setup_attributes();
   if (const char* w = std::getenv("IWAE_ENGINE")) h->engine = std::atoi(w) != 0;   // A/B switch
+  if (const char* w = std::getenv("IWAE_TC_IMG")) h->engine_img = std::atoi(w) != 0;   // A/B switch
   if (e != hipSuccess) {
     g_create_error = std::string("hipFuncSetAttribute failed: ") + hipGetErrorString(e);
     iwae_destroy(h);

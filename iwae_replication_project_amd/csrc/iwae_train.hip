@@ -323,6 +323,15 @@ __device__ __forceinline__ void tc_head(const TcArgs& A, COp& S, const TcBuf& H,
       }
       tc_put1(H, row * H.ld + j0, hv[0]);
       tc_put1(H, row * H.ld + j0 + 1, hv[1]);
+    } else if (KIND == TC_HEADP) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int j = j0 + c;
+        if (j < d && st) {
+          Pr[j] = mu[c];
+          Pr[d + j] = zs[c];
+        }
+      }
     } else {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
@@ -488,8 +497,8 @@ __device__ __forceinline__ void tc_epilogue(const TcArgs& A, COp& S, const TcBuf
 // Every set is addressed statically and always rewritten whole: no register
 // copy of a set with loads in flight (that would wait for every outstanding
 // load and store of the wave).
-struct TcSets {
-  TcFrag X, Y, A, B;
+struct TcSets {              // X, Y live across ops; A, B are local to a Dense op
+  TcFrag X, Y;
 };
 struct TcStream {          // the units of one Dense op for this wave
   __amdgpu_buffer_rsrc_t rh, rl;
@@ -591,6 +600,7 @@ __device__ __forceinline__ int tc_dense(const TcArgs& A, CJob& J, COp& S, const 
         case TC_LIN: tc_epilogue<RT, TC_LIN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
         case TC_BERN: tc_epilogue<RT, TC_BERN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
         case TC_SAMPLE: tc_epilogue<RT, TC_SAMPLE>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_HEADP: tc_epilogue<RT, TC_HEADP>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
         default: tc_epilogue<RT, TC_PRIOR>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
       }
     }
@@ -601,12 +611,13 @@ __device__ __forceinline__ int tc_dense(const TcArgs& A, CJob& J, COp& S, const 
     }
 #endif
   };
-  if (U > 0) step(0, F.X, F.A, true);
-  if (U > 1) step(1, F.Y, F.B, true);
+  TcFrag fA, fB;
+  if (U > 0) step(0, F.X, fA, true);
+  if (U > 1) step(1, F.Y, fB, true);
   for (int u = 2; u < U; u += 2) {
-    step(u, F.A, F.A, false);
+    step(u, fA, fA, false);
     if (u + 1 >= U) break;
-    step(u + 1, F.B, F.B, false);
+    step(u + 1, fB, fB, false);
   }
   return Un;
 }
@@ -780,6 +791,132 @@ __device__ __forceinline__ void tc_gbwd(const TcArgs& A, CJob& J, COp& S, int ro
   }
 }
 
+// Image rows (the first encoder layer, after its split-K input Dense):
+// y1 = tanh(sum of the partial slabs) into out_buf (ones column at N, zeros to
+// next_k) and S.out.  Every slab load of a quad is issued before the sum.
+template <int RT>
+__device__ __forceinline__ void tc_loadslab(CJob& J, COp& S, int row0, int nrows) {
+  constexpr int R = 16 * RT, TPR = (TC_NW * 64) / R;
+  constexpr int kMaxSlab = 4;
+  const int t = threadIdx.x, rr = t / TPR, sub = t - rr * TPR;
+  const TcBuf B = tc_buf<RT>(J, S.out_buf);
+  const int rg = row0 + min(rr, nrows - 1);
+  const bool st = rr < nrows;
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(S.y);
+  for (int c4 = sub; 4 * c4 < S.next_k; c4 += TPR) {
+    const int k = 4 * c4;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i0 = 0; i0 < S.nslab; i0 += kMaxSlab) {      // slabs in fixed order, kMaxSlab loads in flight
+      float4 w[kMaxSlab];
+#pragma unroll
+      for (int i = 0; i < kMaxSlab; ++i)
+        w[i] = bld4(rs, (i0 + i < S.nslab && k < S.N)
+                            ? (unsigned)((i0 + i) * S.slab_stride + (long long)rg * S.ld_y + k) * 4u : kOOB);
+#pragma unroll
+      for (int i = 0; i < kMaxSlab; ++i) { a.x += w[i].x; a.y += w[i].y; a.z += w[i].z; a.w += w[i].w; }
+    }
+    float v[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = k + i;
+      v[i] = c < S.N ? ftanh(v[i]) : (c == S.N ? 1.f : 0.f);
+      if (st && c < S.N) S.out[(size_t)rg * S.ld_out + c] = v[i];
+    }
+    tc_put4(B, rr * B.ld + k, v);
+  }
+}
+
+// Image rows: dP0 = (dmu0 | dzs0) of the first encoder layer's head, the sum
+// over the image's kS sample rows of the h1 Gaussian backward (GBWD_ENC's
+// formula per sample; h1 was sampled from the image's (mu0, s0), F:58-F:60).
+// All threads work on one image row at a time: thread (sample group sg,
+// column quad qi) sums samples sg, sg + 16, ... with every load of a batch in
+// flight, then the 16 groups are added in fixed order through LDS scratch
+// (S.in_buf's planes; deterministic).  dP0 goes to out_buf (natural order,
+// zeros to next_k) and S.out.
+template <int RT>
+__device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int row0, int nrows) {
+  constexpr int NSG = 16, SPT = 2;
+  const int t = threadIdx.x, sg = t >> 5, qi = t & 31;
+  const TcBuf B = tc_buf<RT>(J, S.out_buf);
+  float* scr = reinterpret_cast<float*>(tc_buf<RT>(J, S.in_buf).hi);   // [NSG][32][8] floats
+  const int d = S.d, kS = A.kS;
+  const int padw = S.next_k - 2 * d;
+  for (int e = t; e < 16 * RT * padw; e += TC_NW * 64) {
+    const int r = e / padw, c = 2 * d + e % padw;
+    B.hi[r * B.ld + c] = (__bf16)0.f;
+    B.lo[r * B.ld + c] = (__bf16)0.f;
+  }
+  __amdgpu_buffer_rsrc_t rsrc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) rsrc[u] = buf_rsrc(S.src[u]);
+  const __amdgpu_buffer_rsrc_t rh = buf_rsrc(S.h), re = buf_rsrc(S.eps), rd = buf_rsrc(A.dlw);
+  const int c0 = 4 * qi;
+  const bool live = c0 < d;
+  for (int rr = 0; rr < nrows; ++rr) {
+    const int b = row0 + rr;
+    const float* Pr = S.P + (size_t)b * S.ld_P;
+    float mu[4], rs4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = min(c0 + q, d - 1);
+      mu[q] = Pr[c];
+      rs4[q] = frcp(fexp(Pr[d + c]) + kScaleEps);
+    }
+    float dmu[4] = {0.f, 0.f, 0.f, 0.f}, dsc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int s0 = sg; s0 < kS; s0 += NSG * SPT) {
+      float4 hv[SPT], ev[SPT], gs[SPT][4];
+      float dl[SPT];
+#pragma unroll
+      for (int i = 0; i < SPT; ++i) {
+        const int s = s0 + i * NSG;
+        const bool ok = live && s < kS;
+        const long long r = (long long)b * kS + min(s, kS - 1);
+        hv[i] = bld4(rh, ok ? (unsigned)(r * S.ld_h + c0) * 4u : kOOB);
+        ev[i] = bld4(re, ok ? (unsigned)(r * S.ld_eps + c0) * 4u : kOOB);
+        dl[i] = bld1(rd, ok ? (unsigned)r * 4u : kOOB);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          gs[i][u] = bld4(rsrc[u], (ok && u < S.nsrc) ? (unsigned)(r * S.ld_src[u] + c0) * 4u : kOOB);
+      }
+#pragma unroll
+      for (int i = 0; i < SPT; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float h = f4_at(hv[i], q), e = f4_at(ev[i], q);
+          float G = ((f4_at(gs[i][0], q) + f4_at(gs[i][1], q)) + f4_at(gs[i][2], q)) + f4_at(gs[i][3], q);
+          const float z = h * rs4[q] - mu[q] * rs4[q];
+          const float dlq = -dl[i];
+          if (S.stdnormal) G += dl[i] * (-h);
+          G += dlq * (-z * rs4[q]);
+          dmu[q] += G + dlq * (z * rs4[q]);
+          dsc[q] += G * e + dlq * ((z * z - 1.f) * rs4[q]);
+        }
+      }
+    }
+    float* my = scr + (sg * 32 + qi) * 8;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      my[q] = dmu[q];
+      my[4 + q] = dsc[q];
+    }
+    tc_lds_barrier();
+    if (t < 32 * 8) {
+      const int q = t >> 3, j = t & 7;         // quad q, value j (dmu 0..3, dscale 4..7)
+      float v = 0.f;
+      for (int g = 0; g < NSG; ++g) v += scr[(g * 32 + q) * 8 + j];
+      const int c = 4 * q + (j & 3);
+      if (c < d) {
+        const int col = j < 4 ? c : d + c;
+        if (j >= 4) v *= fexp(Pr[d + c]);      // dzs = dscale * exp(zs)
+        tc_put1(B, rr * B.ld + col, v);
+        S.out[(size_t)b * S.ld_out + col] = v;
+      }
+    }
+    tc_lds_barrier();
+  }
+}
+
 // ----------------------------------------------------------------- kernel
 template <int RT>
 __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
@@ -789,8 +926,9 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
   while (jb + 1 < plan->njobs && (int)blockIdx.x >= A.block_start[jb + 1]) ++jb;
   CJob& J = plan->job[jb];
   tc_warm_descriptors(J);
-  const int row0 = ((int)blockIdx.x - A.block_start[jb]) * R;
-  const int nrows = min(R, A.rows - row0);
+  const int rstep = A.row_step > 0 ? min(A.row_step, R) : R;
+  const int row0 = ((int)blockIdx.x - A.block_start[jb]) * rstep;
+  const int nrows = min(rstep, A.rows - row0);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   float* rq = tcs + plan->acc_off;
   float* rp = rq + R;
@@ -837,10 +975,10 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
     }
 #endif
     COp* Sn = nullptr;
-    if (s + 1 < J.nop && J.op[s + 1].kind <= TC_LIN && !tc_needs_global(J.op[s + 1].kind)) Sn = &J.op[s + 1];
+    if (s + 1 < J.nop && J.op[s + 1].kind <= TC_LAST_DENSE && !tc_needs_global(J.op[s + 1].kind)) Sn = &J.op[s + 1];
     int nx = 0;             // elementwise op: requests the next op's first units
-    if (kind > TC_LIN && Sn) nx = tc_prefetch(*Sn, F);
-    if (kind <= TC_LIN && S.out_buf >= 0) {
+    if (kind > TC_LAST_DENSE && Sn) nx = tc_prefetch(*Sn, F);
+    if (kind <= TC_LAST_DENSE && S.out_buf >= 0) {
       const int width = kind == TC_SAMPLE ? S.d : S.N;
       tc_pad<RT>(tc_buf<RT>(J, S.out_buf), width, S.next_k, S.ones != 0);
     }
@@ -853,14 +991,17 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
       case TC_PRIOR:
       case TC_BERN:
       case TC_TGRAD:
-      case TC_LIN: nx = tc_dense<RT>(A, J, S, kind, base, Rw, row0, nrows, F, npre, Sn, UTR); break;
+      case TC_LIN:
+      case TC_HEADP: nx = tc_dense<RT>(A, J, S, kind, base, Rw, row0, nrows, F, npre, Sn, UTR); break;
 #ifdef IWAE_TC_SKIPELEM    // timing experiment only
       default: break;
 #else
       case TC_SAMPLE0: tc_sample0<RT>(A, J, S, base, row0, nrows, rq, rp); break;
       case TC_GBWD_PRIOR: tc_gbwd<RT, TC_GBWD_PRIOR>(A, J, S, row0, nrows); break;
       case TC_GBWD_ENC: tc_gbwd<RT, TC_GBWD_ENC>(A, J, S, row0, nrows); break;
-      default: tc_loadg<RT>(A, J, S, row0, nrows); break;
+      case TC_LOADG: tc_loadg<RT>(A, J, S, row0, nrows); break;
+      case TC_LOADSLAB: tc_loadslab<RT>(J, S, row0, nrows); break;
+      default: tc_gbwd0<RT>(A, J, S, row0, nrows); break;
 #endif
     }
 #ifdef IWAE_TC_TRACE

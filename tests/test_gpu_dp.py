@@ -186,8 +186,9 @@ def test_library_rccl_communicator_single_rank_step():
     (la, wa, ga), (lb, wb, gb) = runs
     np.testing.assert_allclose(lb, la, rtol=1e-6)
     np.testing.assert_allclose(wb, wa, atol=1e-6)
-    # B * g / B against g: rounding only (north_star: 1e-4 relative)
-    assert np.linalg.norm(gb - ga) <= 1e-5 * np.linalg.norm(ga), np.linalg.norm(gb - ga)
+    # B * g / B against g: rounding only, compounded over the three earlier
+    # steps' weight differences (north_star: 1e-4 relative)
+    assert np.linalg.norm(gb - ga) <= 1e-4 * np.linalg.norm(ga), np.linalg.norm(gb - ga)
 
 
 def _snr(rank, world):
