@@ -501,6 +501,10 @@ struct TcArgs {
   int block_start[kTcMaxJobs + 1];
   int rows, kS;
   int row_step;                             // rows per workgroup (0: 16 * RT; image-row launches: 1)
+  // XCD-aware placement (xcd_slots > 0): workgroup b runs on XCD b % 8 (round-robin dispatch);
+  // XCD x serves job xcd_job[x] as its xcd_rank[x]-th of xcd_count[job] XCDs, so each XCD's
+  // L2 fetches one job's weights.  Grid = 8 * xcd_slots; workgroups past a job's blocks exit.
+  int xcd_slots; int xcd_job[8], xcd_rank[8], xcd_count[kTcMaxJobs];
   const float* x; int ldx;                  // pixels by image
   uint64_t seed; const uint64_t* rng_base;
   const float* eps_a[8]; const float* eps_b[8]; int Bsplit, Bimg;   // injected noise ([k][B][d]) or null

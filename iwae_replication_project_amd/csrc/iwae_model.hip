@@ -163,6 +163,7 @@ struct iwae_handle {
   std::map<std::vector<long long>, TcRec> tc_plans;
   int engine = 1;                    // train step on the row-chain engine when it applies (iwae_set_path)
   int engine_img = 1;                // ... with the first encoder layer's l2 / head on its image-row jobs
+  int tc_xcd = 1;                    // XCD-aware job placement of the engine launches (env IWAE_TC_XCD)
   bool adam_splits = false;          // the Adam launch being built also rewrites the split copies
   // graphs
   bool use_graphs = false;
@@ -1700,6 +1701,28 @@ static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which) {
   a.block_start[kTcMaxJobs] = tot;
   a.rows = which >= 2 ? P.Bimg : P.Bimg * P.kS; a.kS = P.kS;
   a.row_step = rec.row_step;
+  // XCD-aware placement: the XCDs split over the jobs in proportion to their
+  // workgroups, so each XCD's L2 fetches one job's weight copies (a launch that
+  // fills more than the chip keeps the plain order)
+  int njobs = 0;
+  for (int j = 0; j < kTcMaxJobs; ++j) njobs += rec.nb[j] > 0;
+  if (h->tc_xcd && njobs > 1 && tot <= 256) {
+    int cnt[kTcMaxJobs] = {};
+    for (int q = 0; q < kTcMaxJobs; ++q) cnt[q] = rec.nb[q] > 0;      // one XCD per job first
+    for (int x = njobs; x < 8; ++x) {                                   // then the most loaded job
+      int best = -1;
+      for (int q = 0; q < kTcMaxJobs; ++q)
+        if (cnt[q] > 0 && (best < 0 || (double)rec.nb[q] / cnt[q] > (double)rec.nb[best] / cnt[best])) best = q;
+      ++cnt[best];
+    }
+    int slots = 0;
+    for (int q = 0, x = 0; q < kTcMaxJobs; ++q) {
+      a.xcd_count[q] = cnt[q];
+      for (int r = 0; r < cnt[q]; ++r, ++x) { a.xcd_job[x] = q; a.xcd_rank[x] = r; }
+      if (cnt[q] > 0) slots = std::max(slots, (int)cdiv(rec.nb[q], cnt[q]));
+    }
+    a.xcd_slots = slots;
+  }
   a.x = h->x_in.p; a.ldx = h->x_in.ld;
   a.seed = h->seed; a.rng_base = &h->ds->rng[0];
   for (int i = 0; i < h->L && i < 8; ++i) { a.eps_a[i] = E.a[i]; a.eps_b[i] = E.b[i]; }
@@ -2005,6 +2028,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (e == hipSuccess) e = tc_setup_attributes();
   if (const char* w = std::getenv("IWAE_ENGINE")) h->engine = std::atoi(w) != 0;   // A/B switch
   if (const char* w = std::getenv("IWAE_TC_IMG")) h->engine_img = std::atoi(w) != 0;   // A/B switch
+  if (const char* w = std::getenv("IWAE_TC_XCD")) h->tc_xcd = std::atoi(w) != 0;       // A/B switch
   if (e != hipSuccess) {
     g_create_error = std::string("hipFuncSetAttribute failed: ") + hipGetErrorString(e);
     iwae_destroy(h);

@@ -922,12 +922,20 @@ template <int RT>
 __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
   constexpr int R = 16 * RT;
   CPlan* plan = (CPlan*)A.plan;
-  int jb = 0;
-  while (jb + 1 < plan->njobs && (int)blockIdx.x >= A.block_start[jb + 1]) ++jb;
+  int jb = 0, blk;
+  if (A.xcd_slots > 0) {
+    const int x = (int)blockIdx.x & 7;
+    jb = A.xcd_job[x];
+    blk = ((int)blockIdx.x >> 3) * A.xcd_count[jb] + A.xcd_rank[x];
+    if (blk >= A.block_start[jb + 1] - A.block_start[jb]) return;     // idle: before any barrier
+  } else {
+    while (jb + 1 < plan->njobs && (int)blockIdx.x >= A.block_start[jb + 1]) ++jb;
+    blk = (int)blockIdx.x - A.block_start[jb];
+  }
   CJob& J = plan->job[jb];
   tc_warm_descriptors(J);
   const int rstep = A.row_step > 0 ? min(A.row_step, R) : R;
-  const int row0 = ((int)blockIdx.x - A.block_start[jb]) * rstep;
+  const int row0 = blk * rstep;
   const int nrows = min(rstep, A.rows - row0);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   float* rq = tcs + plan->acc_off;
@@ -944,7 +952,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
   }
 #ifdef IWAE_TC_TRACE
   int tr = -1;
-  if ((int)blockIdx.x == A.block_start[jb] && t == 0) {
+  if (blk == 0 && t == 0) {
     tr = (int)atomicAdd(&g_tc_trace_n, 1u);
     if (tr >= 256) tr = -1;
     else { g_tc_trace[tr * 64] = jb; g_tc_trace[tr * 64 + 1] = wall_clock64(); }
@@ -1041,7 +1049,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
 }
 
 hipError_t launch_tc(hipStream_t st, const TcArgs& a, int rt, size_t lds_bytes) {
-  const int nb = a.block_start[kTcMaxJobs];
+  const int nb = a.xcd_slots > 0 ? 8 * a.xcd_slots : a.block_start[kTcMaxJobs];
   if (nb <= 0) return hipSuccess;
   switch (rt) {
     case 1: hipLaunchKernelGGL((tc_kernel<1>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a); break;
