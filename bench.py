@@ -241,7 +241,8 @@ def main():
 
     cands = {"tc_kernel forward (train engine, bf16x3)": (live(10, 0), BF16X3_PEAK_TFLOPS),
              "tc_kernel backward (train engine, bf16x3)": (live(11, 0), BF16X3_PEAK_TFLOPS),
-             "gemm_kernel<FWD, EPI_BERN> (output layer, f32 MFMA)": (live(0, 2), FP32_MFMA_PEAK_TFLOPS)}
+             "gemm_kernel<FWD, EPI_BERN> (output layer, f32 MFMA)": (live(0, 2), FP32_MFMA_PEAK_TFLOPS),
+             "upd_kernel (weight gradients + Adam + FX copies, bf16x3)": (live(15, 0), BF16X3_PEAK_TFLOPS)}
     kern = {k: dict(avg_us=round(v[0] * 1e3, 3), flop_per_launch=v[1],
                     tflops=round(v[1] / (v[0] * 1e-3) / 1e12, 3), peak=pk)
             for k, (v, pk) in cands.items() if v is not None}

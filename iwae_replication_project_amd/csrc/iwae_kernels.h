@@ -330,6 +330,30 @@ struct FxArgs {
 };
 hipError_t launch_fx_refresh(hipStream_t st, const FxArgs& a);
 
+// Fused train-step update (iwae_update.hip): per Dense layer, dW_aug = X_aug^T
+// dZ over all the step's rows in 64 x 64 tiles (bf16x3, no split-K slabs), the
+// gradient buffer, Keras Adam and the FX / GX copies of the updated tile.
+struct UpdJob {
+  const float* A; const float* B; const float* ks;   // X_aug [rows][lda] (ones column at fin), dZ [rows][ldb], dZ row scale (>= rows floats)
+  int lda, ldb, rows;
+  long long off; int fin, fout, ldw;                  // W_aug [fin+1][ldw] at param + off
+  long long fx_off; int fx_steps, head_d;             // FX copy (fx_off < 0: none, GX neither)
+  long long gx_off; int gx_steps;
+  int tiles_m, tiles_n, tile0;                        // tiles [tile0, tile0 + tiles_m * tiles_n), column-major
+  int dbg;                                            // timing ablations (env IWAE_UPD_DBG): 1 no MFMA, 2 no staging, 4 no loads
+};
+constexpr int kUpdMaxJobs = 24, kUpdMaxTiles = 512;
+struct UpdArgs {
+  UpdJob job[kUpdMaxJobs]; int njobs;
+  unsigned char tile_job[kUpdMaxTiles];               // job of each tile
+  int ntiles, per_xcd;                                // grid = 8 * per_xcd; tile = xcd * per_xcd + slot
+  float* param; float* m; float* v; float* grad;
+  __bf16* fx_hi; __bf16* fx_lo;
+  const AdamState* state; int do_adam;
+};
+hipError_t launch_update(hipStream_t st, const UpdArgs& a);
+hipError_t upd_setup_attributes();
+
 // ------------------------------------------------- fused row-block kernels ----
 struct RbNoise {             // where a sampling layer's eps comes from (see eps_at)
   const float* eps_a; const float* eps_b;

@@ -139,6 +139,7 @@ struct iwae_handle {
   float *dlw2 = nullptr, *dpx2 = nullptr, *contrib = nullptr, *part = nullptr, *part2 = nullptr;
   float *run_m = nullptr, *run_s = nullptr;
   float* ebern = nullptr;            // engine: per-row Bernoulli log-likelihood, [rows][4] (cols 1-3 zero)
+  float* ones = nullptr;             // [rows] of 1.0 (the fused update's row scale of unscaled dZ)
   int ldpart = 0, npart = 0;
   float* slabs = nullptr;
   float* fslab = nullptr;            // split-K partials of the first encoder layer (fused path)
@@ -165,6 +166,9 @@ struct iwae_handle {
   int engine_img = 1;                // ... with the first encoder layer's l2 / head on its image-row jobs
   int tc_xcd = 1;                    // XCD-aware job placement of the engine launches (env IWAE_TC_XCD)
   bool adam_splits = false;          // the Adam launch being built also rewrites the split copies
+  int upd = 1;                       // fused weight-gradient + Adam + FX update launch (env IWAE_UPD)
+  long long upd_rows = 4096;         // ... up to this many sample rows per step (env IWAE_UPD_ROWS)
+  int upd_dbg = 0;                   // timing ablations of that launch (env IWAE_UPD_DBG; wrong results)
   // graphs
   bool use_graphs = false;
   // a captured train step; its first kernel reads the caller's x directly
@@ -353,6 +357,7 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
   vec(h->dlw, rows); vec(h->dpx, rows); vec(h->dlw2, rows); vec(h->dpx2, rows);
   vec(h->contrib, Bimg); vec(h->run_m, Bimg); vec(h->run_s, Bimg);
   vec(h->ebern, (size_t)rows * 4);
+  vec(h->ones, rows);
   h->fslab_S = (int)std::min<long long>(16, cdiv(h->xdim + 1, 64));
   vec(h->fslab, (size_t)h->fslab_S * Bimg * r4(h->enc[0].H + 1));
   if (train && rows <= 65536) {
@@ -402,6 +407,7 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
   }
   HIPCHK(launch_fill_col(h->stream, h->ob.y1.p, rows, h->ob.y1.ld, Hd, 1.f));
   HIPCHK(launch_fill_col(h->stream, h->ob.y2.p, rows, h->ob.y2.ld, Hd, 1.f));
+  HIPCHK(launch_fill_col(h->stream, h->ones, rows, 1, 0, 1.f));
   HIPCHK(hipStreamSynchronize(h->stream));
   h->cap_img = Bimg;
   h->cap_rows = rows;
@@ -1371,6 +1377,91 @@ static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const
   return IWAE_OK;
 }
 
+// Fused update (iwae_update.hip): every weight gradient over all the step's rows,
+// the gradient buffer, Adam and the FX / GX copies in one launch.  Single
+// process (the data-parallel merge needs the gradient before Adam), bf16x3
+// products, and up to upd_rows sample rows (one workgroup reduces a tile over
+// all rows: beyond that the split-K GEMM + Adam launches parallelise better).
+static bool use_update(const iwae_handle* h, const Plan& P) {
+  if (!h->upd || !h->x3 || h->dp_weighted || (long long)P.Bimg * P.kS > h->upd_rows) return false;
+  long long tiles = 0;
+  for (const DenseL& d : h->dense) tiles += cdiv(d.fin + 1, 64) * cdiv(d.fout, 64);
+  return tiles <= kUpdMaxTiles && (int)h->dense.size() <= kUpdMaxJobs;
+}
+
+static int run_update(iwae_handle* h, const Plan& P, bool adam) {
+  const int L = h->L, M = P.Bimg * P.kS;
+  struct WJ { int di; const Mat* A; const Mat* dZ; int rows; const float* ks; };
+  std::vector<WJ> js;
+  for (int i = 0; i < L; ++i) {
+    const StochL& S = h->enc[i];
+    const int rows = i == 0 ? P.Bimg : M;
+    js.push_back({S.l1, i == 0 ? &h->x_in : &h->h[i - 1], &h->eb[i].dY1, rows, nullptr});
+    js.push_back({S.l2, &h->eb[i].y1, &h->eb[i].dY2, rows, nullptr});
+    js.push_back({S.head, &h->eb[i].y2, &h->eb[i].dP, rows, nullptr});
+  }
+  for (int i = 0; i < L - 1; ++i) {
+    const StochL& S = h->dec[i];
+    js.push_back({S.l1, &h->h[L - 1 - i], &h->db[i].dY1, M, nullptr});
+    js.push_back({S.l2, &h->db[i].y1, &h->db[i].dY2, M, nullptr});
+    js.push_back({S.head, &h->db[i].y2, &h->db[i].dP, M, nullptr});
+  }
+  js.push_back({h->o1, &h->h[0], &h->ob.dY1, M, nullptr});
+  js.push_back({h->o2, &h->ob.y1, &h->ob.dY2, M, nullptr});
+  js.push_back({h->o3, &h->ob.y2, &h->ob.P, M, h->dpx});
+  if ((int)js.size() > kUpdMaxJobs) return fail(h, IWAE_EINVAL, "fused update: too many layers");
+  // the long reductions first (dispatched first)
+  std::stable_sort(js.begin(), js.end(), [](const WJ& x, const WJ& y) { return x.rows > y.rows; });
+  UpdArgs a{};
+  int tiles = 0;
+  double flop = 0.0;
+  for (const WJ& w : js) {
+    const DenseL& d = h->dense[w.di];
+    UpdJob& J = a.job[a.njobs++];
+    J.A = w.A->p; J.lda = w.A->ld; J.B = w.dZ->p; J.ldb = w.dZ->ld; J.ks = w.ks ? w.ks : h->ones; J.rows = w.rows;
+    J.off = d.off; J.fin = d.fin; J.fout = d.fout; J.ldw = d.ldw;
+    const bool fx = w.di != h->enc[0].l1;       // the input layer has no fragment-major copies
+    J.fx_off = fx ? d.fx_off : -1; J.fx_steps = d.fx_steps; J.head_d = d.head_d;
+    J.gx_off = d.gx_off; J.gx_steps = d.gx_steps;
+    J.tiles_m = (int)cdiv(d.fin + 1, 64); J.tiles_n = (int)cdiv(d.fout, 64);
+    J.tile0 = tiles;
+    J.dbg = h->upd_dbg;
+    tiles += J.tiles_m * J.tiles_n;
+    if (tiles > kUpdMaxTiles) return fail(h, IWAE_EINVAL, "fused update: too many tiles");
+    for (int q = J.tile0; q < tiles; ++q) a.tile_job[q] = (unsigned char)(a.njobs - 1);
+    flop += 2.0 * w.rows * (d.fin + 1) * d.fout;
+  }
+  a.ntiles = tiles;
+  a.per_xcd = (int)cdiv(tiles, 8);
+  a.param = h->params; a.m = h->adam_m; a.v = h->adam_v; a.grad = h->grad;
+  a.fx_hi = h->fx_hi; a.fx_lo = h->fx_lo;
+  a.state = &h->ds->adam; a.do_adam = adam ? 1 : 0;
+  HIPCHK(launch_update(h->stream, a));
+  if (adam) h->params_version++;
+  if (h->prof_kind == 15 && adam && !h->prof_have) {
+    // replays repeat this step's update on scratch copies of the parameters,
+    // moments and fragment-major copies: the model is untouched
+    const size_t pb = (size_t)h->nparam_int * sizeof(float), fb = (size_t)h->fx_elems * 2 * sizeof(__bf16);
+    if (h->prof_adam_bytes < 3 * pb + fb) {
+      if (h->prof_adam) HIPCHK(hipFree(h->prof_adam));
+      h->prof_adam = nullptr;
+      HIPCHK(hipMalloc(&h->prof_adam, 3 * pb + fb));
+      h->prof_adam_bytes = 3 * pb + fb;
+    }
+    HIPCHK(hipMemcpyAsync(h->prof_adam, h->params, pb, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->prof_adam + h->nparam_int, h->adam_m, pb, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->prof_adam + 2 * h->nparam_int, h->adam_v, pb, hipMemcpyDeviceToDevice, h->stream));
+    UpdArgs r = a;
+    r.param = h->prof_adam; r.m = h->prof_adam + h->nparam_int; r.v = h->prof_adam + 2 * h->nparam_int;
+    r.fx_hi = reinterpret_cast<__bf16*>(h->prof_adam + 3 * h->nparam_int);
+    r.fx_lo = r.fx_hi + h->fx_elems;
+    h->prof_mem = [r](hipStream_t st) { return launch_update(st, r); };
+    h->prof_flop1 = flop;
+    h->prof_have = true;
+  }
+  return IWAE_OK;
+}
+
 // ------------------------------------------------ row-chain train engine
 // Train step = first encoder layer (per image, enc0_forward) -> engine forward
 // (jobs E, O) -> bound -> engine backward (jobs O', E') -> first encoder layer
@@ -1791,6 +1882,12 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   // weight gradients measured slower inside the captured graph: sequential)
   if (img) CHK(tc_run(h, P, E, 3));
   else CHK(fused_encoder_bwd(h, P, h->dlw, 0));
+  if (use_update(h, P)) {
+    // weight gradients, Adam and the fragment-major copies in one launch
+    CHK(run_update(h, P, adam));
+    if (adam) h->fx_version = h->params_version;
+    return IWAE_OK;
+  }
   CHK(weight_grads(h, P, true, true, h->dpx));
   CHK(finish_step(h, P, adam));
   if (adam) {
@@ -2026,6 +2123,10 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (const char* w = std::getenv("IWAE_MG_WAVES")) h->mg_waves = std::atoi(w) == 4 ? 4 : 8;   // tuning knob
   if (e == hipSuccess) e = smallm_setup_attributes();
   if (e == hipSuccess) e = tc_setup_attributes();
+  if (e == hipSuccess) e = upd_setup_attributes();
+  if (const char* w = std::getenv("IWAE_UPD")) h->upd = std::atoi(w) != 0;              // A/B switch
+  if (const char* w = std::getenv("IWAE_UPD_ROWS")) h->upd_rows = std::atoll(w);        // tuning knob
+  if (const char* w = std::getenv("IWAE_UPD_DBG")) h->upd_dbg = std::atoi(w);           // timing ablations
   if (const char* w = std::getenv("IWAE_ENGINE")) h->engine = std::atoi(w) != 0;   // A/B switch
   if (const char* w = std::getenv("IWAE_TC_IMG")) h->engine_img = std::atoi(w) != 0;   // A/B switch
   if (const char* w = std::getenv("IWAE_TC_XCD")) h->tc_xcd = std::atoi(w) != 0;       // A/B switch

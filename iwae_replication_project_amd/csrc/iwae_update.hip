@@ -1,0 +1,425 @@
+// Fused parameter update of the train step (gfx950): every weight gradient
+// dW_aug = X_aug^T dZ (tape.gradient, F:243), Keras Adam on it (F:244, E:36-E:40:
+// TF ResourceApplyAdam) and the fragment-major split copies FX / GX of the
+// updated weights (the next step's engine operands), in ONE launch.
+//
+// One workgroup owns a 64 x 64 tile of one layer's W_aug (rows i = the layer's
+// inputs incl. the bias row, columns j = its outputs) and reduces over ALL the
+// step's rows itself -- no split-K slabs, so the gradient never makes the
+// slab round trip through HBM (the grouped GEMM + Adam + FX launches of the
+// unfused step move ~25 MB of partials for a 2 MB model), and the tile's
+// Adam update and copy refresh run in the same workgroup's epilogue.
+//
+// Main loop, per 128-row iteration: every thread loads an 8-row x 4-column
+// block of X and of dZ (16-byte buffer loads, 256 B contiguous per row across
+// 16 lanes; the buffer resource advances by 128 rows per iteration so rows
+// past the last read 0), transposes it in registers and writes k-contiguous
+// bf16 hi / lo rows into LDS (ds_write_b128, row stride 72 dwords = 8 mod 16,
+// 8-row blocks XOR-swizzled by (row >> 3) & 7).  Wave w multiplies k step w
+// (32 rows) of the iteration into its own copy of the whole 64 x 64 tile (16
+// accumulator tiles of v_mfma_f32_16x16x32_bf16, bf16x3: a_hi b_hi + a_hi b_lo
+// + a_lo b_hi), so each LDS byte is read once; the next iteration's split and
+// LDS writes sit between those MFMAs.  Two iterations of loads are in flight
+// (register sets named statically, the group of 8 iterations fully
+// unrolled); one barrier per iteration.  The four wave copies are summed in a
+// fixed order at the end: deterministic.
+//
+// Measured (B = 20, k = 50: 186 tiles, 1000 rows): 25.6 us against 31.2 us
+// for the grouped split-K GEMM + Adam + FX-refresh launches it replaces
+// (16.5 + 9.3 + 5.4), step 137.6 -> 132.5 us.  Ablations (IWAE_UPD_DBG):
+// launch + first loads 3.7 us, reduction 14 us, epilogue (Adam, stores,
+// FX / GX) 8 us.  Tried and measured slower: lanes spread over 8 or 16 rows
+// per load instruction (19 us reduction), the multiply and the staging in
+// separate phases (sched_barrier between them).
+#include "iwae_kernels.h"
+
+namespace iwae {
+
+typedef float up_f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 up_bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int UP_NW = 4;                    // waves
+constexpr int UP_NT = UP_NW * 64;           // threads
+constexpr int UP_RI = 128;                  // sample rows per iteration (4 k steps of 32)
+constexpr int UP_S = 72;                    // dwords per LDS row: 128 bf16 + 16 bf16 pad
+constexpr int UP_PLANE = 64 * UP_S;         // dwords per plane
+constexpr int UP_BUF = 4 * UP_PLANE;        // X hi, X lo, dZ hi, dZ lo
+constexpr int UP_PS = 68;                   // f32 stride of the epilogue tiles
+constexpr int UP_G = 8;                     // iterations per unrolled group (1024 rows)
+
+extern __shared__ __attribute__((aligned(16))) float ups[];
+
+// dword offset of row n's 8-row block `blk` in a plane (blocks XOR-swizzled by
+// (n >> 3) & 7: the column writes of sixteen lanes spread over the banks)
+__device__ __forceinline__ int up_off(int n, int blk) { return n * UP_S + 4 * (blk ^ ((n >> 3) & 7)); }
+// staging lane map: thread t loads rows 8 rg .. 8 rg + 7 of columns 4 cq ..
+// 4 cq + 3; sixteen consecutive lanes read one row's 256 contiguous bytes
+// (measured: lanes spread over more rows per load instruction were slower)
+__device__ __forceinline__ int up_rg(int t) { return t >> 4; }
+__device__ __forceinline__ int up_cq(int t) { return t & 15; }
+
+// (ext_vector_type registers: with HIP's float4 struct the compiler kept the
+// sets in scratch memory)
+struct UpRegs {
+  up_f32x4 x[8], z[8];
+  up_f32x4 k0, k1;
+};
+__device__ __forceinline__ up_f32x4 up_ld4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(up_f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+typedef float up_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 up_bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned up_u32x4 __attribute__((ext_vector_type(4)));
+// Column c of 8 loaded rows -> bf16 hi / lo planes (hi = RNE(v), lo =
+// RNE(v - hi)), pairwise: one v_cvt_pk_bf16_f32 per pair and plane, the hi
+// pair widened back with a shift and a mask, the residual by one packed
+// subtract; SCALE multiplies row q by k[q] first.  (Pairs are built straight
+// from the float4 components: an intermediate float[8] ends up in scratch.)
+template <int C, bool SCALE>
+__device__ __forceinline__ void up_split_col(const up_f32x4 (&a)[8], const UpRegs& R, up_u32x4& h, up_u32x4& l) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    up_f32x2 x = {a[2 * p][C], a[2 * p + 1][C]};
+    if (SCALE) {
+      const up_f32x4& k = p < 2 ? R.k0 : R.k1;
+      x *= up_f32x2{k[(2 * p) & 3], k[(2 * p + 1) & 3]};
+    }
+    const unsigned hb = __builtin_bit_cast(unsigned, __builtin_convertvector(x, up_bf16x2));
+    const up_f32x2 hf = {__uint_as_float(hb << 16), __uint_as_float(hb & 0xFFFF0000u)};
+    const up_f32x2 r = x - hf;
+    h[p] = hb;
+    l[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, up_bf16x2));
+  }
+}
+// stage column C of both operands (X as is, dZ times the row scale)
+template <int C>
+__device__ __forceinline__ void up_stage_col(const UpRegs& R, float* wbuf, int cq, int rg) {
+  const int o = up_off(4 * cq + C, rg);
+  up_u32x4 h, l;
+  up_split_col<C, false>(R.x, R, h, l);
+  *reinterpret_cast<up_u32x4*>(wbuf + o) = h;
+  *reinterpret_cast<up_u32x4*>(wbuf + UP_PLANE + o) = l;
+  up_split_col<C, true>(R.z, R, h, l);
+  *reinterpret_cast<up_u32x4*>(wbuf + 2 * UP_PLANE + o) = h;
+  *reinterpret_cast<up_u32x4*>(wbuf + 3 * UP_PLANE + o) = l;
+}
+__device__ __forceinline__ void up_stage_c(int c, const UpRegs& R, float* wbuf, int cq, int rg) {
+  if (c == 0) up_stage_col<0>(R, wbuf, cq, rg);
+  else if (c == 1) up_stage_col<1>(R, wbuf, cq, rg);
+  else if (c == 2) up_stage_col<2>(R, wbuf, cq, rg);
+  else up_stage_col<3>(R, wbuf, cq, rg);
+}
+
+// Per-thread byte offsets of its first row's 4 columns within an iteration
+// (row q adds q rows), fixed for the whole reduction: the buffer resource
+// moves instead (base and range advanced by 128 rows per iteration in scalar
+// registers), so rows past the last one fall outside the range and read 0.
+struct UpOff {
+  unsigned x, z, k;
+};
+__device__ __forceinline__ UpOff up_offsets(const UpdJob& J, int i0, int j0) {
+  const int t = threadIdx.x, rg = up_rg(t), cq = up_cq(t);
+  const int ci = i0 + 4 * cq, cj = j0 + 4 * cq;
+  const bool okx = ci < J.lda && !(J.dbg & 4), okz = cj < J.ldb && !(J.dbg & 4);
+  UpOff o;
+  o.x = okx ? (unsigned)(8 * rg * J.lda + ci) * 4u : kOOB;     // kOOB + 7 rows stays out of range
+  o.z = okz ? (unsigned)(8 * rg * J.ldb + cj) * 4u : kOOB;
+  o.k = (unsigned)(8 * rg) * 4u;
+  return o;
+}
+
+__device__ __forceinline__ void up_load(const UpdJob& J, const UpOff& O, int it, UpRegs& R) {
+  const int r0 = it * UP_RI;
+  const unsigned left = J.rows > r0 ? (unsigned)(J.rows - r0) : 0u;
+  const __amdgpu_buffer_rsrc_t ra = buf_rsrc(J.A + (size_t)r0 * J.lda, left * (unsigned)J.lda * 4u);
+  const __amdgpu_buffer_rsrc_t rz = buf_rsrc(J.B + (size_t)r0 * J.ldb, left * (unsigned)J.ldb * 4u);
+  const unsigned sx = (unsigned)J.lda * 4u, sz = (unsigned)J.ldb * 4u;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    R.x[q] = up_ld4(ra, O.x + q * sx);
+    R.z[q] = up_ld4(rz, O.z + q * sz);
+  }
+  // dZ row scale (dpx for the output layer, a ones vector otherwise); rows
+  // past the last read 0, which also zeroes dZ's stale rows there
+  const __amdgpu_buffer_rsrc_t rk = buf_rsrc(J.ks + r0, left * 4u);
+  R.k0 = up_ld4(rk, O.k);
+  R.k1 = up_ld4(rk, O.k + 16u);
+}
+
+// registers -> LDS (transposed, split): column c of the thread's 4 becomes one
+// 8-row k-contiguous chunk per plane
+__device__ __forceinline__ void up_stage(const UpdJob& J, const UpRegs& R, float* buf) {
+  const int t = threadIdx.x, rg = up_rg(t), cq = up_cq(t);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) up_stage_c(c, R, buf, cq, rg);
+}
+
+// One iteration's multiply (rbuf) with the next iteration's staging (R -> wbuf)
+// interleaved: the fragments are read first, then per column c of the thread's
+// four the split + LDS writes of that column sit between the MFMAs of
+// accumulator column sj = c, so the matrix core runs while the VALU splits.
+__device__ __forceinline__ void up_mul_stage(const UpdJob& J, const float* rbuf, float* wbuf, const UpRegs& R,
+                                             bool stage, up_f32x4 (&acc)[4][4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int t = threadIdx.x, rg = up_rg(t), cq = up_cq(t);
+  const int blk = 4 * w + (lane >> 4);
+  constexpr bool mul = true;
+  up_bf16x8 ah[4], al[4], bh[2], bl[2];
+  auto read_b = [&](int c) __attribute__((always_inline)) {
+    const int o = up_off(16 * c + (lane & 15), blk);
+    bh[c & 1] = *reinterpret_cast<const up_bf16x8*>(rbuf + 2 * UP_PLANE + o);
+    bl[c & 1] = *reinterpret_cast<const up_bf16x8*>(rbuf + 3 * UP_PLANE + o);
+  };
+  if (mul) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int o = up_off(16 * s + (lane & 15), blk);
+      ah[s] = *reinterpret_cast<const up_bf16x8*>(rbuf + o);
+      al[s] = *reinterpret_cast<const up_bf16x8*>(rbuf + UP_PLANE + o);
+    }
+    read_b(0);
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (mul && c + 1 < 4) read_b(c + 1);          // next column's B fragments (the other pair)
+    if (stage) up_stage_c(c, R, wbuf, cq, rg);
+    if (mul) {
+#pragma unroll
+      for (int si = 0; si < 4; ++si) acc[si][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[si], bh[c & 1], acc[si][c], 0, 0, 0);
+#pragma unroll
+      for (int si = 0; si < 4; ++si) acc[si][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[si], bl[c & 1], acc[si][c], 0, 0, 0);
+#pragma unroll
+      for (int si = 0; si < 4; ++si) acc[si][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[si], bh[c & 1], acc[si][c], 0, 0, 0);
+    }
+  }
+}
+
+// FX position of output feature j (a head's rows permuted into groups of 8,
+// [mu 4q..4q+3 | zs 4q..4q+3]; the inverse of fx_refresh_kernel's mapping)
+__device__ __forceinline__ int up_fx_pos(int j, int head_d) {
+  if (head_d <= 0) return j;
+  const int jj = j < head_d ? j : j - head_d;
+  return 8 * (jj >> 2) + (j < head_d ? 0 : 4) + (jj & 3);
+}
+
+__global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
+  // tile of this workgroup: consecutive tiles (sharing an operand slice) on one XCD
+  const int b = blockIdx.x;
+  const int T = (b & 7) * a.per_xcd + (b >> 3);
+  if ((b >> 3) >= a.per_xcd || T >= a.ntiles) return;
+  const int jb = a.tile_job[T];
+  const UpdJob& J = a.job[jb];
+  // Adam constants (state->t was advanced for this step by the bound kernel),
+  // read now: scalar loads, in flight during the reduction
+  const AdamState st = *a.state;
+  const int lt = T - J.tile0, tn = lt / J.tiles_m, tm = lt - tn * J.tiles_m;
+  const int i0 = 64 * tm, j0 = 64 * tn;
+  const int t = threadIdx.x;
+  const int M = J.fin + 1;
+
+  up_f32x4 acc[4][4];
+#pragma unroll
+  for (int si = 0; si < 4; ++si)
+#pragma unroll
+    for (int sj = 0; sj < 4; ++sj) acc[si][sj] = up_f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // groups of UP_G iterations, fully unrolled: the register sets R0 / R1 are
+  // never carried around a loop (a loop-carried set is renamed at the back
+  // edge with register copies, which drain every load in flight); loads past
+  // the last row are unconditional out-of-range reads of zeros
+  const int ngrp = (J.dbg & 64) ? 0 : (J.rows + UP_G * UP_RI - 1) / (UP_G * UP_RI);
+  float* buf0 = ups;
+  float* buf1 = ups + UP_BUF;
+  const UpOff O = up_offsets(J, i0, j0);
+  const int ei = t >> 2, ej = 16 * (t & 3);
+  const bool erow = i0 + ei < M;
+  float4 pp[4], mm[4], vv[4];
+  // Adam operands of the epilogue's elements (row ei, columns ej .. ej + 15),
+  // requested behind the first two iterations' loads (waiting for them then
+  // never waits for those)
+  auto adam_prefetch = [&]() __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t rp = buf_rsrc(a.param + J.off), rm = buf_rsrc(a.m + J.off),
+                                 rv = buf_rsrc(a.v + J.off);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = j0 + ej + 4 * q;
+      const unsigned off = (a.do_adam && erow && c < J.ldw) ? (unsigned)((i0 + ei) * J.ldw + c) * 4u : kOOB;
+      pp[q] = bld4(rp, off); mm[q] = bld4(rm, off); vv[q] = bld4(rv, off);
+    }
+  };
+  // One group of UP_G iterations from it0, fully unrolled.  Iteration u's
+  // rows are in LDS buffer u & 1; its multiply runs interleaved with staging
+  // iteration u + 1 (register set (u + 1) & 1, requested two iterations
+  // earlier) into the other buffer, whose set then requests iteration u + 3.
+  // One barrier per iteration.  (sched_barrier around the loads: the
+  // scheduler would otherwise interleave the two sets' loads, and waiting for
+  // one set would then wait for most of the other.)  tail: the group is
+  // followed by another (stage / request across the boundary).
+  // (the two sets are named explicitly per step: a reference chosen at run
+  // time would put them in scratch memory)
+  auto step = [&](int u, const float* rbuf, float* wbuf, UpRegs& Rn, int it0, bool tail) __attribute__((always_inline)) {
+    const bool more = u + 1 < UP_G || tail;
+    up_mul_stage(J, rbuf, wbuf, Rn, more, acc);
+    __builtin_amdgcn_sched_barrier(0);
+    if (u + 3 < UP_G || tail) up_load(J, O, it0 + u + 3, Rn);
+    // the Adam operands once the last rows are requested (their registers
+    // would otherwise crowd out the load sets for the whole reduction)
+    if (!tail && u == UP_G - 3) adam_prefetch();
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+  };
+  auto group = [&](UpRegs& R0, UpRegs& R1, int it0, bool tail) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < UP_G; u += 2) {
+      step(u, buf0, buf1, R1, it0, tail);
+      step(u + 1, buf1, buf0, R0, it0, tail);
+    }
+  };
+  auto start = [&](UpRegs& R0, UpRegs& R1) __attribute__((always_inline)) {
+    up_load(J, O, 0, R0);
+    __builtin_amdgcn_sched_barrier(0);
+    up_load(J, O, 1, R1);
+    __builtin_amdgcn_sched_barrier(0);
+    up_stage(J, R0, buf0);
+    __builtin_amdgcn_sched_barrier(0);
+    up_load(J, O, 2, R0);
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+  };
+  if (ngrp == 1) {
+    // straight-line (up to 1024 rows): no loop-carried register set, so no
+    // renaming copy drains the loads in flight
+    UpRegs R0, R1;
+    start(R0, R1);
+    group(R0, R1, 0, false);
+  } else if (ngrp > 1) {
+    // the sets are carried into the next group: renamed once per 1024 rows
+    UpRegs R0, R1;
+    start(R0, R1);
+    for (int gi = 0; gi < ngrp; ++gi) group(R0, R1, gi * UP_G, true);
+    adam_prefetch();
+  } else {
+    adam_prefetch();
+  }
+  __syncthreads();
+  if (J.dbg & 8) return;
+
+  // the four waves' tiles -> LDS, summed in wave order
+  {
+    const int lane = t & 63, w = t >> 6;
+    float* part = ups + w * 64 * UP_PS;
+#pragma unroll
+    for (int si = 0; si < 4; ++si)
+#pragma unroll
+      for (int sj = 0; sj < 4; ++sj)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) part[(16 * si + 4 * (lane >> 4) + q) * UP_PS + 16 * sj + (lane & 15)] = acc[si][sj][q];
+  }
+  __syncthreads();
+  float g[16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float4 s = *reinterpret_cast<const float4*>(ups + ei * UP_PS + ej + 4 * q);
+#pragma unroll
+    for (int w = 1; w < UP_NW; ++w) {
+      const float4 u = *reinterpret_cast<const float4*>(ups + w * 64 * UP_PS + ei * UP_PS + ej + 4 * q);
+      s.x += u.x; s.y += u.y; s.z += u.z; s.w += u.w;
+    }
+    g[4 * q] = s.x; g[4 * q + 1] = s.y; g[4 * q + 2] = s.z; g[4 * q + 3] = s.w;
+  }
+  // gradient buffer (get_gradients, the SNR harness)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = j0 + ej + 4 * q;
+    if (erow && c < J.ldw)
+      *reinterpret_cast<float4*>(a.grad + J.off + (long long)(i0 + ei) * J.ldw + c) =
+          make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+  }
+  if (!a.do_adam) return;
+
+  // Adam (adam_kernel's arithmetic)
+  const float tt = (float)st.t;
+  const float b1p = powf(st.b1, tt), b2p = powf(st.b2, tt);
+  const float alpha = st.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  const float omb1 = 1.f - st.b1, omb2 = 1.f - st.b2, eps = st.eps;
+  __syncthreads();                       // the partial tiles are read: reuse LDS for the new weights
+  float* pw = ups;                       // [64][UP_PS] updated W_aug tile
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float gq[4] = {g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]};
+    float mq[4] = {mm[q].x, mm[q].y, mm[q].z, mm[q].w}, vq[4] = {vv[q].x, vv[q].y, vv[q].z, vv[q].w};
+    float pq[4] = {pp[q].x, pp[q].y, pp[q].z, pp[q].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      mq[e] = mq[e] + (gq[e] - mq[e]) * omb1;
+      vq[e] = vq[e] + (gq[e] * gq[e] - vq[e]) * omb2;
+      pq[e] = pq[e] - (mq[e] * alpha) / (sqrtf(vq[e]) + eps);
+    }
+    const int c = j0 + ej + 4 * q;
+    if (erow && c < J.ldw) {
+      const long long o = J.off + (long long)(i0 + ei) * J.ldw + c;
+      *reinterpret_cast<float4*>(a.m + o) = make_float4(mq[0], mq[1], mq[2], mq[3]);
+      *reinterpret_cast<float4*>(a.v + o) = make_float4(vq[0], vq[1], vq[2], vq[3]);
+      *reinterpret_cast<float4*>(a.param + o) = make_float4(pq[0], pq[1], pq[2], pq[3]);
+    }
+    *reinterpret_cast<float4*>(pw + ei * UP_PS + ej + 4 * q) = make_float4(pq[0], pq[1], pq[2], pq[3]);
+  }
+  if (J.fx_off < 0 || (J.dbg & 16)) return;   // no fragment-major copies (the f32 input layer)
+  __syncthreads();
+  // FX chunks: (feature jj, 8 W_aug rows 8 ib ..) -> lane (pos & 15) + 16 ((k % 32) / 8) of step k / 32
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int c = t + UP_NT * e, jj = c & 63, ib = c >> 6;
+    const int j = j0 + jj, k0 = i0 + 8 * ib;
+    if (j < J.fout && k0 < M) {
+      up_bf16x8 vh, vl;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float v = k0 + q < M ? pw[(8 * ib + q) * UP_PS + jj] : 0.f;
+        const __bf16 h = (__bf16)v;
+        vh[q] = h;
+        vl[q] = (__bf16)(v - (float)h);
+      }
+      const int n = up_fx_pos(j, J.head_d);
+      const long long o = J.fx_off +
+          ((long long)((n >> 4) * J.fx_steps + (k0 >> 5)) * 64 + (n & 15) + 16 * ((k0 & 31) >> 3)) * 8;
+      *reinterpret_cast<up_bf16x8*>(a.fx_hi + o) = vh;
+      *reinterpret_cast<up_bf16x8*>(a.fx_lo + o) = vl;
+    }
+  }
+  // GX chunks: (input feature ii < fin, 8 outputs 8 jb ..)
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int c = t + UP_NT * e, jb = c & 7, ii = c >> 3;
+    const int n = i0 + ii, k0 = j0 + 8 * jb;
+    if (n < J.fin && k0 < J.fout) {
+      up_bf16x8 vh, vl;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float v = k0 + q < J.fout ? pw[ii * UP_PS + 8 * jb + q] : 0.f;
+        const __bf16 h = (__bf16)v;
+        vh[q] = h;
+        vl[q] = (__bf16)(v - (float)h);
+      }
+      const long long o = J.gx_off +
+          ((long long)((n >> 4) * J.gx_steps + (k0 >> 5)) * 64 + (n & 15) + 16 * ((k0 & 31) >> 3)) * 8;
+      *reinterpret_cast<up_bf16x8*>(a.fx_hi + o) = vh;
+      *reinterpret_cast<up_bf16x8*>(a.fx_lo + o) = vl;
+    }
+  }
+}
+
+hipError_t launch_update(hipStream_t st, const UpdArgs& a) {
+  if (a.ntiles <= 0) return hipSuccess;
+  const unsigned grid = 8u * (unsigned)a.per_xcd;
+  hipLaunchKernelGGL(upd_kernel, dim3(grid), dim3(UP_NT), (size_t)2 * UP_BUF * sizeof(float), st, a);
+  return hipGetLastError();
+}
+
+hipError_t upd_setup_attributes() {
+  return hipFuncSetAttribute((const void*)upd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             2 * UP_BUF * (int)sizeof(float));
+}
+
+}  // namespace iwae
