@@ -3,22 +3,11 @@
 // per row (or per image), lanes over the latent dimension (or over samples),
 // reductions by __shfl_xor butterflies -- HBM/latency-bound by design.
 #include "iwae_kernels.h"
+#include "iwae_bound.h"
 
 #include <algorithm>
 
 namespace iwae {
-
-// ----------------------------------------------------------------- helpers
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
-}
 
 // Noise of columns 4g..4g+3 of row r: injected (sample-major [k][B][d], the
 // reference's layout) when given for this row's draw, else device Philox.
@@ -243,190 +232,14 @@ hipError_t launch_gauss_bwd(hipStream_t st, int mode, const GaussBwdArgs& a) {
   return hipGetLastError();
 }
 
-// ----------------------------------------------------------------- bounds
-// One wave per image.  lw = (logp + logpx) - logq (F:345, F:349) with logpx
-// the sum of the Bernoulli epilogue's per-32-column partials.
-__device__ __forceinline__ float row_sum_parts(const float* part, int ldpart, int npart, int r) {
-  // ldpart is a multiple of 4 and the pad columns are zero: independent float4
-  // loads (no serialized latency chain), summed in column order.
-  const float4* p = reinterpret_cast<const float4*>(part + (size_t)r * ldpart);
-  const int n4 = (npart + 3) >> 2;
-  // buffer loads: the columns past n4 read 0 without a branch around the load
-  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(part);
-  const unsigned base = (unsigned)r * (unsigned)ldpart * 4u;
-  float4 v[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) v[t] = bld4(rs, t < n4 ? base + 16u * t : kOOB);
-  float s = 0.f;
-#pragma unroll
-  for (int t = 0; t < 8; ++t) s += ((v[t].x + v[t].y) + v[t].z) + v[t].w;
-  for (int t = 8; t < n4; ++t) s += ((p[t].x + p[t].y) + p[t].z) + p[t].w;
-  return s;
-}
-__device__ __forceinline__ float lw_at(const BoundArgs& a, int r) {
-  return __fsub_rn(__fadd_rn(a.logp[r], row_sum_parts(a.part, a.ldpart, a.npart, r)), a.logq[r]);
-}
-
-struct ImgBound {
-  float val;
-  float mx, se;  // IWAE / POWER
-  int lo, hi;    // MEDIAN (sample indices)
-};
-
-// Per-image bound value.  lw of the image is staged in `sh` (LDS, one wave's
-// slice) when kS <= 1024, otherwise re-read from the lw row the same lane wrote.
-struct LwView {
-  const float* sh;   // LDS copy or nullptr
-  const float* g;    // global lw row (written by this wave, same-lane reads only)
-  __device__ float operator()(int q) const { return sh ? sh[q] : g[q]; }
-};
-
-__device__ ImgBound image_bound(const BoundArgs& a, int mode, const LwView& lw) {
-  const int lane = threadIdx.x & 63;
-  const int kS = a.kS;
-  ImgBound o{0.f, 0.f, 0.f, 0, 0};
-  if (mode == BM_NONE) return o;
-  if (mode == BM_VAE) {
-    float s = 0.f;
-    for (int q = lane; q < kS; q += 64) s += lw(q);
-    o.val = wave_sum(s) / (float)kS;          // reduce_mean (F:430)
-    return o;
-  }
-  if (mode == BM_IWAE || mode == BM_POWER) {
-    const float pp = mode == BM_POWER ? a.p : 1.f;
-    float mx = -INFINITY;
-    for (int q = lane; q < kS; q += 64) mx = fmaxf(mx, lw(q));
-    mx = wave_max(mx);
-    float se = 0.f;
-    for (int q = lane; q < kS; q += 64) se += expf((lw(q) - mx) * pp);
-    se = wave_sum(se);
-    o.mx = mx; o.se = se;
-    // F:369: log(reduce_mean(exp(lw - max))) + max ; F:408: .../p + max
-    o.val = (mode == BM_POWER) ? logf(se / (float)kS) / pp + mx : logf(se / (float)kS) + mx;
-    return o;
-  }
-  if (mode == BM_MEDIAN) {
-    // tfp.stats.percentile(50, 'midpoint') = mean of order statistics
-    // floor((k-1)/2) and ceil((k-1)/2) (F:377).  Rank by counting (kS <= 1024, LDS).
-    const int klo = (kS - 1) / 2, khi = kS / 2;
-    float vlo = 0.f, vhi = 0.f;
-    int ilo = 0, ihi = 0;
-    for (int q = lane; q < kS; q += 64) {
-      const float v = lw.sh[q];
-      int rank = 0;
-      for (int t = 0; t < kS; ++t) {
-        const float u = lw.sh[t];
-        rank += (u < v) || (u == v && t < q);
-      }
-      if (rank == klo) { vlo = v; ilo = q + 1; }
-      if (rank == khi) { vhi = v; ihi = q + 1; }
-    }
-    // exactly one lane found each rank
-    vlo = wave_sum(ilo ? vlo : 0.f); vhi = wave_sum(ihi ? vhi : 0.f);
-    const float flo = wave_max((float)ilo), fhi = wave_max((float)ihi);
-    o.lo = (int)flo - 1; o.hi = (int)fhi - 1;
-    o.val = (vlo + vhi) * 0.5f;
-    return o;
-  }
-  // BM_MIWAE: sample s = j*k1 + i; mean_j [log mean_i exp(lw - m_j) + m_j]  (LDS)
-  float tot = 0.f;
-  for (int j = 0; j < a.k2; ++j) {
-    const int g0 = j * a.k1;
-    float mx = -INFINITY;
-    for (int i = lane; i < a.k1; i += 64) mx = fmaxf(mx, lw.sh[g0 + i]);
-    mx = wave_max(mx);
-    float se = 0.f;
-    for (int i = lane; i < a.k1; i += 64) se += expf(lw.sh[g0 + i] - mx);
-    se = wave_sum(se);
-    tot += logf(se / (float)a.k1) + mx;
-  }
-  o.val = tot / (float)a.k2;
-  return o;
-}
-
-// coef * dBound/dlw written to out[row0 + q] (and to out2 when given: no
-// store-then-reload of out)
-__device__ __forceinline__ void image_grad(const BoundArgs& a, int mode, int row0, const ImgBound& ib,
-                                           float coef, const LwView& lw, float* out, float* out2 = nullptr) {
-  const int lane = threadIdx.x & 63;
-  const int kS = a.kS;
-  auto put = [&](int i, float v) {
-    out[i] = v;
-    if (out2) out2[i] = v;
-  };
-  if (mode == BM_NONE) {
-    for (int q = lane; q < kS; q += 64) put(row0 + q, 0.f);
-  } else if (mode == BM_VAE) {
-    for (int q = lane; q < kS; q += 64) put(row0 + q, coef / (float)kS);
-  } else if (mode == BM_IWAE || mode == BM_POWER) {
-    const float pp = mode == BM_POWER ? a.p : 1.f;
-    for (int q = lane; q < kS; q += 64) put(row0 + q, coef * (expf((lw(q) - ib.mx) * pp) / ib.se));
-  } else if (mode == BM_MEDIAN) {
-    for (int q = lane; q < kS; q += 64)
-      put(row0 + q, coef * (0.5f * (q == ib.lo) + 0.5f * (q == ib.hi)));
-  } else {  // MIWAE
-    for (int j = 0; j < a.k2; ++j) {
-      const int g0 = j * a.k1;
-      float mx = -INFINITY;
-      for (int i = lane; i < a.k1; i += 64) mx = fmaxf(mx, lw.sh[g0 + i]);
-      mx = wave_max(mx);
-      float se = 0.f;
-      for (int i = lane; i < a.k1; i += 64) se += expf(lw.sh[g0 + i] - mx);
-      se = wave_sum(se);
-      for (int i = lane; i < a.k1; i += 64)
-        put(row0 + g0 + i, coef * (expf(lw.sh[g0 + i] - mx) / se) / (float)a.k2);
-    }
-  }
-}
-
 constexpr int kBoundWaves = 16;
 
 __global__ __launch_bounds__(kBoundWaves * 64) void bound_kernel(BoundArgs a) {
   __shared__ float sh_all[kBoundWaves][1024];
   __shared__ float red[kBoundWaves];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float wsum = 0.f;                       // this wave's images (single-workgroup finalize)
-  for (int b = blockIdx.x * kBoundWaves + wave; b < a.Bimg; b += gridDim.x * kBoundWaves) {
-    const bool ga = b < a.Bsplit;
-    const int mode = ga ? a.mode_a : a.mode_b;
-    const float w = ga ? a.w_a : a.w_b;
-    const int Bg = ga ? a.Bsplit : a.Bimg - a.Bsplit;
-    const int row0 = b * a.kS;
-    // log weights (for get_log_weights) and the optional Keras-BCE mean
-    const bool staged = a.kS <= 1024;
-    float bsum = 0.f;
-    for (int q = lane; q < a.kS; q += 64) {
-      const int r = row0 + q;
-      const float v = lw_at(a, r);
-      a.lw[r] = v;
-      if (staged) sh_all[wave][q] = v;
-      if (a.part2) bsum += row_sum_parts(a.part2, a.ldpart, a.npart, r);
-    }
-    bsum = wave_sum(bsum);
-    if (staged) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    const LwView lwv{staged ? sh_all[wave] : nullptr, a.lw + row0};
-    const ImgBound ib = image_bound(a, mode, lwv);
-    if (lane == 0) {
-      float c = w * ib.val / (float)Bg;
-      if (a.part2) c += a.bce_w * (bsum / (float)a.kS) / (float)Bg;
-      a.contrib[b] = c;
-      wsum += c;
-    }
-    if (a.dlw) {
-      // loss = -objective: dL/dlw = -(w/Bg) * dBound/dlw
-      image_grad(a, mode, row0, ib, -w / (float)Bg, lwv, a.dlw, a.dpx_is_const ? nullptr : a.dpx);
-      if (a.dpx && a.dpx_is_const)
-        for (int q = lane; q < a.kS; q += 64) a.dpx[row0 + q] = a.dpx_const;
-    }
-    if (a.dlw2) {
-      const ImgBound ib2 = image_bound(a, a.mode2, lwv);
-      image_grad(a, a.mode2, row0, ib2, -w / (float)Bg, lwv, a.dlw2, a.dpx2);
-    }
-  }
+  // this wave's images (single-workgroup finalize)
+  const float wsum = bound_images(a, blockIdx.x * kBoundWaves + wave, gridDim.x * kBoundWaves, sh_all[wave]);
   bool finalize;
   if (gridDim.x == 1) {
     // one workgroup: per-wave sums in a fixed order, no global round trip
@@ -443,15 +256,9 @@ __global__ __launch_bounds__(kBoundWaves * 64) void bound_kernel(BoundArgs a) {
       __syncthreads();
     }
   }
-  if (finalize) {
-    if (threadIdx.x == 0) {
-      float tot = 0.f;
-      for (int i = 0; i < kBoundWaves; ++i) tot += red[i];
-      if (a.loss) *a.loss = a.loss_sign * tot + (a.loss_add ? a.loss_add_coef * *a.loss_add : 0.f);
-      if (a.rng_base) { a.rng_base[1] = a.rng_base[0]; a.rng_base[0] += 1; }
-      if (a.adam_step) *a.adam_step += 1;      // the Adam launch of this train step reads it
-      if (gridDim.x > 1) *a.ticket = 0u;
-    }
+  if (finalize && threadIdx.x == 0) {
+    bound_finalize(a, red, kBoundWaves);
+    if (gridDim.x > 1) *a.ticket = 0u;
   }
 }
 

@@ -533,6 +533,12 @@ struct TcArgs {
   uint64_t seed; const uint64_t* rng_base;
   const float* eps_a[8]; const float* eps_b[8]; int Bsplit, Bimg;   // injected noise ([k][B][d]) or null
   const float* dlw; const float* dpx; float wa;
+  // the bound inside the backward launch (bnd_rows): every workgroup computes
+  // its rows' dL/dlw and dpx into LDS at float offset bnd_lds (dpx at + 16 RT)
+  // from its images' log weights, staging an image per wave at wave * bnd_ld;
+  // workgroup bnd_block (the grid's last) runs the whole bound: log weights,
+  // loss, global dlw / dpx, the Philox base and the Adam step
+  BoundArgs bnd; int bnd_rows, bnd_block, bnd_ld, bnd_lds;
 };
 hipError_t launch_tc(hipStream_t st, const TcArgs& a, int rt, size_t lds_bytes);
 hipError_t tc_setup_attributes();

@@ -159,12 +159,14 @@ struct iwae_handle {
     int rt = 1, nb[kTcMaxJobs] = {};
     int row_step = 0;                  // rows per workgroup (image-row launches; 0: 16 rt)
     size_t lds = 0;
+    int acc_off = 0;                 // float offset of the per-row accumulators in LDS
     double flop = 0.0;               // algorithmic FLOPs of one launch (weight products, no bias rows)
   };
   std::map<std::vector<long long>, TcRec> tc_plans;
   int engine = 1;                    // train step on the row-chain engine when it applies (iwae_set_path)
   int engine_img = 1;                // ... with the first encoder layer's l2 / head on its image-row jobs
   int tc_xcd = 1;                    // XCD-aware job placement of the engine launches (env IWAE_TC_XCD)
+  int tc_bound = 1;                  // the train step's bound inside the engine's backward launch (env IWAE_TC_BOUND)
   bool adam_splits = false;          // the Adam launch being built also rewrites the split copies
   int upd = 1;                       // fused weight-gradient + Adam + FX update launch (env IWAE_UPD)
   long long upd_rows = 4096;         // ... up to this many sample rows per step (env IWAE_UPD_ROWS)
@@ -676,14 +678,8 @@ static int forward_core(iwae_handle* h, const Plan& P, const EpsSet& E, bool tra
   return IWAE_OK;
 }
 
-static int run_bound(iwae_handle* h, const Plan& P, bool train, float sign, float* value_out,
-                     bool adam_tick = false, bool engine = false) {
-  if (P.kl) {
-    const int Lm1 = h->L - 1;
-    const int rows = Lm1 == 0 ? P.Bimg : P.Bimg * P.kS;
-    HIPCHK(launch_kl_v1(h->stream, h->eb[Lm1].P.p, h->eb[Lm1].P.ld, h->enc[Lm1].d, rows,
-                        &h->ds->scalars[2]));
-  }
+static BoundArgs make_bound_args(iwae_handle* h, const Plan& P, bool train, float sign, float* value_out,
+                                 bool adam_tick, bool engine) {
   BoundArgs b{};
   b.part = h->part; b.part2 = P.need_bce ? h->part2 : nullptr; b.ldpart = h->ldpart; b.npart = h->npart;
   b.logp = h->logp; b.logq = h->logq;
@@ -704,6 +700,18 @@ static int run_bound(iwae_handle* h, const Plan& P, bool train, float sign, floa
   }
   b.ticket = &h->ds->tickets[0]; b.rng_base = &h->ds->rng[0];
   b.adam_step = adam_tick ? &h->ds->adam.t : nullptr;
+  return b;
+}
+
+static int run_bound(iwae_handle* h, const Plan& P, bool train, float sign, float* value_out,
+                     bool adam_tick = false, bool engine = false) {
+  if (P.kl) {
+    const int Lm1 = h->L - 1;
+    const int rows = Lm1 == 0 ? P.Bimg : P.Bimg * P.kS;
+    HIPCHK(launch_kl_v1(h->stream, h->eb[Lm1].P.p, h->eb[Lm1].P.ld, h->enc[Lm1].d, rows,
+                        &h->ds->scalars[2]));
+  }
+  const BoundArgs b = make_bound_args(h, P, train, sign, value_out, adam_tick, engine);
   HIPCHK(launch_bound(h->stream, b));
   if (h->prof_kind == 13 && !h->prof_have) {
     // replays write the loss, Philox base and Adam step into scratch instead
@@ -1740,10 +1748,13 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
       mx = std::max(mx, b);
     }
     acc_off = (int)((mx + 15) / 16 * 4);            // floats, 16-byte aligned
-    const size_t lds = (size_t)acc_off * sizeof(float) + (size_t)(2 + 3 * 8) * 16 * rt * sizeof(float);
+    // per-row accumulators: log q, log p, [3][8 waves] partials, the in-launch
+    // bound's dL/dlw and dpx
+    const size_t lds = (size_t)acc_off * sizeof(float) + (size_t)(4 + 3 * 8) * 16 * rt * sizeof(float);
     if (lds <= 160 * 1024) {
       rec.rt = rt;
       rec.lds = lds;
+      rec.acc_off = acc_off;
       TcPlan plan;
       std::memset(&plan, 0, sizeof(plan));
       plan.njobs = (int)jobs.size();
@@ -1777,7 +1788,7 @@ static int tc_prepare(iwae_handle* h, const Plan& P) {
   return tc_prepare_one(h, P, 1);
 }
 
-static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which) {
+static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which, const BoundArgs* bnd = nullptr) {
   auto it = h->tc_plans.find(tc_key(P, which));
   if (it == h->tc_plans.end()) return fail(h, IWAE_EINVAL, "engine plan missing");
   const iwae_handle::TcRec& rec = it->second;
@@ -1819,6 +1830,18 @@ static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which) {
   for (int i = 0; i < h->L && i < 8; ++i) { a.eps_a[i] = E.a[i]; a.eps_b[i] = E.b[i]; }
   a.Bsplit = P.Bsplit; a.Bimg = P.Bimg;
   a.dlw = h->dlw; a.dpx = h->dpx; a.wa = P.wa;
+  a.bnd_block = -1;
+  if (bnd) {
+    // the bound in this (backward) launch: its rows' dL/dlw per workgroup, the
+    // whole bound in one extra workgroup (it advances the Philox base, which
+    // this launch does not read: nothing samples in the backward)
+    a.bnd = *bnd;
+    a.bnd_rows = 1;
+    a.bnd_block = h->tc_xcd && a.xcd_slots > 0 ? 8 * a.xcd_slots : tot;
+    a.bnd_ld = r4(P.kS);
+    a.bnd_lds = rec.acc_off + (2 + 3 * 8) * 16 * rec.rt;
+    a.rng_base = nullptr;
+  }
   const bool prof = h->prof_kind == 10 + which;
   if (prof) {
     if (h->prof_used + 2 > h->prof_ev.size()) {
@@ -1837,6 +1860,13 @@ static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which) {
     h->prof_flop += rec.flop;
     h->prof_have = true; h->prof_is_tc = true;
     h->prof_tc = a; h->prof_tc_rt = rec.rt; h->prof_tc_lds = rec.lds; h->prof_flop1 = rec.flop;
+    if (bnd) {
+      // replays write the loss, Philox base and Adam step into scratch
+      if (!h->prof_scratch) HIPCHK(hipMalloc(&h->prof_scratch, 64 * sizeof(float)));
+      h->prof_tc.bnd.loss = h->prof_scratch;
+      h->prof_tc.bnd.rng_base = reinterpret_cast<uint64_t*>(h->prof_scratch + 8);
+      h->prof_tc.bnd.adam_step = bnd->adam_step ? reinterpret_cast<long long*>(h->prof_scratch + 16) : nullptr;
+    }
   }
   return IWAE_OK;
 }
@@ -1860,6 +1890,17 @@ static int finish_step(iwae_handle* h, const Plan& P, bool adam) {
   return run_adam(h, false, true, true, 0.f, false, tail);
 }
 
+// The bound inside the engine's backward launch (no bound launch): up to 256
+// samples per image (an image's log weights staged per wave in the op buffers'
+// LDS, which must hold 8 of them plus the spare workgroup's 64 floats).
+static bool use_tc_bound(iwae_handle* h, const Plan& P) {
+  // (one spare workgroup runs the whole bound: up to 64 images, 8 per wave)
+  if (!h->tc_bound || P.kS > 256 || P.Bimg > 64 || P.need_bce || P.kl || P.piwae || h->prof_kind == 13) return false;
+  auto it = h->tc_plans.find(tc_key(P, 1));
+  if (it == h->tc_plans.end()) return false;
+  return (long long)it->second.acc_off >= 64 + 8LL * r4(P.kS);
+}
+
 static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
   // The first encoder layer's l2 / head: up to 32 images the few-row N-split
   // launches (one 16-column tile per workgroup; at B = 20 the image-row jobs,
@@ -1876,8 +1917,13 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
     CHK(enc0_forward(h, P));
   }
   CHK(tc_run(h, P, E, 0));
-  CHK(run_bound(h, P, true, -1.f, train_loss_ptr(h), adam, true));
-  CHK(tc_run(h, P, E, 1));
+  if (use_tc_bound(h, P)) {
+    const BoundArgs b = make_bound_args(h, P, true, -1.f, train_loss_ptr(h), adam, true);
+    CHK(tc_run(h, P, E, 1, &b));
+  } else {
+    CHK(run_bound(h, P, true, -1.f, train_loss_ptr(h), adam, true));
+    CHK(tc_run(h, P, E, 1));
+  }
   // (a second stream for the first encoder layer's backward beside the other
   // weight gradients measured slower inside the captured graph: sequential)
   if (img) CHK(tc_run(h, P, E, 3));
@@ -2130,6 +2176,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (const char* w = std::getenv("IWAE_ENGINE")) h->engine = std::atoi(w) != 0;   // A/B switch
   if (const char* w = std::getenv("IWAE_TC_IMG")) h->engine_img = std::atoi(w) != 0;   // A/B switch
   if (const char* w = std::getenv("IWAE_TC_XCD")) h->tc_xcd = std::atoi(w) != 0;       // A/B switch
+  if (const char* w = std::getenv("IWAE_TC_BOUND")) h->tc_bound = std::atoi(w) != 0;   // A/B switch
   if (e != hipSuccess) {
     g_create_error = std::string("hipFuncSetAttribute failed: ") + hipGetErrorString(e);
     iwae_destroy(h);

@@ -30,6 +30,7 @@
 // sample row: epilogues store them as one 16-byte f32 store and one 8-byte
 // store per LDS plane.
 #include "iwae_kernels.h"
+#include "iwae_bound.h"
 
 namespace iwae {
 
@@ -704,7 +705,7 @@ __device__ __forceinline__ void tc_loadg(const TcArgs& A, CJob& J, COp& S, int r
   const int t = threadIdx.x, rr = t / TPR, sub = t - rr * TPR;
   const TcBuf B = tc_buf<RT>(J, S.out_buf);
   const int rg = row0 + min(rr, nrows - 1);
-  const float dp = A.dpx[rg];
+  const float dp = A.bnd_rows ? tcs[A.bnd_lds + R + min(rr, nrows - 1)] : A.dpx[rg];
   const __amdgpu_buffer_rsrc_t rs = buf_rsrc(S.y);
   for (int c4 = sub; 4 * c4 < S.next_k; c4 += TPR) {
     const int k = 4 * c4;
@@ -736,7 +737,7 @@ __device__ __forceinline__ void tc_gbwd(const TcArgs& A, CJob& J, COp& S, int ro
   }
   const int rg = row0 + min(rr, nrows - 1);
   const bool st = rr < nrows;
-  const float dl = A.dlw[rg];
+  const float dl = A.bnd_rows ? tcs[A.bnd_lds + min(rr, nrows - 1)] : A.dlw[rg];
   const float* Pr = S.P + (size_t)rg * S.ld_P;
   const float* Hr = S.h + (size_t)rg * S.ld_h;
   __amdgpu_buffer_rsrc_t rsrc[4];
@@ -922,6 +923,16 @@ template <int RT>
 __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
   constexpr int R = 16 * RT;
   CPlan* plan = (CPlan*)A.plan;
+  if ((int)blockIdx.x == A.bnd_block) {
+    // the step's bound (bound_kernel's work in this launch's spare workgroup)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float* red = tcs;
+    const float ws = bound_images(A.bnd, wave, TC_NW, tcs + 64 + wave * A.bnd_ld);
+    if (lane == 0) red[wave] = ws;
+    __syncthreads();
+    if (threadIdx.x == 0) bound_finalize(A.bnd, red, TC_NW);
+    return;
+  }
   int jb = 0, blk;
   if (A.xcd_slots > 0) {
     const int x = (int)blockIdx.x & 7;
@@ -942,6 +953,11 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
   float* rp = rq + R;
   float* red = rp + R;                  // [3][NW][R]
   if (t < R) { rq[t] = 0.f; rp[t] = 0.f; }
+  // this workgroup's dL/dlw and dpx (the op buffers' space stages the images'
+  // log weights: nothing is in them yet).  (Inside the op loop, beside the
+  // first op's weight prefetch, it slowed every engine launch by 2-3 us.)
+  if (A.bnd_rows) bound_rows(A.bnd, row0, row0 + nrows, wave, TC_NW, tcs + wave * A.bnd_ld, tcs + A.bnd_lds,
+                             tcs + A.bnd_lds + R);
   const uint64_t base = A.rng_base ? *A.rng_base : 0ull;
   TcRows<RT> Rw;
 #pragma unroll
@@ -986,6 +1002,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
     if (s + 1 < J.nop && J.op[s + 1].kind <= TC_LAST_DENSE && !tc_needs_global(J.op[s + 1].kind)) Sn = &J.op[s + 1];
     int nx = 0;             // elementwise op: requests the next op's first units
     if (kind > TC_LAST_DENSE && Sn) nx = tc_prefetch(*Sn, F);
+
     if (kind <= TC_LAST_DENSE && S.out_buf >= 0) {
       const int width = kind == TC_SAMPLE ? S.d : S.N;
       tc_pad<RT>(tc_buf<RT>(J, S.out_buf), width, S.next_k, S.ones != 0);
@@ -1049,7 +1066,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
 }
 
 hipError_t launch_tc(hipStream_t st, const TcArgs& a, int rt, size_t lds_bytes) {
-  const int nb = a.xcd_slots > 0 ? 8 * a.xcd_slots : a.block_start[kTcMaxJobs];
+  const int nb = (a.xcd_slots > 0 ? 8 * a.xcd_slots : a.block_start[kTcMaxJobs]) + (a.bnd_block >= 0 ? 1 : 0);
   if (nb <= 0) return hipSuccess;
   switch (rt) {
     case 1: hipLaunchKernelGGL((tc_kernel<1>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a); break;
