@@ -91,6 +91,8 @@ struct Plan {
 struct iwae_handle {
   int device = 0;
   hipStream_t own_stream = nullptr;
+  hipStream_t side_stream = nullptr;   // second branch of a train step (the fused update's sample-row tiles)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
   iwae_config cfg{};
@@ -172,6 +174,7 @@ struct iwae_handle {
   int upd = 1;                       // fused weight-gradient + Adam + FX update launch (env IWAE_UPD)
   long long upd_rows = 4096;         // ... up to this many sample rows per step (env IWAE_UPD_ROWS)
   int upd_dbg = 0;                   // timing ablations of that launch (env IWAE_UPD_DBG; wrong results)
+  int upd_split = 0;                 // ... split over two graph branches (env IWAE_UPD_SPLIT)
   // graphs
   bool use_graphs = false;
   // a captured train step; its first kernel reads the caller's x directly
@@ -1398,7 +1401,11 @@ static bool use_update(const iwae_handle* h, const Plan& P) {
   return tiles <= kUpdMaxTiles && (int)h->dense.size() <= kUpdMaxJobs;
 }
 
-static int run_update(iwae_handle* h, const Plan& P, bool adam) {
+// part: 0 every layer, 1 all but the first encoder layer (sample rows), 2 the
+// first encoder layer (image rows; its backward may still be running when
+// part 1 starts on another stream)
+static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hipStream_t st = nullptr) {
+  if (!st) st = h->stream;
   const int L = h->L, M = P.Bimg * P.kS;
   struct WJ { int di; const Mat* A; const Mat* dZ; int rows; const float* ks; };
   std::vector<WJ> js;
@@ -1418,6 +1425,15 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam) {
   js.push_back({h->o1, &h->h[0], &h->ob.dY1, M, nullptr});
   js.push_back({h->o2, &h->ob.y1, &h->ob.dY2, M, nullptr});
   js.push_back({h->o3, &h->ob.y2, &h->ob.P, M, h->dpx});
+  if (part != 0) {
+    const StochL& S0 = h->enc[0];
+    std::vector<WJ> keep;
+    for (const WJ& w : js) {
+      const bool first = w.di == S0.l1 || w.di == S0.l2 || w.di == S0.head;
+      if (first == (part == 2)) keep.push_back(w);
+    }
+    js.swap(keep);
+  }
   if ((int)js.size() > kUpdMaxJobs) return fail(h, IWAE_EINVAL, "fused update: too many layers");
   // the long reductions first (dispatched first)
   std::stable_sort(js.begin(), js.end(), [](const WJ& x, const WJ& y) { return x.rows > y.rows; });
@@ -1445,8 +1461,8 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam) {
   a.param = h->params; a.m = h->adam_m; a.v = h->adam_v; a.grad = h->grad;
   a.fx_hi = h->fx_hi; a.fx_lo = h->fx_lo;
   a.state = &h->ds->adam; a.do_adam = adam ? 1 : 0;
-  HIPCHK(launch_update(h->stream, a));
-  if (adam) h->params_version++;
+  HIPCHK(launch_update(st, a));
+  if (adam && part != 1) h->params_version++;
   if (h->prof_kind == 15 && adam && !h->prof_have) {
     // replays repeat this step's update on scratch copies of the parameters,
     // moments and fragment-major copies: the model is untouched
@@ -1929,7 +1945,22 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   // weight gradients measured slower inside the captured graph: sequential).
   // Its image-row job also at small batches (B = 20: step 128.1 -> 126.4 us
   // against the row-block Gaussian backward + two few-row launches)
-  if (img || h->engine_img_bwd) CHK(tc_run(h, P, E, 3));
+  const bool img_bwd = img || h->engine_img_bwd;
+  if (use_update(h, P) && img_bwd && h->upd_split) {
+    // two branches: the update of every layer after the first encoder layer
+    // (its inputs are complete) beside the first layer's backward, then that
+    // layer's update
+    HIPCHK(hipEventRecord(h->ev_fork, h->stream));
+    HIPCHK(hipStreamWaitEvent(h->side_stream, h->ev_fork, 0));
+    CHK(run_update(h, P, adam, 1, h->side_stream));
+    CHK(tc_run(h, P, E, 3));
+    CHK(run_update(h, P, adam, 2));
+    HIPCHK(hipEventRecord(h->ev_join, h->side_stream));
+    HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+    if (adam) h->fx_version = h->params_version;
+    return IWAE_OK;
+  }
+  if (img_bwd) CHK(tc_run(h, P, E, 3));
   else CHK(fused_encoder_bwd(h, P, h->dlw, 0));
   if (use_update(h, P)) {
     // weight gradients, Adam and the fragment-major copies in one launch
@@ -2133,6 +2164,9 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   }
   hipError_t e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
   h->stream = h->own_stream;
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
   const size_t pb = (size_t)h->nparam_int * sizeof(float);
   // the row-block kernels fetch whole padded k ranges (up to 255 rows, or 256
   // floats of a row, past a matrix's end): keep that inside a zeroed tail
@@ -2176,6 +2210,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (const char* w = std::getenv("IWAE_UPD")) h->upd = std::atoi(w) != 0;              // A/B switch
   if (const char* w = std::getenv("IWAE_UPD_ROWS")) h->upd_rows = std::atoll(w);        // tuning knob
   if (const char* w = std::getenv("IWAE_UPD_DBG")) h->upd_dbg = std::atoi(w);           // timing ablations
+  if (const char* w = std::getenv("IWAE_UPD_SPLIT")) h->upd_split = std::atoi(w) != 0;  // A/B switch
   if (const char* w = std::getenv("IWAE_ENGINE")) h->engine = std::atoi(w) != 0;   // A/B switch
   if (const char* w = std::getenv("IWAE_TC_IMG")) h->engine_img = std::atoi(w) != 0;   // A/B switch
   if (const char* w = std::getenv("IWAE_TC_IMGBWD")) h->engine_img_bwd = std::atoi(w) != 0;   // A/B switch
@@ -2208,6 +2243,9 @@ void iwae_destroy(iwae_handle* h) {
   if (h->prof_scratch) (void)hipFree(h->prof_scratch);
   if (h->prof_adam) (void)hipFree(h->prof_adam);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+  if (h->side_stream) (void)hipStreamDestroy(h->side_stream);
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   delete h;
 }
 

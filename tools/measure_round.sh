@@ -14,5 +14,9 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
   python -u bench.py > $O/bench_prof.jsonl 2> $O/bench_prof.err || exit $?
 PMC_OUT=$O/pmc bash tools/pmc_passes.sh python -u bench.py --steps 20 --warmup 5 --no-nll --no-cpu --no-c0 \
   --no-large-batch || exit $?
-python tools/pmc_to_json.py $O/pmc "tc_kernel<" $O/pmc_traffic.json "tc_kernel forward (train engine, bf16x3)" max &&
-python tools/pmc_to_json.py $O/pmc "tc_kernel<" $O/pmc_traffic.json "tc_kernel backward (train engine, bf16x3)" min
+python tools/pmc_to_json.py $O/pmc "tc_kernel<" $O/pmc_traffic.json "tc_kernel forward (train engine, bf16x3)" rank:0 &&
+python tools/pmc_to_json.py $O/pmc "tc_kernel<" $O/pmc_traffic.json "tc_kernel backward (train engine, bf16x3)" rank:1 &&
+python tools/pmc_to_json.py $O/pmc "upd_kernel" $O/pmc_traffic.json "upd_kernel (weight gradients + Adam + FX copies, bf16x3)" max &&
+python tools/pmc_summary.py $O/pmc > $O/pmc_summary.txt &&
+PROF_OUT=$O/pstep bash tools/prof_step.sh > /dev/null
+T=$(find $O/prof -name "*kernel_trace.csv" | head -1); python tools/kernel_by_grid.py "$T" > $O/kernel_by_grid.txt

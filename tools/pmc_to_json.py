@@ -5,7 +5,7 @@ FETCH_SIZE is in KiB per dispatch and is doubled (gfx950 tallies a 128-B wide
 streaming request as 64 B: MI355X_MICROARCH.md, HBM section); WRITE_SIZE is
 taken as is (exact for 16-B-per-lane streaming stores).
 
-    python tools/pmc_to_json.py <pmc dir> <kernel name substring> <out.json> <label> [grid: threads | max | min]
+    python tools/pmc_to_json.py <pmc dir> <kernel name substring> <out.json> <label> [grid: threads | max | min | rank:n]
 
 The record is merged into out.json under `label` (the kernel label bench.py
 uses); the grid size separates launches of one kernel with different roles
@@ -23,6 +23,9 @@ rows = [r for f in glob.glob(os.path.join(root, "*", "**", "*counter_collection.
 if grid in ("max", "min"):
     sizes = {int(r["Grid_Size"]) for r in rows}
     grid = max(sizes) if grid == "max" else min(sizes)
+elif grid is not None and grid.startswith("rank:"):        # the n-th largest grid (0 = max)
+    sizes = sorted({int(r["Grid_Size"]) for r in rows}, reverse=True)
+    grid = sizes[int(grid[5:])]
 elif grid is not None:
     grid = int(grid)
 vals = {}
