@@ -350,6 +350,8 @@ struct UpdArgs {
   float* param; float* m; float* v; float* grad;
   __bf16* fx_hi; __bf16* fx_lo;
   const AdamState* state; int do_adam;
+  float gscale;                                       // gradient written as gscale * dW (data parallel: B_local)
+  float* tail; float tail_val;                        // data parallel: *tail = tail_val (B_local), or null
 };
 hipError_t launch_update(hipStream_t st, const UpdArgs& a);
 hipError_t upd_setup_attributes();
@@ -510,6 +512,8 @@ struct TcOp {
   float* dh; int ld_dh;       // GBWD_PRIOR: dL/dh of the target h
   int t0;                     // dense ops: first column tile (a job may run a column range [16 t0, N))
   int nslab; long long slab_stride;   // LOADSLAB: partial slabs at y + i * slab_stride ([rows][ld_y] each)
+  int img;                    // runs on the images of the workgroup's sample rows (rows b = row / kS)
+  int gsync;                  // reads global data an earlier op of this launch wrote: full barrier before it
 };
 struct TcJob {
   TcOp op[kTcMaxOps]; int nop;

@@ -167,6 +167,7 @@ struct iwae_handle {
   std::map<std::vector<long long>, TcRec> tc_plans;
   int engine = 1;                    // train step on the row-chain engine when it applies (iwae_set_path)
   int engine_img = 1;                // ... with the first encoder layer's l2 / head on its image-row jobs
+  int engine_fold0 = 0;              // ... its l2 / head folded into the forward jobs at small batches (env IWAE_TC_FOLD0)
   int engine_img_bwd = 1;            // ... their backward on the image-row job at small batches too (env IWAE_TC_IMGBWD)
   int tc_xcd = 1;                    // XCD-aware job placement of the engine launches (env IWAE_TC_XCD)
   int tc_bound = 1;                  // the train step's bound inside the engine's backward launch (env IWAE_TC_BOUND)
@@ -1390,12 +1391,13 @@ static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const
 }
 
 // Fused update (iwae_update.hip): every weight gradient over all the step's rows,
-// the gradient buffer, Adam and the FX / GX copies in one launch.  Single
-// process (the data-parallel merge needs the gradient before Adam), bf16x3
-// products, and up to upd_rows sample rows (one workgroup reduces a tile over
-// all rows: beyond that the split-K GEMM + Adam launches parallelise better).
+// the gradient buffer, Adam and the FX / GX copies in one launch (data
+// parallel: the gradient pass only, B_local-weighted, before the all-reduce),
+// bf16x3 products, and up to upd_rows sample rows (one workgroup reduces a
+// tile over all rows: beyond that the split-K GEMM + Adam launches parallelise
+// better).
 static bool use_update(const iwae_handle* h, const Plan& P) {
-  if (!h->upd || !h->x3 || h->dp_weighted || (long long)P.Bimg * P.kS > h->upd_rows) return false;
+  if (!h->upd || !h->x3 || (long long)P.Bimg * P.kS > h->upd_rows) return false;
   long long tiles = 0;
   for (const DenseL& d : h->dense) tiles += cdiv(d.fin + 1, 64) * cdiv(d.fout, 64);
   return tiles <= kUpdMaxTiles && (int)h->dense.size() <= kUpdMaxJobs;
@@ -1404,7 +1406,8 @@ static bool use_update(const iwae_handle* h, const Plan& P) {
 // part: 0 every layer, 1 all but the first encoder layer (sample rows), 2 the
 // first encoder layer (image rows; its backward may still be running when
 // part 1 starts on another stream)
-static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hipStream_t st = nullptr) {
+static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hipStream_t st = nullptr,
+                      float gscale = 1.f, float* tail = nullptr) {
   if (!st) st = h->stream;
   const int L = h->L, M = P.Bimg * P.kS;
   struct WJ { int di; const Mat* A; const Mat* dZ; int rows; const float* ks; };
@@ -1461,6 +1464,7 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hi
   a.param = h->params; a.m = h->adam_m; a.v = h->adam_v; a.grad = h->grad;
   a.fx_hi = h->fx_hi; a.fx_lo = h->fx_lo;
   a.state = &h->ds->adam; a.do_adam = adam ? 1 : 0;
+  a.gscale = gscale; a.tail = tail; a.tail_val = gscale;
   HIPCHK(launch_update(st, a));
   if (adam && part != 1) h->params_version++;
   if (h->prof_kind == 15 && adam && !h->prof_have) {
@@ -1561,6 +1565,32 @@ static size_t tc_layout(TcBuild& B, int rt) {
   return (size_t)off * sizeof(__bf16);
 }
 
+// The first encoder layer's l2 and head folded into a forward sample-row job
+// (small batches): every workgroup sums the input Dense's slabs of its images,
+// runs l2 and the head on those image rows and stores P0, which the job's
+// SAMPLE0 then reads (full barrier).  Buffers 0 / 1 are dead before SAMPLE0.
+static void tc_fold_first_layer(iwae_handle* h, const Plan& P, TcBuild& B) {
+  const StochL& S0 = h->enc[0];
+  auto ldF = [&](int di) { return h->dense[di].ldF; };
+  TcOp& ls = B.add(TC_LOADSLAB);
+  ls.img = 1;
+  ls.N = h->dense[S0.l1].fout; ls.out_buf = 0; ls.next_k = ldF(S0.l2);
+  ls.y = h->fslab; ls.ld_y = h->eb[0].y1.ld;
+  ls.nslab = enc0_nslab(h, P.Bimg); ls.slab_stride = (long long)P.Bimg * h->eb[0].y1.ld;
+  ls.out = h->eb[0].y1.p; ls.ld_out = h->eb[0].y1.ld;
+  B.need(0, ls.next_k);
+  TcOp& a = tc_dense_op(h, B, TC_TANH, S0.l2, false, 0, 1, ldF(S0.head));
+  a.img = 1;
+  a.out = h->eb[0].y2.p; a.ld_out = h->eb[0].y2.ld;
+  TcOp& c = tc_head_op(h, B, TC_HEADP, S0.head, 1, -1, S0.d, 0);
+  c.img = 1;
+  c.out = h->eb[0].P.p; c.ld_out = h->eb[0].P.ld;
+}
+
+static bool use_fold0(const iwae_handle* h, const Plan& P) {
+  return h->engine_fold0 && smallm_ok(h, P.Bimg) && h->L >= 1;
+}
+
 static std::vector<long long> tc_key(const Plan& P, int which) {
   return {which, P.Bimg, P.Bsplit, P.kS};
 }
@@ -1574,6 +1604,7 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
   const int L = h->L, kS = P.kS;
   auto r32 = [](int x) { return (x + 31) & ~31; };
   std::vector<TcBuild> jobs;
+  const bool fold0 = which == 0 && use_fold0(h, P);
   auto ldF = [&](int di) { return h->dense[di].ldF; };
   auto ldG = [&](int di) { return h->dense[di].ldG; };
   if (which == 0) {
@@ -1582,7 +1613,9 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
       TcBuild B;
       const int bP = L - 1, bQ = L;
       auto hbuf = [&](int i) { return i == L - 1 ? bP : i; };
+      if (fold0) tc_fold_first_layer(h, P, B);
       TcOp& s0 = B.add(TC_SAMPLE0);
+      s0.gsync = fold0;
       s0.d = h->enc[0].d; s0.layer = 0; s0.acc = 1; s0.stdnormal = 0;
       s0.P = h->eb[0].P.p; s0.ld_P = h->eb[0].P.ld; s0.P_div = kS;
       s0.h = h->h[0].p; s0.ld_h = h->h[0].ld; s0.eps = h->eps_st[0].p; s0.ld_eps = h->eps_st[0].ld;
@@ -1623,7 +1656,9 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
     for (int part = 0; part < nsplit; ++part) {
       const bool first = part == 0;
       TcBuild B;
+      if (fold0) tc_fold_first_layer(h, P, B);
       TcOp& s0 = B.add(TC_SAMPLE0);
+      s0.gsync = fold0;
       s0.d = h->enc[0].d; s0.layer = 0; s0.acc = L == 1 && first; s0.stdnormal = L == 1;
       s0.P = h->eb[0].P.p; s0.ld_P = h->eb[0].P.ld; s0.P_div = kS;
       if (L == 1 && first) {
@@ -1788,6 +1823,8 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
           if (op.kind > TC_LAST_DENSE) continue;
           const int kin = op.kind == TC_TGRAD || op.kind == TC_LIN ? op.K : op.K - 1;
           const int nout = op.kind == TC_SAMPLE || op.kind == TC_PRIOR ? 2 * op.d : op.N;
+          // (a folded image-row op: its images once, however many workgroups recompute them)
+          if (op.img) { if (j == 0) rec.flop += 2.0 * (double)P.Bimg * kin * nout; continue; }
           rec.flop += 2.0 * (double)rows * kin * nout;
         }
       }
@@ -1930,6 +1967,9 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
     // first encoder layer: input Dense (few-row / split-K), then its image-row engine job
     CHK(enc0_forward(h, P, true));
     CHK(tc_run(h, P, E, 2));
+  } else if (use_fold0(h, P)) {
+    // input Dense only: its l2 and head run inside the forward launch's jobs
+    CHK(enc0_forward(h, P, true));
   } else {
     CHK(enc0_forward(h, P));
   }
@@ -1946,7 +1986,7 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   // Its image-row job also at small batches (B = 20: step 128.1 -> 126.4 us
   // against the row-block Gaussian backward + two few-row launches)
   const bool img_bwd = img || h->engine_img_bwd;
-  if (use_update(h, P) && img_bwd && h->upd_split) {
+  if (use_update(h, P) && img_bwd && h->upd_split && !h->dp_weighted) {
     // two branches: the update of every layer after the first encoder layer
     // (its inputs are complete) beside the first layer's backward, then that
     // layer's update
@@ -1962,6 +2002,21 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   }
   if (img_bwd) CHK(tc_run(h, P, E, 3));
   else CHK(fused_encoder_bwd(h, P, h->dlw, 0));
+  if (use_update(h, P) && h->dp_weighted) {
+    // data parallel: the fused gradient pass (B_local * g, B_local in the
+    // tail), the all-reduce, then Adam and the fragment-major copies
+    float* tail = h->grad + h->nparam_int;
+    CHK(run_update(h, P, false, 0, nullptr, (float)P.B, tail));
+    if (!adam) return IWAE_OK;
+    if (!h->comm) return fail(h, IWAE_EINVAL, "data parallel without a library communicator");
+    if (ncclAllReduce(h->grad, h->grad, (size_t)h->nparam_int + 4, ncclFloat32, ncclSum, h->comm, h->stream) !=
+        ncclSuccess)
+      return fail(h, IWAE_EHIP, "ncclAllReduce of the gradient failed");
+    CHK(run_adam(h, false, true, true, 0.f, false, tail));
+    CHK(run_fx(h));
+    h->fx_version = h->params_version;
+    return IWAE_OK;
+  }
   if (use_update(h, P)) {
     // weight gradients, Adam and the fragment-major copies in one launch
     CHK(run_update(h, P, adam));
@@ -2214,6 +2269,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (const char* w = std::getenv("IWAE_ENGINE")) h->engine = std::atoi(w) != 0;   // A/B switch
   if (const char* w = std::getenv("IWAE_TC_IMG")) h->engine_img = std::atoi(w) != 0;   // A/B switch
   if (const char* w = std::getenv("IWAE_TC_IMGBWD")) h->engine_img_bwd = std::atoi(w) != 0;   // A/B switch
+  if (const char* w = std::getenv("IWAE_TC_FOLD0")) h->engine_fold0 = std::atoi(w) != 0;     // A/B switch
   if (const char* w = std::getenv("IWAE_TC_XCD")) h->tc_xcd = std::atoi(w) != 0;       // A/B switch
   if (const char* w = std::getenv("IWAE_TC_BOUND")) h->tc_bound = std::atoi(w) != 0;   // A/B switch
   if (e != hipSuccess) {

@@ -998,8 +998,17 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
       g_tc_ptrace[(tr * 32 + s) * 4] = wall_clock64();
     }
 #endif
+    // image-row ops (the first encoder layer folded into a sample-row job) run on
+    // the images of this workgroup's rows
+    int r0 = row0, nr = nrows;
+    if (S.img) {
+      r0 = row0 / A.kS;
+      nr = (row0 + nrows - 1) / A.kS - r0 + 1;
+    }
     COp* Sn = nullptr;
-    if (s + 1 < J.nop && J.op[s + 1].kind <= TC_LAST_DENSE && !tc_needs_global(J.op[s + 1].kind)) Sn = &J.op[s + 1];
+    if (s + 1 < J.nop && J.op[s + 1].kind <= TC_LAST_DENSE && !tc_needs_global(J.op[s + 1].kind) &&
+        !J.op[s + 1].gsync)
+      Sn = &J.op[s + 1];
     int nx = 0;             // elementwise op: requests the next op's first units
     if (kind > TC_LAST_DENSE && Sn) nx = tc_prefetch(*Sn, F);
 
@@ -1017,7 +1026,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
       case TC_BERN:
       case TC_TGRAD:
       case TC_LIN:
-      case TC_HEADP: nx = tc_dense<RT>(A, J, S, kind, base, Rw, row0, nrows, F, npre, Sn, UTR); break;
+      case TC_HEADP: nx = tc_dense<RT>(A, J, S, kind, base, Rw, r0, nr, F, npre, Sn, UTR); break;
 #ifdef IWAE_TC_SKIPELEM    // timing experiment only
       default: break;
 #else
@@ -1025,7 +1034,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
       case TC_GBWD_PRIOR: tc_gbwd<RT, TC_GBWD_PRIOR>(A, J, S, row0, nrows); break;
       case TC_GBWD_ENC: tc_gbwd<RT, TC_GBWD_ENC>(A, J, S, row0, nrows); break;
       case TC_LOADG: tc_loadg<RT>(A, J, S, row0, nrows); break;
-      case TC_LOADSLAB: tc_loadslab<RT>(J, S, row0, nrows); break;
+      case TC_LOADSLAB: tc_loadslab<RT>(J, S, r0, nr); break;
       default: tc_gbwd0<RT>(A, J, S, row0, nrows); break;
 #endif
     }
@@ -1033,7 +1042,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
     if (tr >= 0 && 3 + 2 * s < 64) g_tc_trace[tr * 64 + 3 + 2 * s] = wall_clock64();
 #endif
     npre = nx;
-    if (s + 1 < J.nop && !tc_needs_global(J.op[s + 1].kind)) tc_lds_barrier();
+    if (s + 1 < J.nop && !tc_needs_global(J.op[s + 1].kind) && !J.op[s + 1].gsync) tc_lds_barrier();
     else __syncthreads();
   }
   if (!J.logq && !J.logp && !J.bern) return;

@@ -328,13 +328,15 @@ __global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
     }
     g[4 * q] = s.x; g[4 * q + 1] = s.y; g[4 * q + 2] = s.z; g[4 * q + 3] = s.w;
   }
-  // gradient buffer (get_gradients, the SNR harness)
+  // gradient buffer (get_gradients, the SNR harness; data parallel: B_local
+  // times the gradient, all-reduced before Adam)
+  if (a.tail && b == 0 && t == 0) *a.tail = a.tail_val;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int c = j0 + ej + 4 * q;
     if (erow && c < J.ldw)
       *reinterpret_cast<float4*>(a.grad + J.off + (long long)(i0 + ei) * J.ldw + c) =
-          make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+          make_float4(a.gscale * g[4 * q], a.gscale * g[4 * q + 1], a.gscale * g[4 * q + 2], a.gscale * g[4 * q + 3]);
   }
   if (!a.do_adam) return;
 
