@@ -340,13 +340,14 @@ struct UpdJob {
   long long fx_off; int fx_steps, head_d;             // FX copy (fx_off < 0: none, GX neither)
   long long gx_off; int gx_steps;
   int tiles_m, tiles_n, tile0;                        // tiles [tile0, tile0 + tiles_m * tiles_n), column-major
+  int tn;                                             // tile columns: 64, or 32
   int dbg;                                            // timing ablations (env IWAE_UPD_DBG): 1 no MFMA, 2 no staging, 4 no loads
 };
 constexpr int kUpdMaxJobs = 24, kUpdMaxTiles = 512;
 struct UpdArgs {
   UpdJob job[kUpdMaxJobs]; int njobs;
   unsigned char tile_job[kUpdMaxTiles];               // job of each tile
-  int ntiles, per_xcd;                                // grid = 8 * per_xcd; tile = xcd * per_xcd + slot
+  int ntiles, nheavy, per_xcd, per_xcd2;              // tiles [0, nheavy): per_xcd per XCD, the rest per_xcd2 per XCD
   float* param; float* m; float* v; float* grad;
   __bf16* fx_hi; __bf16* fx_lo;
   const AdamState* state; int do_adam;

@@ -176,6 +176,7 @@ struct iwae_handle {
   long long upd_rows = 4096;         // ... up to this many sample rows per step (env IWAE_UPD_ROWS)
   int upd_dbg = 0;                   // timing ablations of that launch (env IWAE_UPD_DBG; wrong results)
   int upd_split = 0;                 // ... split over two graph branches (env IWAE_UPD_SPLIT)
+  int upd_tn32 = 0;                  // ... sample-row layers in 64 x 32 tiles (env IWAE_UPD_TN32)
   // graphs
   bool use_graphs = false;
   // a captured train step; its first kernel reads the caller's x directly
@@ -1399,7 +1400,7 @@ static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const
 static bool use_update(const iwae_handle* h, const Plan& P) {
   if (!h->upd || !h->x3 || (long long)P.Bimg * P.kS > h->upd_rows) return false;
   long long tiles = 0;
-  for (const DenseL& d : h->dense) tiles += cdiv(d.fin + 1, 64) * cdiv(d.fout, 64);
+  for (const DenseL& d : h->dense) tiles += cdiv(d.fin + 1, 64) * cdiv(d.fout, h->upd_tn32 ? 32 : 64);
   return tiles <= kUpdMaxTiles && (int)h->dense.size() <= kUpdMaxJobs;
 }
 
@@ -1451,7 +1452,10 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hi
     const bool fx = w.di != h->enc[0].l1;       // the input layer has no fragment-major copies
     J.fx_off = fx ? d.fx_off : -1; J.fx_steps = d.fx_steps; J.head_d = d.head_d;
     J.gx_off = d.gx_off; J.gx_steps = d.gx_steps;
-    J.tiles_m = (int)cdiv(d.fin + 1, 64); J.tiles_n = (int)cdiv(d.fout, 64);
+    // sample-row layers in 64 x 32 tiles (up_tn32): twice the workgroups, each
+    // with half the MFMAs and a quarter less staging over the same 1000+ rows
+    J.tn = (h->upd_tn32 && w.rows == M) ? 32 : 64;
+    J.tiles_m = (int)cdiv(d.fin + 1, 64); J.tiles_n = (int)cdiv(d.fout, J.tn);
     J.tile0 = tiles;
     J.dbg = h->upd_dbg;
     tiles += J.tiles_m * J.tiles_n;
@@ -1460,7 +1464,12 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hi
     flop += 2.0 * w.rows * (d.fin + 1) * d.fout;
   }
   a.ntiles = tiles;
-  a.per_xcd = (int)cdiv(tiles, 8);
+  int heavy = 0;                                // the jobs are sorted by rows: the sample-row jobs' tiles first
+  for (int j = 0; j < a.njobs; ++j)
+    if (a.job[j].rows == js[0].rows) heavy = a.job[j].tile0 + a.job[j].tiles_m * a.job[j].tiles_n;
+  a.nheavy = heavy;
+  a.per_xcd = (int)cdiv(heavy, 8);
+  a.per_xcd2 = (int)cdiv(tiles - heavy, 8);
   a.param = h->params; a.m = h->adam_m; a.v = h->adam_v; a.grad = h->grad;
   a.fx_hi = h->fx_hi; a.fx_lo = h->fx_lo;
   a.state = &h->ds->adam; a.do_adam = adam ? 1 : 0;
@@ -2266,6 +2275,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (const char* w = std::getenv("IWAE_UPD_ROWS")) h->upd_rows = std::atoll(w);        // tuning knob
   if (const char* w = std::getenv("IWAE_UPD_DBG")) h->upd_dbg = std::atoi(w);           // timing ablations
   if (const char* w = std::getenv("IWAE_UPD_SPLIT")) h->upd_split = std::atoi(w) != 0;  // A/B switch
+  if (const char* w = std::getenv("IWAE_UPD_TN32")) h->upd_tn32 = std::atoi(w) != 0;    // A/B switch
   if (const char* w = std::getenv("IWAE_ENGINE")) h->engine = std::atoi(w) != 0;   // A/B switch
   if (const char* w = std::getenv("IWAE_TC_IMG")) h->engine_img = std::atoi(w) != 0;   // A/B switch
   if (const char* w = std::getenv("IWAE_TC_IMGBWD")) h->engine_img_bwd = std::atoi(w) != 0;   // A/B switch

@@ -44,7 +44,6 @@ constexpr int UP_RI = 128;                  // sample rows per iteration (4 k st
 constexpr int UP_S = 72;                    // dwords per LDS row: 128 bf16 + 16 bf16 pad
 constexpr int UP_PLANE = 64 * UP_S;         // dwords per plane
 constexpr int UP_BUF = 4 * UP_PLANE;        // X hi, X lo, dZ hi, dZ lo
-constexpr int UP_PS = 68;                   // f32 stride of the epilogue tiles
 constexpr int UP_G = 8;                     // iterations per unrolled group (1024 rows)
 
 extern __shared__ __attribute__((aligned(16))) float ups[];
@@ -60,24 +59,34 @@ __device__ __forceinline__ int up_cq(int t) { return t & 15; }
 
 // (ext_vector_type registers: with HIP's float4 struct the compiler kept the
 // sets in scratch memory)
+typedef float up_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 up_bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned up_u32x4 __attribute__((ext_vector_type(4)));
+// one iteration's loads of one thread: X rows 8 rg .. + 7 at columns 4 cq ..
+// + 3, dZ the same rows at TN / 16 columns (TN = 64: 4, TN = 32: 2), the row scale
+template <int TN> struct UpZ { typedef up_f32x4 type; };
+template <> struct UpZ<32> { typedef up_f32x2 type; };
+template <int TN>
 struct UpRegs {
-  up_f32x4 x[8], z[8];
+  up_f32x4 x[8];
+  typename UpZ<TN>::type z[8];
   up_f32x4 k0, k1;
 };
 __device__ __forceinline__ up_f32x4 up_ld4(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_bit_cast(up_f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
+__device__ __forceinline__ up_f32x2 up_ld2(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(up_f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
 
-typedef float up_f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 up_bf16x2 __attribute__((ext_vector_type(2)));
-typedef unsigned up_u32x4 __attribute__((ext_vector_type(4)));
-// Column c of 8 loaded rows -> bf16 hi / lo planes (hi = RNE(v), lo =
+// Column C of 8 loaded rows -> bf16 hi / lo planes (hi = RNE(v), lo =
 // RNE(v - hi)), pairwise: one v_cvt_pk_bf16_f32 per pair and plane, the hi
 // pair widened back with a shift and a mask, the residual by one packed
-// subtract; SCALE multiplies row q by k[q] first.  (Pairs are built straight
-// from the float4 components: an intermediate float[8] ends up in scratch.)
-template <int C, bool SCALE>
-__device__ __forceinline__ void up_split_col(const up_f32x4 (&a)[8], const UpRegs& R, up_u32x4& h, up_u32x4& l) {
+// subtract; SCALE multiplies row q by the row scale first.  (Pairs are built
+// straight from the vector components: an intermediate float[8] ends up in
+// scratch.)
+template <int C, bool SCALE, typename V, int TN>
+__device__ __forceinline__ void up_split_col(const V (&a)[8], const UpRegs<TN>& R, up_u32x4& h, up_u32x4& l) {
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     up_f32x2 x = {a[2 * p][C], a[2 * p + 1][C]};
@@ -92,35 +101,41 @@ __device__ __forceinline__ void up_split_col(const up_f32x4 (&a)[8], const UpReg
     l[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, up_bf16x2));
   }
 }
-// stage column C of both operands (X as is, dZ times the row scale)
-template <int C>
-__device__ __forceinline__ void up_stage_col(const UpRegs& R, float* wbuf, int cq, int rg) {
-  const int o = up_off(4 * cq + C, rg);
+// stage column C of X (plane row 4 cq + C) and, for C < TN / 16, of dZ times
+// the row scale (plane row (TN / 16) cq + C)
+template <int C, int TN>
+__device__ __forceinline__ void up_stage_col(const UpRegs<TN>& R, float* wbuf, int cq, int rg) {
   up_u32x4 h, l;
+  const int o = up_off(4 * cq + C, rg);
   up_split_col<C, false>(R.x, R, h, l);
   *reinterpret_cast<up_u32x4*>(wbuf + o) = h;
   *reinterpret_cast<up_u32x4*>(wbuf + UP_PLANE + o) = l;
-  up_split_col<C, true>(R.z, R, h, l);
-  *reinterpret_cast<up_u32x4*>(wbuf + 2 * UP_PLANE + o) = h;
-  *reinterpret_cast<up_u32x4*>(wbuf + 3 * UP_PLANE + o) = l;
+  if (C < TN / 16) {
+    const int oz = up_off((TN / 16) * cq + C, rg);
+    up_split_col<C < TN / 16 ? C : 0, true>(R.z, R, h, l);
+    *reinterpret_cast<up_u32x4*>(wbuf + 2 * UP_PLANE + oz) = h;
+    *reinterpret_cast<up_u32x4*>(wbuf + 3 * UP_PLANE + oz) = l;
+  }
 }
-__device__ __forceinline__ void up_stage_c(int c, const UpRegs& R, float* wbuf, int cq, int rg) {
+template <int TN>
+__device__ __forceinline__ void up_stage_c(int c, const UpRegs<TN>& R, float* wbuf, int cq, int rg) {
   if (c == 0) up_stage_col<0>(R, wbuf, cq, rg);
   else if (c == 1) up_stage_col<1>(R, wbuf, cq, rg);
   else if (c == 2) up_stage_col<2>(R, wbuf, cq, rg);
   else up_stage_col<3>(R, wbuf, cq, rg);
 }
 
-// Per-thread byte offsets of its first row's 4 columns within an iteration
+// Per-thread byte offsets of its first row's columns within an iteration
 // (row q adds q rows), fixed for the whole reduction: the buffer resource
 // moves instead (base and range advanced by 128 rows per iteration in scalar
 // registers), so rows past the last one fall outside the range and read 0.
 struct UpOff {
   unsigned x, z, k;
 };
+template <int TN>
 __device__ __forceinline__ UpOff up_offsets(const UpdJob& J, int i0, int j0) {
   const int t = threadIdx.x, rg = up_rg(t), cq = up_cq(t);
-  const int ci = i0 + 4 * cq, cj = j0 + 4 * cq;
+  const int ci = i0 + 4 * cq, cj = j0 + (TN / 16) * cq;
   const bool okx = ci < J.lda && !(J.dbg & 4), okz = cj < J.ldb && !(J.dbg & 4);
   UpOff o;
   o.x = okx ? (unsigned)(8 * rg * J.lda + ci) * 4u : kOOB;     // kOOB + 7 rows stays out of range
@@ -129,7 +144,8 @@ __device__ __forceinline__ UpOff up_offsets(const UpdJob& J, int i0, int j0) {
   return o;
 }
 
-__device__ __forceinline__ void up_load(const UpdJob& J, const UpOff& O, int it, UpRegs& R) {
+template <int TN>
+__device__ __forceinline__ void up_load(const UpdJob& J, const UpOff& O, int it, UpRegs<TN>& R) {
   const int r0 = it * UP_RI;
   const unsigned left = J.rows > r0 ? (unsigned)(J.rows - r0) : 0u;
   const __amdgpu_buffer_rsrc_t ra = buf_rsrc(J.A + (size_t)r0 * J.lda, left * (unsigned)J.lda * 4u);
@@ -138,7 +154,8 @@ __device__ __forceinline__ void up_load(const UpdJob& J, const UpOff& O, int it,
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     R.x[q] = up_ld4(ra, O.x + q * sx);
-    R.z[q] = up_ld4(rz, O.z + q * sz);
+    if constexpr (TN == 64) R.z[q] = up_ld4(rz, O.z + q * sz);
+    else R.z[q] = up_ld2(rz, O.z + q * sz);
   }
   // dZ row scale (dpx for the output layer, a ones vector otherwise); rows
   // past the last read 0, which also zeroes dZ's stale rows there
@@ -147,51 +164,49 @@ __device__ __forceinline__ void up_load(const UpdJob& J, const UpOff& O, int it,
   R.k1 = up_ld4(rk, O.k + 16u);
 }
 
-// registers -> LDS (transposed, split): column c of the thread's 4 becomes one
-// 8-row k-contiguous chunk per plane
-__device__ __forceinline__ void up_stage(const UpdJob& J, const UpRegs& R, float* buf) {
+// registers -> LDS (transposed, split)
+template <int TN>
+__device__ __forceinline__ void up_stage(const UpRegs<TN>& R, float* buf) {
   const int t = threadIdx.x, rg = up_rg(t), cq = up_cq(t);
 #pragma unroll
   for (int c = 0; c < 4; ++c) up_stage_c(c, R, buf, cq, rg);
 }
 
 // One iteration's multiply (rbuf) with the next iteration's staging (R -> wbuf)
-// interleaved: the fragments are read first, then per column c of the thread's
-// four the split + LDS writes of that column sit between the MFMAs of
-// accumulator column sj = c, so the matrix core runs while the VALU splits.
-__device__ __forceinline__ void up_mul_stage(const UpdJob& J, const float* rbuf, float* wbuf, const UpRegs& R,
-                                             bool stage, up_f32x4 (&acc)[4][4]) {
+// interleaved: the B fragments are read first, then per chunk c the A
+// fragments of row tile c + 1 are requested, column c of the staging is split
+// and written, and the MFMAs of accumulator row tile si = c run, so the matrix
+// core works while the VALU splits.
+template <int TN>
+__device__ __forceinline__ void up_mul_stage(const float* rbuf, float* wbuf, const UpRegs<TN>& R, bool stage,
+                                             up_f32x4 (&acc)[4][TN / 16]) {
+  constexpr int NJ = TN / 16;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int t = threadIdx.x, rg = up_rg(t), cq = up_cq(t);
   const int blk = 4 * w + (lane >> 4);
-  constexpr bool mul = true;
-  up_bf16x8 ah[4], al[4], bh[2], bl[2];
-  auto read_b = [&](int c) __attribute__((always_inline)) {
+  up_bf16x8 ah[2], al[2], bh[NJ], bl[NJ];
+  auto read_a = [&](int c) __attribute__((always_inline)) {
     const int o = up_off(16 * c + (lane & 15), blk);
-    bh[c & 1] = *reinterpret_cast<const up_bf16x8*>(rbuf + 2 * UP_PLANE + o);
-    bl[c & 1] = *reinterpret_cast<const up_bf16x8*>(rbuf + 3 * UP_PLANE + o);
+    ah[c & 1] = *reinterpret_cast<const up_bf16x8*>(rbuf + o);
+    al[c & 1] = *reinterpret_cast<const up_bf16x8*>(rbuf + UP_PLANE + o);
   };
-  if (mul) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int o = up_off(16 * s + (lane & 15), blk);
-      ah[s] = *reinterpret_cast<const up_bf16x8*>(rbuf + o);
-      al[s] = *reinterpret_cast<const up_bf16x8*>(rbuf + UP_PLANE + o);
-    }
-    read_b(0);
+  for (int s = 0; s < NJ; ++s) {
+    const int o = up_off(16 * s + (lane & 15), blk);
+    bh[s] = *reinterpret_cast<const up_bf16x8*>(rbuf + 2 * UP_PLANE + o);
+    bl[s] = *reinterpret_cast<const up_bf16x8*>(rbuf + 3 * UP_PLANE + o);
   }
+  read_a(0);
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    if (mul && c + 1 < 4) read_b(c + 1);          // next column's B fragments (the other pair)
+    if (c + 1 < 4) read_a(c + 1);          // next row tile's A fragments (the other pair)
     if (stage) up_stage_c(c, R, wbuf, cq, rg);
-    if (mul) {
 #pragma unroll
-      for (int si = 0; si < 4; ++si) acc[si][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[si], bh[c & 1], acc[si][c], 0, 0, 0);
+    for (int sj = 0; sj < NJ; ++sj) acc[c][sj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[c & 1], bh[sj], acc[c][sj], 0, 0, 0);
 #pragma unroll
-      for (int si = 0; si < 4; ++si) acc[si][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[si], bl[c & 1], acc[si][c], 0, 0, 0);
+    for (int sj = 0; sj < NJ; ++sj) acc[c][sj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[c & 1], bl[sj], acc[c][sj], 0, 0, 0);
 #pragma unroll
-      for (int si = 0; si < 4; ++si) acc[si][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[si], bh[c & 1], acc[si][c], 0, 0, 0);
-    }
+    for (int sj = 0; sj < NJ; ++sj) acc[c][sj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[c & 1], bh[sj], acc[c][sj], 0, 0, 0);
   }
 }
 
@@ -203,26 +218,21 @@ __device__ __forceinline__ int up_fx_pos(int j, int head_d) {
   return 8 * (jj >> 2) + (j < head_d ? 0 : 4) + (jj & 3);
 }
 
-__global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
-  // tile of this workgroup: consecutive tiles (sharing an operand slice) on one XCD
-  const int b = blockIdx.x;
-  const int T = (b & 7) * a.per_xcd + (b >> 3);
-  if ((b >> 3) >= a.per_xcd || T >= a.ntiles) return;
-  const int jb = a.tile_job[T];
-  const UpdJob& J = a.job[jb];
-  // Adam constants (state->t was advanced for this step by the bound kernel),
-  // read now: scalar loads, in flight during the reduction
-  const AdamState st = *a.state;
-  const int lt = T - J.tile0, tn = lt / J.tiles_m, tm = lt - tn * J.tiles_m;
-  const int i0 = 64 * tm, j0 = 64 * tn;
+// One 64 x TN tile (TN = 64, or 32 for the sample-row layers: more
+// workgroups, half the MFMA and a quarter less staging per workgroup).
+template <int TN>
+__device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, const AdamState& st, int b, int lt) {
+  constexpr int NJ = TN / 16, EJ = TN / 4, PS = TN + 4;
+  const int tn = lt / J.tiles_m, tm = lt - tn * J.tiles_m;
+  const int i0 = 64 * tm, j0 = TN * tn;
   const int t = threadIdx.x;
   const int M = J.fin + 1;
 
-  up_f32x4 acc[4][4];
+  up_f32x4 acc[4][NJ];
 #pragma unroll
   for (int si = 0; si < 4; ++si)
 #pragma unroll
-    for (int sj = 0; sj < 4; ++sj) acc[si][sj] = up_f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int sj = 0; sj < NJ; ++sj) acc[si][sj] = up_f32x4{0.f, 0.f, 0.f, 0.f};
 
   // groups of UP_G iterations, fully unrolled: the register sets R0 / R1 are
   // never carried around a loop (a loop-carried set is renamed at the back
@@ -231,18 +241,17 @@ __global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
   const int ngrp = (J.dbg & 64) ? 0 : (J.rows + UP_G * UP_RI - 1) / (UP_G * UP_RI);
   float* buf0 = ups;
   float* buf1 = ups + UP_BUF;
-  const UpOff O = up_offsets(J, i0, j0);
-  const int ei = t >> 2, ej = 16 * (t & 3);
+  const UpOff O = up_offsets<TN>(J, i0, j0);
+  // epilogue elements: row ei, columns ej .. ej + EJ - 1
+  const int ei = t >> 2, ej = EJ * (t & 3);
   const bool erow = i0 + ei < M;
-  float4 pp[4], mm[4], vv[4];
-  // Adam operands of the epilogue's elements (row ei, columns ej .. ej + 15),
-  // requested behind the first two iterations' loads (waiting for them then
-  // never waits for those)
+  float4 pp[EJ / 4], mm[EJ / 4], vv[EJ / 4];
+  // Adam operands of the epilogue's elements
   auto adam_prefetch = [&]() __attribute__((always_inline)) {
     const __amdgpu_buffer_rsrc_t rp = buf_rsrc(a.param + J.off), rm = buf_rsrc(a.m + J.off),
                                  rv = buf_rsrc(a.v + J.off);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < EJ / 4; ++q) {
       const int c = j0 + ej + 4 * q;
       const unsigned off = (a.do_adam && erow && c < J.ldw) ? (unsigned)((i0 + ei) * J.ldw + c) * 4u : kOOB;
       pp[q] = bld4(rp, off); mm[q] = bld4(rm, off); vv[q] = bld4(rv, off);
@@ -258,44 +267,45 @@ __global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
   // followed by another (stage / request across the boundary).
   // (the two sets are named explicitly per step: a reference chosen at run
   // time would put them in scratch memory)
-  auto step = [&](int u, const float* rbuf, float* wbuf, UpRegs& Rn, int it0, bool tail) __attribute__((always_inline)) {
+  auto step = [&](int u, const float* rbuf, float* wbuf, UpRegs<TN>& Rn, int it0, bool tail)
+                  __attribute__((always_inline)) {
     const bool more = u + 1 < UP_G || tail;
-    up_mul_stage(J, rbuf, wbuf, Rn, more, acc);
+    up_mul_stage<TN>(rbuf, wbuf, Rn, more, acc);
     __builtin_amdgcn_sched_barrier(0);
-    if (u + 3 < UP_G || tail) up_load(J, O, it0 + u + 3, Rn);
+    if (u + 3 < UP_G || tail) up_load<TN>(J, O, it0 + u + 3, Rn);
     // the Adam operands once the last rows are requested (their registers
     // would otherwise crowd out the load sets for the whole reduction)
     if (!tail && u == UP_G - 3) adam_prefetch();
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   };
-  auto group = [&](UpRegs& R0, UpRegs& R1, int it0, bool tail) __attribute__((always_inline)) {
+  auto group = [&](UpRegs<TN>& R0, UpRegs<TN>& R1, int it0, bool tail) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < UP_G; u += 2) {
       step(u, buf0, buf1, R1, it0, tail);
       step(u + 1, buf1, buf0, R0, it0, tail);
     }
   };
-  auto start = [&](UpRegs& R0, UpRegs& R1) __attribute__((always_inline)) {
-    up_load(J, O, 0, R0);
+  auto start = [&](UpRegs<TN>& R0, UpRegs<TN>& R1) __attribute__((always_inline)) {
+    up_load<TN>(J, O, 0, R0);
     __builtin_amdgcn_sched_barrier(0);
-    up_load(J, O, 1, R1);
+    up_load<TN>(J, O, 1, R1);
     __builtin_amdgcn_sched_barrier(0);
-    up_stage(J, R0, buf0);
+    up_stage<TN>(R0, buf0);
     __builtin_amdgcn_sched_barrier(0);
-    up_load(J, O, 2, R0);
+    up_load<TN>(J, O, 2, R0);
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   };
   if (ngrp == 1) {
     // straight-line (up to 1024 rows): no loop-carried register set, so no
     // renaming copy drains the loads in flight
-    UpRegs R0, R1;
+    UpRegs<TN> R0, R1;
     start(R0, R1);
     group(R0, R1, 0, false);
   } else if (ngrp > 1) {
     // the sets are carried into the next group: renamed once per 1024 rows
-    UpRegs R0, R1;
+    UpRegs<TN> R0, R1;
     start(R0, R1);
     for (int gi = 0; gi < ngrp; ++gi) group(R0, R1, gi * UP_G, true);
     adam_prefetch();
@@ -308,22 +318,22 @@ __global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
   // the four waves' tiles -> LDS, summed in wave order
   {
     const int lane = t & 63, w = t >> 6;
-    float* part = ups + w * 64 * UP_PS;
+    float* part = ups + w * 64 * PS;
 #pragma unroll
     for (int si = 0; si < 4; ++si)
 #pragma unroll
-      for (int sj = 0; sj < 4; ++sj)
+      for (int sj = 0; sj < NJ; ++sj)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) part[(16 * si + 4 * (lane >> 4) + q) * UP_PS + 16 * sj + (lane & 15)] = acc[si][sj][q];
+        for (int q = 0; q < 4; ++q) part[(16 * si + 4 * (lane >> 4) + q) * PS + 16 * sj + (lane & 15)] = acc[si][sj][q];
   }
   __syncthreads();
-  float g[16];
+  float g[EJ];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float4 s = *reinterpret_cast<const float4*>(ups + ei * UP_PS + ej + 4 * q);
+  for (int q = 0; q < EJ / 4; ++q) {
+    float4 s = *reinterpret_cast<const float4*>(ups + ei * PS + ej + 4 * q);
 #pragma unroll
     for (int w = 1; w < UP_NW; ++w) {
-      const float4 u = *reinterpret_cast<const float4*>(ups + w * 64 * UP_PS + ei * UP_PS + ej + 4 * q);
+      const float4 u = *reinterpret_cast<const float4*>(ups + w * 64 * PS + ei * PS + ej + 4 * q);
       s.x += u.x; s.y += u.y; s.z += u.z; s.w += u.w;
     }
     g[4 * q] = s.x; g[4 * q + 1] = s.y; g[4 * q + 2] = s.z; g[4 * q + 3] = s.w;
@@ -332,7 +342,7 @@ __global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
   // times the gradient, all-reduced before Adam)
   if (a.tail && b == 0 && t == 0) *a.tail = a.tail_val;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < EJ / 4; ++q) {
     const int c = j0 + ej + 4 * q;
     if (erow && c < J.ldw)
       *reinterpret_cast<float4*>(a.grad + J.off + (long long)(i0 + ei) * J.ldw + c) =
@@ -346,9 +356,9 @@ __global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
   const float alpha = st.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float omb1 = 1.f - st.b1, omb2 = 1.f - st.b2, eps = st.eps;
   __syncthreads();                       // the partial tiles are read: reuse LDS for the new weights
-  float* pw = ups;                       // [64][UP_PS] updated W_aug tile
+  float* pw = ups;                       // [64][PS] updated W_aug tile
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < EJ / 4; ++q) {
     float gq[4] = {g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]};
     float mq[4] = {mm[q].x, mm[q].y, mm[q].z, mm[q].w}, vq[4] = {vv[q].x, vv[q].y, vv[q].z, vv[q].w};
     float pq[4] = {pp[q].x, pp[q].y, pp[q].z, pp[q].w};
@@ -365,20 +375,20 @@ __global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
       *reinterpret_cast<float4*>(a.v + o) = make_float4(vq[0], vq[1], vq[2], vq[3]);
       *reinterpret_cast<float4*>(a.param + o) = make_float4(pq[0], pq[1], pq[2], pq[3]);
     }
-    *reinterpret_cast<float4*>(pw + ei * UP_PS + ej + 4 * q) = make_float4(pq[0], pq[1], pq[2], pq[3]);
+    *reinterpret_cast<float4*>(pw + ei * PS + ej + 4 * q) = make_float4(pq[0], pq[1], pq[2], pq[3]);
   }
   if (J.fx_off < 0 || (J.dbg & 16)) return;   // no fragment-major copies (the f32 input layer)
   __syncthreads();
   // FX chunks: (feature jj, 8 W_aug rows 8 ib ..) -> lane (pos & 15) + 16 ((k % 32) / 8) of step k / 32
 #pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int c = t + UP_NT * e, jj = c & 63, ib = c >> 6;
+  for (int e = 0; e < TN / 32; ++e) {
+    const int c = t + UP_NT * e, jj = c % TN, ib = c / TN;
     const int j = j0 + jj, k0 = i0 + 8 * ib;
     if (j < J.fout && k0 < M) {
       up_bf16x8 vh, vl;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const float v = k0 + q < M ? pw[(8 * ib + q) * UP_PS + jj] : 0.f;
+        const float v = k0 + q < M ? pw[(8 * ib + q) * PS + jj] : 0.f;
         const __bf16 h = (__bf16)v;
         vh[q] = h;
         vl[q] = (__bf16)(v - (float)h);
@@ -392,14 +402,14 @@ __global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
   }
   // GX chunks: (input feature ii < fin, 8 outputs 8 jb ..)
 #pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int c = t + UP_NT * e, jb = c & 7, ii = c >> 3;
+  for (int e = 0; e < TN / 32; ++e) {
+    const int c = t + UP_NT * e, jb = c % (TN / 8), ii = c / (TN / 8);
     const int n = i0 + ii, k0 = j0 + 8 * jb;
     if (n < J.fin && k0 < J.fout) {
       up_bf16x8 vh, vl;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const float v = k0 + q < J.fout ? pw[ii * UP_PS + 8 * jb + q] : 0.f;
+        const float v = k0 + q < J.fout ? pw[ii * PS + 8 * jb + q] : 0.f;
         const __bf16 h = (__bf16)v;
         vh[q] = h;
         vl[q] = (__bf16)(v - (float)h);
@@ -412,9 +422,31 @@ __global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
   }
 }
 
+__global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
+  // tile of this workgroup: consecutive tiles (sharing an operand slice) on one XCD
+  // (the long reductions -- tiles [0, nheavy) -- are spread evenly over the
+  // XCDs first, the short ones after, so no XCD gets more long tiles than CUs)
+  const int b = blockIdx.x, x = b & 7, sl = b >> 3;
+  int T;
+  if (sl < a.per_xcd) {
+    T = x * a.per_xcd + sl;
+    if (T >= a.nheavy) return;
+  } else {
+    T = a.nheavy + x * a.per_xcd2 + (sl - a.per_xcd);
+    if (sl - a.per_xcd >= a.per_xcd2 || T >= a.ntiles) return;
+  }
+  const int jb = a.tile_job[T];
+  const UpdJob& J = a.job[jb];
+  // Adam constants (state->t was advanced for this step by the bound), read
+  // now: in flight during the reduction
+  const AdamState st = *a.state;
+  if (J.tn == 32) upd_tile<32>(a, J, st, b, T - J.tile0);
+  else upd_tile<64>(a, J, st, b, T - J.tile0);
+}
+
 hipError_t launch_update(hipStream_t st, const UpdArgs& a) {
   if (a.ntiles <= 0) return hipSuccess;
-  const unsigned grid = 8u * (unsigned)a.per_xcd;
+  const unsigned grid = 8u * (unsigned)(a.per_xcd + a.per_xcd2);
   hipLaunchKernelGGL(upd_kernel, dim3(grid), dim3(UP_NT), (size_t)2 * UP_BUF * sizeof(float), st, a);
   return hipGetLastError();
 }
