@@ -67,6 +67,7 @@ struct DevState {
   AdamState adam;
   uint64_t rng[2];             // [0] next forward's Philox counter, [1] last forward's
   unsigned tickets[4];         // 0: bound, 1: lse, 2: adam
+  unsigned upd_ctr[2];         // the fused update's image hand-off (UpdArgs::ctr), zero between launches
   float scalars[8];            // 0: loss, 1: bound value, 2: KL (V1)
 };
 
@@ -177,6 +178,8 @@ struct iwae_handle {
   int upd_dbg = 0;                   // timing ablations of that launch (env IWAE_UPD_DBG; wrong results)
   int upd_split = 0;                 // ... split over two graph branches (env IWAE_UPD_SPLIT)
   int upd_tn32 = 0;                  // ... sample-row layers in 64 x 32 tiles (env IWAE_UPD_TN32)
+  int upd_img = 0;                   // ... with the first encoder layer's backward inside it (env IWAE_UPD_IMG)
+  bool upd_fuse_img = false;         // (set per step by engine_train_body for run_update)
   // graphs
   bool use_graphs = false;
   // a captured train step; its first kernel reads the caller's x directly
@@ -1458,6 +1461,8 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hi
     J.tiles_m = (int)cdiv(d.fin + 1, 64); J.tiles_n = (int)cdiv(d.fout, J.tn);
     J.tile0 = tiles;
     J.dbg = h->upd_dbg;
+    const StochL& S0 = h->enc[0];
+    J.wait_img = h->upd_fuse_img && (w.di == S0.l1 || w.di == S0.l2 || w.di == S0.head);
     tiles += J.tiles_m * J.tiles_n;
     if (tiles > kUpdMaxTiles) return fail(h, IWAE_EINVAL, "fused update: too many tiles");
     for (int q = J.tile0; q < tiles; ++q) a.tile_job[q] = (unsigned char)(a.njobs - 1);
@@ -1470,6 +1475,31 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hi
   a.nheavy = heavy;
   a.per_xcd = (int)cdiv(heavy, 8);
   a.per_xcd2 = (int)cdiv(tiles - heavy, 8);
+  if (h->upd_fuse_img && part == 0) {
+    // the first encoder layer's backward (job I''s work) in this launch
+    const StochL& S0 = h->enc[0];
+    const DenseL& dh = h->dense[S0.head];
+    const DenseL& dl = h->dense[S0.l2];
+    a.nimg = P.Bimg; a.per_img = (int)cdiv(P.Bimg, 8);
+    a.nwait = 0;
+    for (int j = 0; j < a.njobs; ++j)
+      if (a.job[j].wait_img) a.nwait += a.job[j].tiles_m * a.job[j].tiles_n;
+    a.ctr = h->ds->upd_ctr;
+    a.P0 = h->eb[0].P.p; a.ldP0 = h->eb[0].P.ld; a.d0 = S0.d; a.kS = P.kS; a.stdnormal = h->L == 1;
+    a.h1 = h->h[0].p; a.ldh1 = h->h[0].ld; a.eps1 = h->eps_st[0].p; a.ldeps1 = h->eps_st[0].ld; a.dlw = h->dlw;
+    a.nsrc = 0;
+    a.src[a.nsrc] = h->dh_out[0].p; a.ldsrc[a.nsrc++] = h->dh_out[0].ld;
+    if (h->L >= 2) {
+      a.src[a.nsrc] = h->dh_prior[0].p; a.ldsrc[a.nsrc++] = h->dh_prior[0].ld;
+      a.src[a.nsrc] = h->dh_enc[0].p; a.ldsrc[a.nsrc++] = h->dh_enc[0].ld;
+    }
+    for (int q = a.nsrc; q < 3; ++q) { a.src[q] = a.src[0]; a.ldsrc[q] = a.ldsrc[0]; }
+    a.dP0 = h->eb[0].dP.p; a.lddP0 = h->eb[0].dP.ld;
+    a.Wh = h->params + dh.off; a.ldWh = dh.ldw; a.Hh = dh.fin;
+    a.Wl = h->params + dl.off; a.ldWl = dl.ldw; a.Hl = dl.fin;
+    a.y2 = h->eb[0].y2.p; a.ldy2 = h->eb[0].y2.ld; a.y1 = h->eb[0].y1.p; a.ldy1 = h->eb[0].y1.ld;
+    a.dY2 = h->eb[0].dY2.p; a.lddY2 = h->eb[0].dY2.ld; a.dY1 = h->eb[0].dY1.p; a.lddY1 = h->eb[0].dY1.ld;
+  }
   a.param = h->params; a.m = h->adam_m; a.v = h->adam_v; a.grad = h->grad;
   a.fx_hi = h->fx_hi; a.fx_lo = h->fx_lo;
   a.state = &h->ds->adam; a.do_adam = adam ? 1 : 0;
@@ -1995,6 +2025,15 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   // Its image-row job also at small batches (B = 20: step 128.1 -> 126.4 us
   // against the row-block Gaussian backward + two few-row launches)
   const bool img_bwd = img || h->engine_img_bwd;
+  // the first encoder layer's backward inside the update launch (its short
+  // tiles wait for it there): every workgroup of that launch must be resident
+  h->upd_fuse_img = false;
+  if (img_bwd && h->upd_img && !h->upd_split && use_update(h, P) && h->enc[0].d <= 256 &&
+      h->dense[h->enc[0].head].fin <= 512) {
+    long long tiles = 0;
+    for (const DenseL& d : h->dense) tiles += cdiv(d.fin + 1, 64) * cdiv(d.fout, h->upd_tn32 ? 32 : 64);
+    h->upd_fuse_img = tiles + P.Bimg + 16 <= 240;
+  }
   if (use_update(h, P) && img_bwd && h->upd_split && !h->dp_weighted) {
     // two branches: the update of every layer after the first encoder layer
     // (its inputs are complete) beside the first layer's backward, then that
@@ -2009,8 +2048,8 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
     if (adam) h->fx_version = h->params_version;
     return IWAE_OK;
   }
-  if (img_bwd) CHK(tc_run(h, P, E, 3));
-  else CHK(fused_encoder_bwd(h, P, h->dlw, 0));
+  if (img_bwd && !h->upd_fuse_img) CHK(tc_run(h, P, E, 3));
+  else if (!img_bwd) CHK(fused_encoder_bwd(h, P, h->dlw, 0));
   if (use_update(h, P) && h->dp_weighted) {
     // data parallel: the fused gradient pass (B_local * g, B_local in the
     // tail), the all-reduce, then Adam and the fragment-major copies
@@ -2276,6 +2315,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (const char* w = std::getenv("IWAE_UPD_DBG")) h->upd_dbg = std::atoi(w);           // timing ablations
   if (const char* w = std::getenv("IWAE_UPD_SPLIT")) h->upd_split = std::atoi(w) != 0;  // A/B switch
   if (const char* w = std::getenv("IWAE_UPD_TN32")) h->upd_tn32 = std::atoi(w) != 0;    // A/B switch
+  if (const char* w = std::getenv("IWAE_UPD_IMG")) h->upd_img = std::atoi(w) != 0;      // A/B switch
   if (const char* w = std::getenv("IWAE_ENGINE")) h->engine = std::atoi(w) != 0;   // A/B switch
   if (const char* w = std::getenv("IWAE_TC_IMG")) h->engine_img = std::atoi(w) != 0;   // A/B switch
   if (const char* w = std::getenv("IWAE_TC_IMGBWD")) h->engine_img_bwd = std::atoi(w) != 0;   // A/B switch
