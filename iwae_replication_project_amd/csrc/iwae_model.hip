@@ -1540,7 +1540,7 @@ constexpr int kTcMaxLayers = 3;      // op-table capacity: 4 ops per stochastic 
 static bool use_engine(const iwae_handle* h, const Plan& P) {
   if (!h->engine || !h->x3 || h->path == 1 || h->path == 2 || h->masked) return false;
   if (P.need_bce || P.kl || P.piwae) return false;       // BCE / KL / two-weighting losses: fused row-block path
-  if (h->L > kTcMaxLayers) return false;
+  if (h->L > kTcMaxLayers || h->enc[0].d > 2048) return false;   // (image-row backward: d / 4 column quads)
   return (long long)P.Bimg * P.kS <= (1LL << 18);
 }
 

@@ -831,29 +831,32 @@ __device__ __forceinline__ void tc_loadslab(CJob& J, COp& S, int row0, int nrows
 // over the image's kS sample rows of the h1 Gaussian backward (GBWD_ENC's
 // formula per sample; h1 was sampled from the image's (mu0, s0), F:58-F:60).
 // All threads work on one image row at a time: thread (sample group sg,
-// column quad qi) sums samples sg, sg + 16, ... with every load of a batch in
-// flight, then the 16 groups are added in fixed order through LDS scratch
-// (S.in_buf's planes; deterministic).  dP0 goes to out_buf (natural order,
+// column quad qi < nq = d / 4) sums samples sg, sg + nsg, ... (nsg = 512 / nq
+// groups: at d = 100 and k = 50 every sample's loads are in flight in one
+// batch), then the groups are added in fixed order through LDS scratch
+// (S.in_buf's planes, [nsg][nq][8] floats; deterministic).  dP0 goes to out_buf (natural order,
 // zeros to next_k) and S.out.
 template <int RT>
 __device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int row0, int nrows) {
-  constexpr int NSG = 16, SPT = 2;
-  const int t = threadIdx.x, sg = t >> 5, qi = t & 31;
-  const TcBuf B = tc_buf<RT>(J, S.out_buf);
-  float* scr = reinterpret_cast<float*>(tc_buf<RT>(J, S.in_buf).hi);   // [NSG][32][8] floats
+  constexpr int SPT = 3;
   const int d = S.d, kS = A.kS;
+  const int nq = (d + 3) >> 2, nsg = (TC_NW * 64) / nq;   // (d <= 2048: nsg >= 1)
+  const int t = threadIdx.x, sg = t / nq, qi = t - sg * nq;
+  const TcBuf B = tc_buf<RT>(J, S.out_buf);
+  float* scr = reinterpret_cast<float*>(tc_buf<RT>(J, S.in_buf).hi);   // [nsg][nq][8] floats
   const int padw = S.next_k - 2 * d;
   for (int e = t; e < 16 * RT * padw; e += TC_NW * 64) {
     const int r = e / padw, c = 2 * d + e % padw;
     B.hi[r * B.ld + c] = (__bf16)0.f;
     B.lo[r * B.ld + c] = (__bf16)0.f;
   }
-  __amdgpu_buffer_rsrc_t rsrc[4];
+  constexpr int NSRC = 3;                      // dh from the output MLP, the prior, the next encoder layer
+  __amdgpu_buffer_rsrc_t rsrc[NSRC];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) rsrc[u] = buf_rsrc(S.src[u]);
+  for (int u = 0; u < NSRC; ++u) rsrc[u] = buf_rsrc(S.src[u]);
   const __amdgpu_buffer_rsrc_t rh = buf_rsrc(S.h), re = buf_rsrc(S.eps), rd = buf_rsrc(A.dlw);
   const int c0 = 4 * qi;
-  const bool live = c0 < d;
+  const bool live = sg < nsg;
   for (int rr = 0; rr < nrows; ++rr) {
     const int b = row0 + rr;
     const float* Pr = S.P + (size_t)b * S.ld_P;
@@ -865,19 +868,19 @@ __device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int r
       rs4[q] = frcp(fexp(Pr[d + c]) + kScaleEps);
     }
     float dmu[4] = {0.f, 0.f, 0.f, 0.f}, dsc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int s0 = sg; s0 < kS; s0 += NSG * SPT) {
-      float4 hv[SPT], ev[SPT], gs[SPT][4];
+    for (int s0 = sg; s0 < kS; s0 += nsg * SPT) {
+      float4 hv[SPT], ev[SPT], gs[SPT][NSRC];
       float dl[SPT];
 #pragma unroll
       for (int i = 0; i < SPT; ++i) {
-        const int s = s0 + i * NSG;
+        const int s = s0 + i * nsg;
         const bool ok = live && s < kS;
         const long long r = (long long)b * kS + min(s, kS - 1);
         hv[i] = bld4(rh, ok ? (unsigned)(r * S.ld_h + c0) * 4u : kOOB);
         ev[i] = bld4(re, ok ? (unsigned)(r * S.ld_eps + c0) * 4u : kOOB);
         dl[i] = bld1(rd, ok ? (unsigned)r * 4u : kOOB);
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < NSRC; ++u)
           gs[i][u] = bld4(rsrc[u], (ok && u < S.nsrc) ? (unsigned)(r * S.ld_src[u] + c0) * 4u : kOOB);
       }
 #pragma unroll
@@ -885,7 +888,7 @@ __device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int r
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const float h = f4_at(hv[i], q), e = f4_at(ev[i], q);
-          float G = ((f4_at(gs[i][0], q) + f4_at(gs[i][1], q)) + f4_at(gs[i][2], q)) + f4_at(gs[i][3], q);
+          float G = (f4_at(gs[i][0], q) + f4_at(gs[i][1], q)) + f4_at(gs[i][2], q);
           const float z = h * rs4[q] - mu[q] * rs4[q];
           const float dlq = -dl[i];
           if (S.stdnormal) G += dl[i] * (-h);
@@ -895,17 +898,19 @@ __device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int r
         }
       }
     }
-    float* my = scr + (sg * 32 + qi) * 8;
+    if (live) {
+      float* my = scr + t * 8;                 // (sg * nq + qi) * 8
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      my[q] = dmu[q];
-      my[4 + q] = dsc[q];
+      for (int q = 0; q < 4; ++q) {
+        my[q] = dmu[q];
+        my[4 + q] = dsc[q];
+      }
     }
     tc_lds_barrier();
-    if (t < 32 * 8) {
-      const int q = t >> 3, j = t & 7;         // quad q, value j (dmu 0..3, dscale 4..7)
+    for (int e = t; e < nq * 8; e += TC_NW * 64) {
+      const int q = e >> 3, j = e & 7;         // quad q, value j (dmu 0..3, dscale 4..7)
       float v = 0.f;
-      for (int g = 0; g < NSG; ++g) v += scr[(g * 32 + q) * 8 + j];
+      for (int g = 0; g < nsg; ++g) v += scr[(g * nq + q) * 8 + j];
       const int c = 4 * q + (j & 3);
       if (c < d) {
         const int col = j < 4 ? c : d + c;
