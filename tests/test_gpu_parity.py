@@ -202,6 +202,24 @@ def test_fused_and_layerwise_paths_agree(arch, loss, path):
     np.testing.assert_allclose(wb, wa, atol=2 * ADAM_ATOL)      # see the Adam note above
 
 
+@pytest.mark.parametrize("d0", [130, 260])
+def test_engine_wide_first_latent_agrees_with_layerwise(d0):
+    """A first latent wider than 128 (the image-row Gaussian backward splits
+    d0 / 4 column quads over the workgroup): engine and layer-wise steps agree."""
+    rng = np.random.default_rng(23)
+    x = (rng.random((5, 784)) < 0.2).astype(np.float32)
+    outs = []
+    for path in ("layerwise", "engine"):
+        from iwae_replication_project_amd import Adam
+        m = make_model([64, 32], [32, 64], [d0, 16], [d0, 784], loss="IWAE", k=7, seed=5, kernel_path=path)
+        m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+        l1 = m.train_step(x)["IWAE"]
+        outs.append((l1, flat(m.get_gradients())))
+    (a1, ga), (b1, gb) = outs
+    assert abs(a1 - b1) <= 2 * REL * abs(a1)
+    assert rel_l2(gb, ga) <= 2 * REL
+
+
 def test_fused_and_layerwise_paths_agree_at_large_batch():
     """configs[1]/[4] architecture at 10,000 sample rows (B=200, k=50): the
     large-batch kernel choices of the fused step (128x128 output-layer dX
