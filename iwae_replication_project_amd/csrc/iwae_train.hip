@@ -831,16 +831,18 @@ __device__ __forceinline__ void tc_loadslab(CJob& J, COp& S, int row0, int nrows
 // over the image's kS sample rows of the h1 Gaussian backward (GBWD_ENC's
 // formula per sample; h1 was sampled from the image's (mu0, s0), F:58-F:60).
 // All threads work on one image row at a time: thread (sample group sg,
-// column quad qi < nq = d / 4) sums samples sg, sg + nsg, ... (nsg = 512 / nq
-// groups: at d = 100 and k = 50 every sample's loads are in flight in one
-// batch), then the groups are added in fixed order through LDS scratch
-// (S.in_buf's planes, [nsg][nq][8] floats; deterministic).  dP0 goes to out_buf (natural order,
+// column quad qi < nq = max(32, d / 4)) sums samples sg, sg + nsg, ... (nsg =
+// 512 / nq groups) with every load of a batch in flight, then the groups are
+// added in fixed order through LDS scratch (S.in_buf's planes, [nsg][nq][8]
+// floats; deterministic).  dP0 goes to out_buf (natural order,
 // zeros to next_k) and S.out.
 template <int RT>
 __device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int row0, int nrows) {
-  constexpr int SPT = 3;
+  constexpr int SPT = 2;
   const int d = S.d, kS = A.kS;
-  const int nq = (d + 3) >> 2, nsg = (TC_NW * 64) / nq;   // (d <= 2048: nsg >= 1)
+  // 32 column quads (16 sample groups) up to d = 128 (measured: one batch of
+  // every sample at d / 4 quads was no faster at k = 50), d / 4 beyond
+  const int nq = max(32, (d + 3) >> 2), nsg = (TC_NW * 64) / nq;   // (d <= 2048: nsg >= 1)
   const int t = threadIdx.x, sg = t / nq, qi = t - sg * nq;
   const TcBuf B = tc_buf<RT>(J, S.out_buf);
   float* scr = reinterpret_cast<float*>(tc_buf<RT>(J, S.in_buf).hi);   // [nsg][nq][8] floats
@@ -856,7 +858,7 @@ __device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int r
   for (int u = 0; u < NSRC; ++u) rsrc[u] = buf_rsrc(S.src[u]);
   const __amdgpu_buffer_rsrc_t rh = buf_rsrc(S.h), re = buf_rsrc(S.eps), rd = buf_rsrc(A.dlw);
   const int c0 = 4 * qi;
-  const bool live = sg < nsg;
+  const bool live = sg < nsg && c0 < d;
   for (int rr = 0; rr < nrows; ++rr) {
     const int b = row0 + rr;
     const float* Pr = S.P + (size_t)b * S.ld_P;
