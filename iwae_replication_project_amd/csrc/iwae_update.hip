@@ -348,7 +348,7 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
       *reinterpret_cast<float4*>(a.grad + J.off + (long long)(i0 + ei) * J.ldw + c) =
           make_float4(a.gscale * g[4 * q], a.gscale * g[4 * q + 1], a.gscale * g[4 * q + 2], a.gscale * g[4 * q + 3]);
   }
-  if (!a.do_adam) return;
+  if (!a.do_adam || (J.dbg & 32)) return;
 
   // Adam (adam_kernel's arithmetic)
   const float tt = (float)st.t;

@@ -1,6 +1,7 @@
 #!/bin/bash
 # upd_kernel timing ablations (IWAE_UPD_DBG bits: 1 no MFMA, 2 no LDS staging,
-# 4 no activation loads) on the bench's train leg; prints the replayed avg.
+# 4 no activation loads, 8 stop after the reduction, 32 after the gradient write, 16
+# after Adam) on the bench's train leg; prints the replayed avg.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/abl
