@@ -343,12 +343,17 @@ struct UpdJob {
   int tn;                                             // tile columns: 64, or 32
   int wait_img;                                       // reads the in-launch image backward's outputs
   int dbg;                                            // timing ablations (env IWAE_UPD_DBG): 1 no MFMA, 2 no staging, 4 no loads
+  // split-K over rows (large batches, gradient pass only): nsplit row chunks of
+  // `chunk` rows, split s writes its partial W_aug tile at off + s * slab_stride
+  // (the Adam launch sums the slabs); the job's tiles are then split-major
+  int nsplit, chunk; long long slab_stride;
 };
 constexpr int kUpdMaxJobs = 20, kUpdMaxTiles = 384;
 struct UpdArgs {
   UpdJob job[kUpdMaxJobs]; int njobs;
   unsigned char tile_job[kUpdMaxTiles];               // job of each tile
   int ntiles, nheavy, per_xcd, per_xcd2;              // tiles [0, nheavy): per_xcd per XCD, the rest per_xcd2 per XCD
+  int search;                                         // more than kUpdMaxTiles tiles: job of a tile by the jobs' tile0
   float* param; float* m; float* v; float* grad;
   __bf16* fx_hi; __bf16* fx_lo;
   const AdamState* state; int do_adam;

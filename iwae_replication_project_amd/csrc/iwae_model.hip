@@ -178,6 +178,7 @@ struct iwae_handle {
   int upd_dbg = 0;                   // timing ablations of that launch (env IWAE_UPD_DBG; wrong results)
   int upd_split = 0;                 // ... split over two graph branches (env IWAE_UPD_SPLIT)
   int upd_tn32 = 0;                  // ... sample-row layers in 64 x 32 tiles (env IWAE_UPD_TN32)
+  int upd_slabs = 1;                 // ... and beyond upd_rows its split-K gradient pass into the slabs (env IWAE_UPD_SLABS)
   int upd_img = 0;                   // ... with the first encoder layer's backward inside it (env IWAE_UPD_IMG)
   bool upd_fuse_img = false;         // (set per step by engine_train_body for run_update)
   // graphs
@@ -1410,10 +1411,19 @@ static bool use_update(const iwae_handle* h, const Plan& P) {
 // part: 0 every layer, 1 all but the first encoder layer (sample rows), 2 the
 // first encoder layer (image rows; its backward may still be running when
 // part 1 starts on another stream)
+// slabs: larger batches (beyond upd_rows), the gradient pass only, split over
+// rows into the split-K slabs the Adam launch sums (the weight-gradient GEMMs'
+// role); about two workgroups per CU of sample-row tiles
+static bool use_update_slabs(const iwae_handle* h, const Plan& P) {
+  return h->upd_slabs && h->x3 && h->slabs && (long long)P.Bimg * P.kS > h->upd_rows &&
+         (int)h->dense.size() <= kUpdMaxJobs;
+}
+
 static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hipStream_t st = nullptr,
-                      float gscale = 1.f, float* tail = nullptr) {
+                      float gscale = 1.f, float* tail = nullptr, bool slabs = false) {
   if (!st) st = h->stream;
   const int L = h->L, M = P.Bimg * P.kS;
+  constexpr long long UP_ROWS_ITER = 128;      // rows per reduction iteration of the update kernel
   struct WJ { int di; const Mat* A; const Mat* dZ; int rows; const float* ks; };
   std::vector<WJ> js;
   for (int i = 0; i < L; ++i) {
@@ -1447,8 +1457,20 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hi
   UpdArgs a{};
   int tiles = 0;
   double flop = 0.0;
+  int nsplit = 1;
+  if (slabs) {
+    long long st_tiles = 0;                      // sample-row tiles: nsplit of them per CU pair
+    for (const WJ& w : js)
+      if (w.rows == M) st_tiles += cdiv(h->dense[w.di].fin + 1, 64) * cdiv(h->dense[w.di].fout, 64);
+    static const long long target = [] {        // tuning knob: sample-row workgroups of the pass
+      const char* e = std::getenv("IWAE_UPD_SLAB_WG");
+      return e ? std::max(1LL, std::atoll(e)) : 512LL;
+    }();
+    nsplit = (int)std::max(1LL, (target + st_tiles / 2) / std::max(1LL, st_tiles));
+    a.search = 1;
+  }
   for (const WJ& w : js) {
-    const DenseL& d = h->dense[w.di];
+    DenseL& d = h->dense[w.di];
     UpdJob& J = a.job[a.njobs++];
     J.A = w.A->p; J.lda = w.A->ld; J.B = w.dZ->p; J.ldb = w.dZ->ld; J.ks = w.ks ? w.ks : h->ones; J.rows = w.rows;
     J.off = d.off; J.fin = d.fin; J.fout = d.fout; J.ldw = d.ldw;
@@ -1463,15 +1485,28 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hi
     J.dbg = h->upd_dbg;
     const StochL& S0 = h->enc[0];
     J.wait_img = h->upd_fuse_img && (w.di == S0.l1 || w.di == S0.l2 || w.di == S0.head);
-    tiles += J.tiles_m * J.tiles_n;
-    if (tiles > kUpdMaxTiles) return fail(h, IWAE_EINVAL, "fused update: too many tiles");
-    for (int q = J.tile0; q < tiles; ++q) a.tile_job[q] = (unsigned char)(a.njobs - 1);
+    J.nsplit = 1;
+    if (slabs) {
+      // row chunks of whole 128-row iterations, at most the layer's slab count
+      long long S = std::min<long long>(w.rows == M ? nsplit : 1, d.max_splits);
+      const long long chunk = cdiv(cdiv(w.rows, S), UP_ROWS_ITER) * UP_ROWS_ITER;
+      S = cdiv(w.rows, chunk);
+      J.nsplit = (int)S; J.chunk = (int)chunk; J.slab_stride = d.size();
+      J.off = d.slab_off; J.fx_off = -1; J.tn = 64;
+      J.tiles_n = (int)cdiv(d.fout, 64);
+      d.splits = (int)S;
+    }
+    tiles += J.tiles_m * J.tiles_n * J.nsplit;
+    if (!slabs) {
+      if (tiles > kUpdMaxTiles) return fail(h, IWAE_EINVAL, "fused update: too many tiles");
+      for (int q = J.tile0; q < tiles; ++q) a.tile_job[q] = (unsigned char)(a.njobs - 1);
+    }
     flop += 2.0 * w.rows * (d.fin + 1) * d.fout;
   }
   a.ntiles = tiles;
   int heavy = 0;                                // the jobs are sorted by rows: the sample-row jobs' tiles first
   for (int j = 0; j < a.njobs; ++j)
-    if (a.job[j].rows == js[0].rows) heavy = a.job[j].tile0 + a.job[j].tiles_m * a.job[j].tiles_n;
+    if (a.job[j].rows == js[0].rows) heavy = a.job[j].tile0 + a.job[j].tiles_m * a.job[j].tiles_n * a.job[j].nsplit;
   a.nheavy = heavy;
   a.per_xcd = (int)cdiv(heavy, 8);
   a.per_xcd2 = (int)cdiv(tiles - heavy, 8);
@@ -1500,10 +1535,10 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hi
     a.y2 = h->eb[0].y2.p; a.ldy2 = h->eb[0].y2.ld; a.y1 = h->eb[0].y1.p; a.ldy1 = h->eb[0].y1.ld;
     a.dY2 = h->eb[0].dY2.p; a.lddY2 = h->eb[0].dY2.ld; a.dY1 = h->eb[0].dY1.p; a.lddY1 = h->eb[0].dY1.ld;
   }
-  a.param = h->params; a.m = h->adam_m; a.v = h->adam_v; a.grad = h->grad;
+  a.param = h->params; a.m = h->adam_m; a.v = h->adam_v; a.grad = slabs ? h->slabs : h->grad;
   a.fx_hi = h->fx_hi; a.fx_lo = h->fx_lo;
-  a.state = &h->ds->adam; a.do_adam = adam ? 1 : 0;
-  a.gscale = gscale; a.tail = tail; a.tail_val = gscale;
+  a.state = &h->ds->adam; a.do_adam = adam && !slabs ? 1 : 0;
+  a.gscale = slabs ? 1.f : gscale; a.tail = slabs ? nullptr : tail; a.tail_val = gscale;
   HIPCHK(launch_update(st, a));
   if (adam && part != 1) h->params_version++;
   if (h->prof_kind == 15 && adam && !h->prof_have) {
@@ -2071,7 +2106,8 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
     if (adam) h->fx_version = h->params_version;
     return IWAE_OK;
   }
-  CHK(weight_grads(h, P, true, true, h->dpx));
+  if (use_update_slabs(h, P)) CHK(run_update(h, P, false, 0, nullptr, 1.f, nullptr, true));
+  else CHK(weight_grads(h, P, true, true, h->dpx));
   CHK(finish_step(h, P, adam));
   if (adam) {
     // the next step's engine reads the updated weights' fragment-major copies
@@ -2315,6 +2351,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (const char* w = std::getenv("IWAE_UPD_DBG")) h->upd_dbg = std::atoi(w);           // timing ablations
   if (const char* w = std::getenv("IWAE_UPD_SPLIT")) h->upd_split = std::atoi(w) != 0;  // A/B switch
   if (const char* w = std::getenv("IWAE_UPD_TN32")) h->upd_tn32 = std::atoi(w) != 0;    // A/B switch
+  if (const char* w = std::getenv("IWAE_UPD_SLABS")) h->upd_slabs = std::atoi(w) != 0;  // A/B switch
   if (const char* w = std::getenv("IWAE_UPD_IMG")) h->upd_img = std::atoi(w) != 0;      // A/B switch
   if (const char* w = std::getenv("IWAE_ENGINE")) h->engine = std::atoi(w) != 0;   // A/B switch
   if (const char* w = std::getenv("IWAE_TC_IMG")) h->engine_img = std::atoi(w) != 0;   // A/B switch

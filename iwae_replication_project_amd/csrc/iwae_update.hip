@@ -561,14 +561,33 @@ __global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
     T = a.nheavy + x * a.per_xcd2 + s2;
     if (s2 >= a.per_xcd2 || T >= a.ntiles) return;
   }
-  const int jb = a.tile_job[T];
+  int jb = 0;
+  if (a.search) {
+    while (jb + 1 < a.njobs && T >= a.job[jb + 1].tile0) ++jb;
+  } else {
+    jb = a.tile_job[T];
+  }
   const UpdJob& J = a.job[jb];
   // Adam constants (state->t was advanced for this step by the bound), read
   // now: in flight during the reduction
   const AdamState st = *a.state;
   if (J.wait_img && a.nimg > 0) upd_wait_images(a);
-  if (J.tn == 32) upd_tile<32>(a, J, st, b, T - J.tile0);
-  else upd_tile<64>(a, J, st, b, T - J.tile0);
+  if (J.nsplit > 1) {
+    // split s of the rows: this tile's partial sum into slab s
+    const int per = J.tiles_m * J.tiles_n, lt = T - J.tile0, s = lt / per;
+    const long long r0 = (long long)s * J.chunk;
+    UpdJob Js = J;
+    Js.A = J.A + r0 * J.lda;
+    Js.B = J.B + r0 * J.ldb;
+    Js.ks = J.ks + r0;
+    Js.rows = min(J.chunk, J.rows - (int)r0);
+    Js.off = J.off + s * J.slab_stride;
+    upd_tile<64>(a, Js, st, b, lt - s * per);
+  } else if (J.tn == 32) {
+    upd_tile<32>(a, J, st, b, T - J.tile0);
+  } else {
+    upd_tile<64>(a, J, st, b, T - J.tile0);
+  }
   if (J.wait_img && a.nimg > 0) {
     // the last short tile resets the counters for the next launch (every short
     // tile has passed its wait by then)
