@@ -119,6 +119,30 @@ def test_fused_update_matches_split_k_update(B, k, L, monkeypatch):
     assert np.abs(ma - mb).max() <= 1e-3 * np.abs(mb).max()
 
 
+def test_large_batch_slab_pass_matches_grouped_gemms(monkeypatch):
+    """Beyond 4096 sample rows the update kernel's split-K gradient pass (row
+    chunks into the Adam slabs) replaces the grouped weight-gradient GEMMs:
+    same loss, gradient and updated weights on the same injected noise."""
+    from iwae_replication_project_amd import Adam, Flexible_Model
+    rng = np.random.default_rng(65)
+    B, k = 100, 50
+    x = (rng.random((B, 784)) < 0.2).astype(np.float32)
+    eps = [rng.standard_normal((k, B, d)).astype(np.float32) for d in ARCH2[2]]
+
+    def step(flag):
+        monkeypatch.setenv("IWAE_UPD_SLABS", flag)
+        m = Flexible_Model(*ARCH2, dataset_bias=None, loss_function="IWAE", k=k, seed=13)
+        m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+        loss = m.train_step(x, eps=eps)["IWAE"]
+        monkeypatch.delenv("IWAE_UPD_SLABS", raising=False)
+        return loss, _flat(m.get_gradients()), _flat(m.get_weights())
+    la, ga, wa = step("1")
+    lb, gb, wb = step("0")
+    assert la == lb                                   # the forward and bound are the same launches
+    assert np.linalg.norm(ga - gb) <= 1e-5 * np.linalg.norm(ga)
+    assert np.abs(wa - wb).max() <= 1e-6
+
+
 @pytest.mark.parametrize("env", ["IWAE_UPD_IMG", "IWAE_UPD_TN32", "IWAE_TC_FOLD0", "IWAE_TC_BOUND"])
 def test_train_step_variants_agree(env, monkeypatch):
     """The measured-and-parked variants of the configs[1] step (first-layer
