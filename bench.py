@@ -34,11 +34,17 @@ B_PER_GPU, K = 20, 50
 LARGE_B_PER_GPU = 512              # configs[4]: global batch 4096 over 8 GPUs
 # algorithmic train FLOP per image*sample, 2L k=50
 TRAIN_FLOP_PER_ROW = 1_712_944
+SAMPLE_ROW_MACS = 281_800          # per sample row, one pass over the sample-row Dense layers (2L)
 NLL_FLOP_PER_IMAGE = 2.818e9
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec peak
 BF16_PEAK_TFLOPS = 2500.0          # MI355X_MICROARCH.md: BF16 MFMA dense peak
 BF16X3_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 3, 1)   # f32-accurate bf16x3 products: 3 bf16 MFMAs each
 HBM_PEAK_GBS = 8000.0
+PRECISION = ("fp32 values and fp32 accumulation everywhere; every sample-row matrix product of the train step "
+             "(forward, backward-data and weight gradients) and of the NLL is a bf16x3 split product "
+             "(a_hi b_hi + a_hi b_lo + a_lo b_hi on bf16 MFMA, ~2^-16 relative per product); the first encoder "
+             "layer's input Dense (784 -> 200 on image rows) is exact f32 MFMA, at <= 32 images its l2 and head "
+             "too (DESIGN.md section 4)")
 
 
 def pixel_profile():
@@ -57,6 +63,11 @@ def synthetic_images(n, seed):
     return (rng.random((n, 784)) < pi).astype(np.float32), pi
 
 
+CORES_NOTE = ("threads = the process's CPU affinity set capped by OMP_NUM_THREADS: the GPU pool gives each "
+              "GPU a 16-CPU share of the host and sets OMP_NUM_THREADS=16 (nproc counts the whole machine); "
+              "threads_curve shows how the oracle's small per-step BLAS calls scale with threads")
+
+
 def host_cores():
     """(threads used, cores this process may run on, nproc): the threads are the
     cores of the process's CPU affinity set (the box's share), capped by
@@ -70,18 +81,11 @@ def host_cores():
     return used, avail, os.cpu_count() or 1
 
 
-def cpu_baseline(seconds=12.0):
-    """The oracle (numpy restatement of the reference's op sequence, incl. the
-    duplicate decoder pass at F:340) timed on host cores: IWAE train steps at
-    the bench workload (B=20, k=50, 2L), float32."""
-    from oracle import iwae_oracle as O
-    try:
-        from threadpoolctl import threadpool_limits
-    except Exception:          # pragma: no cover
-        threadpool_limits = None
-    cores, avail, nproc = host_cores()
-    ctx = threadpool_limits(limits=cores) if threadpool_limits else None
-    try:
+def _oracle_train_rate(O, seconds, threads):
+    """IWAE train steps of the oracle (B=20, k=50, 2L, float32, incl. the F:340
+    duplicate decoder pass) on `threads` BLAS threads for about `seconds`."""
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(limits=threads):
         spec = O.ModelSpec(HE, HD, LE, LD)
         x, pi = synthetic_images(B_PER_GPU, 1)
         rng = np.random.default_rng(2)
@@ -99,13 +103,28 @@ def cpu_baseline(seconds=12.0):
             el = time.perf_counter() - t0
             if el >= seconds:
                 break
-    finally:
-        if ctx is not None:
-            ctx.__exit__(None, None, None)
+    return steps, el
+
+
+def cpu_baseline(seconds=12.0):
+    """The oracle (numpy restatement of the reference's op sequence, incl. the
+    duplicate decoder pass at F:340) timed on host cores: IWAE train steps at
+    the bench workload (B=20, k=50, 2L), float32.  `value` is the rate on the
+    process's thread budget (`cores`); `threads_curve` is the rate at 1, 4 and
+    that many threads (a third of the time each is spent on the curve)."""
+    from oracle import iwae_oracle as O
+    cores, avail, nproc = host_cores()
+    curve = {}
+    for t in sorted({1, min(4, cores)}):
+        st, el = _oracle_train_rate(O, seconds / 6, t)
+        curve[t] = round(st * B_PER_GPU * K / el, 1)
+    steps, el = _oracle_train_rate(O, seconds * 2 / 3, cores)
+    curve[cores] = round(steps * B_PER_GPU * K / el, 1)
     return dict(value=steps * B_PER_GPU * K / el, unit="image*samples/s", cores=cores, cores_available=avail,
-                nproc=nproc, kind="port",
+                nproc=nproc, kind="port", threads_curve={str(k): v for k, v in sorted(curve.items())},
+                cores_note=CORES_NOTE,
                 sample=f"{steps} IWAE train steps (2L, k={K}, batch {B_PER_GPU}, float32 numpy, incl. the "
-                       f"F:340 duplicate decoder pass) in {el:.1f} s")
+                       f"F:340 duplicate decoder pass) in {el:.1f} s on {cores} threads")
 
 
 def cpu_baseline_nll(seconds=8.0, k=5000):
@@ -144,7 +163,7 @@ def cpu_baseline_nll(seconds=8.0, k=5000):
         if ctx is not None:
             ctx.__exit__(None, None, None)
     return dict(value=n / el, unit="images/s", cores=cores, cores_available=avail, nproc=nproc, kind="port",
-                sample=f"{n} test images at k={k} (2L, float32 numpy, incl. the F:340 duplicate decoder pass) in "
+                cores_note=CORES_NOTE, sample=f"{n} test images at k={k} (2L, float32 numpy, incl. the F:340 duplicate decoder pass) in "
                        f"{el:.1f} s; extrapolates linearly to 10k images")
 
 
@@ -163,6 +182,8 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-c0", action="store_true")
     ap.add_argument("--c0-steps", type=int, default=200)
+    ap.add_argument("--tune", action="append", default=[],
+                    help="library tuning knob name=value (include/iwae.h enum iwae_knob), repeatable; A/B runs only")
     args = ap.parse_args()
 
     import torch
@@ -182,8 +203,9 @@ def main():
     from iwae_replication_project_amd import Adam, Flexible_Model, distributed
 
     x_all, pi = synthetic_images(50_000, 1 + rank)
+    tuning = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in args.tune}
     model = Flexible_Model(HE, HD, LE, LD, dataset_bias=pi, loss_function="IWAE", k=K, seed=2,
-                           use_graphs=not args.no_graphs)
+                           use_graphs=not args.no_graphs, tuning=tuning)
     model.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
     if world > 1:
         distributed.enable_data_parallel(model)
@@ -239,13 +261,24 @@ def main():
             return None
         return ms.value / args.steps, fl.value / args.steps
 
-    cands = {"tc_kernel forward (train engine, bf16x3)": (live(10, 0), BF16X3_PEAK_TFLOPS),
-             "tc_kernel backward (train engine, bf16x3)": (live(11, 0), BF16X3_PEAK_TFLOPS),
-             "gemm_kernel<FWD, EPI_BERN> (output layer, f32 MFMA)": (live(0, 2), FP32_MFMA_PEAK_TFLOPS),
-             "upd_kernel (weight gradients + Adam + FX copies, bf16x3)": (live(15, 0), BF16X3_PEAK_TFLOPS)}
-    kern = {k: dict(avg_us=round(v[0] * 1e3, 3), flop_per_launch=v[1],
-                    tflops=round(v[1] / (v[0] * 1e-3) / 1e12, 3), peak=pk)
-            for k, (v, pk) in cands.items() if v is not None}
+    # algorithmic FLOP per launch: the forward and backward launches each do one
+    # product per sample-row Dense layer (281,800 MACs per row);
+    # the library's own count of the forward includes the output MLP's two
+    # hidden layers that its column-split jobs recompute (reported as executed)
+    rows_step = B_PER_GPU * K
+    alg = {10: 2.0 * SAMPLE_ROW_MACS * rows_step, 11: 2.0 * SAMPLE_ROW_MACS * rows_step}
+    specs = {"tc_kernel forward (train engine, bf16x3)": (10, 0, BF16X3_PEAK_TFLOPS),
+             "tc_kernel backward (train engine, bf16x3)": (11, 0, BF16X3_PEAK_TFLOPS),
+             "gemm_kernel<FWD, EPI_BERN> (output layer, f32 MFMA)": (0, 2, FP32_MFMA_PEAK_TFLOPS),
+             "upd_kernel (weight gradients + Adam + FX copies, bf16x3)": (15, 0, BF16X3_PEAK_TFLOPS)}
+    kern = {}
+    for name, (kind, epi, pk) in specs.items():
+        v = live(kind, epi)
+        if v is None:
+            continue
+        fl = alg.get(kind, v[1])
+        kern[name] = dict(avg_us=round(v[0] * 1e3, 3), flop_per_launch=fl, flop_executed=v[1],
+                          tflops=round(fl / (v[0] * 1e-3) / 1e12, 3), peak=pk)
     dom = max(kern, key=lambda k: kern[k]["avg_us"])
     kd = kern[dom]
     achieved = kd["tflops"]
@@ -310,10 +343,10 @@ def main():
         ltf = TRAIN_FLOP_PER_ROW * lrows / el3 / 1e12
         large = dict(value=round(lrows / el3, 1), unit="image*samples/s", per_gpu_batch=bl, global_batch=bl * world,
                      k=K, steps=args.large_batch_steps, ms_per_step=round(1e3 * el3 / args.large_batch_steps, 4),
-                     tflops=round(ltf, 3), frac_of_fp32_mfma_peak=round(ltf / (FP32_MFMA_PEAK_TFLOPS * world), 4),
+                     tflops=round(ltf, 3), frac_of_peak=round(ltf / (BF16X3_PEAK_TFLOPS * world), 4),
+                     peak_basis="bf16x3 products: bf16 dense 2.5 PFLOP/s / 3 = 833.3 TFLOP/s per GPU",
                      workload="BASELINE configs[4] per-GPU share (4096 over 8 GPUs)",
-                     precision="as the train step, except the output layer's Bernoulli and dX GEMMs: bf16x3 "
-                               "(>= 8192 sample rows, DESIGN.md section 4)")
+                     precision=PRECISION)
 
     # ---- k=5000 NLL over the test images, sharded by image
     nll = None
@@ -348,7 +381,7 @@ def main():
     c0 = None
     if not args.no_c0:
         m0 = Flexible_Model([200], [200], [50], [784], dataset_bias=pi, loss_function="IWAE", k=5, seed=2,
-                            use_graphs=not args.no_graphs)
+                            use_graphs=not args.no_graphs, tuning=tuning)
         m0.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
         if world > 1:
             distributed.enable_data_parallel(m0)
@@ -392,10 +425,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32 (bf16x3 split products)",
-            "precision": "fp32 values, fp32 accumulate; matrix products either exact f32 MFMA or bf16x3 split "
-                         "products (a_hi b_hi + a_hi b_lo + a_lo b_hi, ~2^-16 relative per product): train step "
-                         "weight-operand products f32 except as DESIGN.md section 4 lists, weight gradients bf16x3, "
-                         "NLL bf16x3",
+            "precision": PRECISION,
             "data": "synthetic",
             "config": {"workload": "IWAE train step (fwd+bound+bwd+Adam), k=50, 2 stochastic layers "
                                    "784-200-200-100-100-50, batch 20 per GPU (BASELINE configs[1])",

@@ -97,10 +97,38 @@ int iwae_set_seed(iwae_handle* h, unsigned long long seed);
  * splitmix64(seed ^ splitmix64(stream)) for stream != 0 (stream 0: the seed
  * itself), so ranks that share a seed still draw independent noise -- the iid
  * draws of F:59 qh1Ix.sample(n) / F:68 .sample() hold across the ranks of a
- * data-parallel step or a sample-sharded NLL.  Restarts the Philox counter. */
+ * data-parallel step or a sample-sharded NLL.  Each stream keeps its own
+ * Philox counter position: switching away and back continues where the stream
+ * stopped (its noise is never replayed), re-selecting the current stream is a
+ * no-op, and iwae_set_seed restarts every stream from counter 0. */
 int iwae_set_noise_stream(iwae_handle* h, unsigned long long stream);
 /* 1 = capture the Philox train step in a hipGraph per shape and replay it. */
 int iwae_set_graphs(iwae_handle* h, int enable);
+/* Tuning knobs (A/B measurements and tests; none changes the arithmetic
+ * beyond summation order / which of two parity-tested kernel paths runs).
+ * They replace the environment switches of earlier builds: the release
+ * library reads no environment variables.  Setting one drops the handle's
+ * captured graphs and engine plans. */
+enum iwae_knob {
+  IWAE_KNOB_ENGINE = 1,        /* train step on the row-chain engine (default 1) */
+  IWAE_KNOB_TC_IMG = 2,        /* ... first encoder layer's l2 / head as image-row jobs above 32 images (1) */
+  IWAE_KNOB_TC_IMGBWD = 3,     /* ... its backward as an image-row job at small batches too (1) */
+  IWAE_KNOB_TC_FOLD0 = 4,      /* ... its l2 / head folded into the forward jobs (0) */
+  IWAE_KNOB_TC_XCD = 5,        /* XCD-aware job placement of the engine launches (1) */
+  IWAE_KNOB_TC_BOUND = 6,      /* the bound inside the engine's backward launch (1) */
+  IWAE_KNOB_TC_RT = 7,         /* 16-row tiles per engine workgroup: 1, 2 or 4 (1) */
+  IWAE_KNOB_UPD = 8,           /* fused weight-gradient + Adam + FX update launch (1) */
+  IWAE_KNOB_UPD_ROWS = 9,      /* ... up to this many sample rows per step (4096) */
+  IWAE_KNOB_UPD_TN32 = 10,     /* ... sample-row layers in 64 x 32 tiles (0) */
+  IWAE_KNOB_UPD_SLABS = 11,    /* beyond UPD_ROWS: its split-K gradient pass into the Adam slabs (1) */
+  IWAE_KNOB_UPD_SLAB_WG = 12,  /* ... sample-row workgroups of that pass (512) */
+  IWAE_KNOB_DW_TARGET = 13,    /* split-K workgroups per layer of the grouped weight-gradient GEMMs (768) */
+  IWAE_KNOB_SMALLM_ROWS = 14,  /* few-row first-layer launches up to this many images, <= 32 (32) */
+  IWAE_KNOB_OUT_X3_ROWS = 15,  /* row-block path: bf16x3 output layer from this many sample rows (8192) */
+  IWAE_KNOB_MG_WAVES = 16,     /* NLL kernel workgroup: 8 waves / 64 rows or 4 waves / 32 rows (8) */
+  IWAE_KNOB_NLL_ROWS = 17      /* sample rows per NLL chunk (2^20) */
+};
+int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --
  * a.b = a_hi b_hi + a_hi b_lo + a_lo b_hi with hi = bf16(x), lo = bf16(x - hi),
  * f32 accumulate on v_mfma_f32_32x32x16_bf16 (~2^-16 relative per product,
@@ -173,7 +201,8 @@ int iwae_apply_adam(iwae_handle* h, float grad_scale);
  *    With NULL, the caller reduces the buffer itself between
  *    iwae_forward_backward and iwae_apply_adam(h, 0); iwae_train_step then
  *    returns IWAE_EINVAL.
- * world == 1 with NULL restores single-process behaviour. */
+ * world == 1 with NULL restores single-process behaviour.  A failed call
+ * (bad rank / world, a bound gradient buffer, RCCL init) changes nothing. */
 int iwae_dp_unique_id(void* out128);
 int iwae_dp_init(iwae_handle* h, int rank, int world, const void* rccl_unique_id);
 /* Broadcast parameters, Adam moments and the Adam step from rank 0 over the

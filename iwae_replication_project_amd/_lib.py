@@ -14,6 +14,12 @@ LIB_NAME = "libiwae_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 # loss ids (include/iwae.h enum iwae_loss_id)
+# include/iwae.h enum iwae_knob (iwae_set_tuning)
+KNOBS = {
+    "engine": 1, "tc_img": 2, "tc_imgbwd": 3, "tc_fold0": 4, "tc_xcd": 5, "tc_bound": 6, "tc_rt": 7,
+    "upd": 8, "upd_rows": 9, "upd_tn32": 10, "upd_slabs": 11, "upd_slab_wg": 12, "dw_target": 13,
+    "smallm_rows": 14, "out_x3_rows": 15, "mg_waves": 16, "nll_rows": 17,
+}
 LOSS_IDS = {
     "VAE": 0, "IWAE": 1, "VAE_V1": 2, "L_alpha": 3, "L_power_p": 4,
     "L_median": 5, "CIWAE": 6, "MIWAE": 7, "PIWAE": 8,
@@ -55,6 +61,7 @@ SIGNATURES = {
     "iwae_set_graphs": (c_int, [H, c_int]),
     "iwae_set_path": (c_int, [H, c_int]),
     "iwae_set_precision": (c_int, [H, c_int]),
+    "iwae_set_tuning": (c_int, [H, c_int, c_longlong]),
     "iwae_num_params": (c_longlong, [H]),
     "iwae_set_params": (c_int, [H, FP, c_longlong]),
     "iwae_get_params": (c_int, [H, FP, c_longlong]),

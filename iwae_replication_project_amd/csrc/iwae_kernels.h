@@ -341,8 +341,6 @@ struct UpdJob {
   long long gx_off; int gx_steps;
   int tiles_m, tiles_n, tile0;                        // tiles [tile0, tile0 + tiles_m * tiles_n), column-major
   int tn;                                             // tile columns: 64, or 32
-  int wait_img;                                       // reads the in-launch image backward's outputs
-  int dbg;                                            // timing ablations (env IWAE_UPD_DBG): 1 no MFMA, 2 no staging, 4 no loads
   // split-K over rows (large batches, gradient pass only): nsplit row chunks of
   // `chunk` rows, split s writes its partial W_aug tile at off + s * slab_stride
   // (the Adam launch sums the slabs); the job's tiles are then split-major
@@ -359,22 +357,6 @@ struct UpdArgs {
   const AdamState* state; int do_adam;
   float gscale;                                       // gradient written as gscale * dW (data parallel: B_local)
   float* tail; float tail_val;                        // data parallel: *tail = tail_val (B_local), or null
-  // The first encoder layer's backward on its images inside this launch (nimg >
-  // 0; the train engine's image-row job I' otherwise): per image, dP0 = the
-  // sum over its kS samples of the h1 Gaussian backward, dY2 = dP0 W_head^T
-  // (1 - y2^2), dY1 = dY2 W_l2^T (1 - y1^2), exact f32; per_img workgroups per
-  // XCD after the long tiles.  The short tiles (the first layer's weight
-  // gradients, wait_img jobs) wait for the nimg images through ctr[0]; the
-  // last of them resets the counters (ctr[1] counts them, nwait in all).
-  int nimg, per_img, nwait; unsigned* ctr;
-  const float* P0; int ldP0; int d0, kS, stdnormal;
-  const float* h1; int ldh1; const float* eps1; int ldeps1; const float* dlw;
-  const float* src[3]; int ldsrc[3]; int nsrc;
-  float* dP0; int lddP0;
-  const float* Wh; int ldWh; int Hh;                  // head W_aug [Hh + 1][ldWh] (rows: l2 outputs), 2 d0 columns
-  const float* Wl; int ldWl; int Hl;                  // l2 W_aug [Hl + 1][ldWl], Hh columns
-  const float* y2; int ldy2; const float* y1; int ldy1;
-  float* dY2; int lddY2; float* dY1; int lddY1;
 };
 hipError_t launch_update(hipStream_t st, const UpdArgs& a);
 hipError_t upd_setup_attributes();

@@ -125,6 +125,7 @@ struct iwae_handle {
   uint64_t seed = 0x5eed5eedULL;       // Philox key actually used (derived from user_seed, noise_stream)
   uint64_t user_seed = 0x5eed5eedULL;
   uint64_t noise_stream = 0;
+  std::map<uint64_t, uint64_t> stream_pos;   // saved Philox counter of the streams not selected
   // data parallelism (iwae_dp_init)
   int dp_rank = 0, dp_world = 1;
   bool dp_weighted = false;            // forward_backward writes B_local * grad and B_local at grad[nparam_int]
@@ -168,19 +169,20 @@ struct iwae_handle {
   std::map<std::vector<long long>, TcRec> tc_plans;
   int engine = 1;                    // train step on the row-chain engine when it applies (iwae_set_path)
   int engine_img = 1;                // ... with the first encoder layer's l2 / head on its image-row jobs
-  int engine_fold0 = 0;              // ... its l2 / head folded into the forward jobs at small batches (env IWAE_TC_FOLD0)
-  int engine_img_bwd = 1;            // ... their backward on the image-row job at small batches too (env IWAE_TC_IMGBWD)
-  int tc_xcd = 1;                    // XCD-aware job placement of the engine launches (env IWAE_TC_XCD)
-  int tc_bound = 1;                  // the train step's bound inside the engine's backward launch (env IWAE_TC_BOUND)
+  int engine_fold0 = 0;              // ... its l2 / head folded into the forward jobs at small batches
+  int engine_img_bwd = 1;            // ... their backward on the image-row job at small batches too
+  int tc_xcd = 1;                    // XCD-aware job placement of the engine launches
+  int tc_bound = 1;                  // the train step's bound inside the engine's backward launch
   bool adam_splits = false;          // the Adam launch being built also rewrites the split copies
-  int upd = 1;                       // fused weight-gradient + Adam + FX update launch (env IWAE_UPD)
-  long long upd_rows = 4096;         // ... up to this many sample rows per step (env IWAE_UPD_ROWS)
-  int upd_dbg = 0;                   // timing ablations of that launch (env IWAE_UPD_DBG; wrong results)
-  int upd_split = 0;                 // ... split over two graph branches (env IWAE_UPD_SPLIT)
-  int upd_tn32 = 0;                  // ... sample-row layers in 64 x 32 tiles (env IWAE_UPD_TN32)
-  int upd_slabs = 1;                 // ... and beyond upd_rows its split-K gradient pass into the slabs (env IWAE_UPD_SLABS)
-  int upd_img = 0;                   // ... with the first encoder layer's backward inside it (env IWAE_UPD_IMG)
-  bool upd_fuse_img = false;         // (set per step by engine_train_body for run_update)
+  int upd = 1;                       // fused weight-gradient + Adam + FX update launch
+  long long upd_rows = 4096;         // ... up to this many sample rows per step
+  int upd_tn32 = 0;                  // ... sample-row layers in 64 x 32 tiles
+  int upd_slabs = 1;                 // ... and beyond upd_rows its split-K gradient pass into the slabs
+  long long upd_slab_wg = 512;       // sample-row workgroups of that pass
+  long long dw_target = 768;         // split-K target workgroups per layer of the grouped weight-gradient GEMMs
+  int smallm_rows = 32;              // first encoder layer on the few-row launches up to this many images (0: never)
+  long long nll_rows = 1LL << 20;    // sample rows per NLL chunk (measured fastest: 2^17-2^20 within 10 %)
+  int tc_rt = 1;                     // row tiles of 16 per engine workgroup (2 and 4 spill registers)
   // graphs
   bool use_graphs = false;
   // a captured train step; its first kernel reads the caller's x directly
@@ -383,11 +385,7 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
     for (auto& d : h->dense) {
       const long long R = d.rows_kind == 0 ? Bimg : rows;
       const long long tiles = cdiv(d.fin + 1, 64) * cdiv(d.fout, 64);
-      static const long long kSlabTarget = [] {      // tuning knob: split-K target workgroups per layer
-        const char* e = std::getenv("IWAE_DW_TARGET");
-        return e ? std::max(1LL, std::atoll(e)) : 768LL;
-      }();
-      long long S = std::max(1LL, cdiv(kSlabTarget, tiles));
+      long long S = std::max(1LL, cdiv(h->dw_target, tiles));   // split-K target workgroups per layer
       // at most 16 slabs (the Adam kernel sums up to 16 with all loads in flight;
       // more slabs only add write + read traffic at large batch)
       S = std::min(S, std::min(16LL, std::max(1LL, cdiv(R, 64))));
@@ -1013,11 +1011,7 @@ static int smallm(iwae_handle* h, const Mat& A, int rows, const DenseL& d, bool 
   return IWAE_OK;
 }
 static bool smallm_ok(const iwae_handle* h, int rows) {
-  static const int max_rows = [] {      // tuning knob (0: never the few-row launches)
-    const char* e = std::getenv("IWAE_SMALLM_ROWS");
-    return e ? std::atoi(e) : 32;
-  }();
-  if (rows > std::min(max_rows, 32)) return false;
+  if (rows > std::min(h->smallm_rows, 32)) return false;      // (0: never the few-row launches)
   for (int di : {h->enc[0].l1, h->enc[0].l2, h->enc[0].head})
     if (h->dense[di].fin + 1 > 1024 || h->dense[di].fout > 1024) return false;
   return true;
@@ -1462,10 +1456,7 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hi
     long long st_tiles = 0;                      // sample-row tiles: nsplit of them per CU pair
     for (const WJ& w : js)
       if (w.rows == M) st_tiles += cdiv(h->dense[w.di].fin + 1, 64) * cdiv(h->dense[w.di].fout, 64);
-    static const long long target = [] {        // tuning knob: sample-row workgroups of the pass
-      const char* e = std::getenv("IWAE_UPD_SLAB_WG");
-      return e ? std::max(1LL, std::atoll(e)) : 512LL;
-    }();
+    const long long target = h->upd_slab_wg;     // sample-row workgroups of the pass
     nsplit = (int)std::max(1LL, (target + st_tiles / 2) / std::max(1LL, st_tiles));
     a.search = 1;
   }
@@ -1482,9 +1473,6 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hi
     J.tn = (h->upd_tn32 && w.rows == M) ? 32 : 64;
     J.tiles_m = (int)cdiv(d.fin + 1, 64); J.tiles_n = (int)cdiv(d.fout, J.tn);
     J.tile0 = tiles;
-    J.dbg = h->upd_dbg;
-    const StochL& S0 = h->enc[0];
-    J.wait_img = h->upd_fuse_img && (w.di == S0.l1 || w.di == S0.l2 || w.di == S0.head);
     J.nsplit = 1;
     if (slabs) {
       // row chunks of whole 128-row iterations, at most the layer's slab count
@@ -1510,31 +1498,6 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hi
   a.nheavy = heavy;
   a.per_xcd = (int)cdiv(heavy, 8);
   a.per_xcd2 = (int)cdiv(tiles - heavy, 8);
-  if (h->upd_fuse_img && part == 0) {
-    // the first encoder layer's backward (job I''s work) in this launch
-    const StochL& S0 = h->enc[0];
-    const DenseL& dh = h->dense[S0.head];
-    const DenseL& dl = h->dense[S0.l2];
-    a.nimg = P.Bimg; a.per_img = (int)cdiv(P.Bimg, 8);
-    a.nwait = 0;
-    for (int j = 0; j < a.njobs; ++j)
-      if (a.job[j].wait_img) a.nwait += a.job[j].tiles_m * a.job[j].tiles_n;
-    a.ctr = h->ds->upd_ctr;
-    a.P0 = h->eb[0].P.p; a.ldP0 = h->eb[0].P.ld; a.d0 = S0.d; a.kS = P.kS; a.stdnormal = h->L == 1;
-    a.h1 = h->h[0].p; a.ldh1 = h->h[0].ld; a.eps1 = h->eps_st[0].p; a.ldeps1 = h->eps_st[0].ld; a.dlw = h->dlw;
-    a.nsrc = 0;
-    a.src[a.nsrc] = h->dh_out[0].p; a.ldsrc[a.nsrc++] = h->dh_out[0].ld;
-    if (h->L >= 2) {
-      a.src[a.nsrc] = h->dh_prior[0].p; a.ldsrc[a.nsrc++] = h->dh_prior[0].ld;
-      a.src[a.nsrc] = h->dh_enc[0].p; a.ldsrc[a.nsrc++] = h->dh_enc[0].ld;
-    }
-    for (int q = a.nsrc; q < 3; ++q) { a.src[q] = a.src[0]; a.ldsrc[q] = a.ldsrc[0]; }
-    a.dP0 = h->eb[0].dP.p; a.lddP0 = h->eb[0].dP.ld;
-    a.Wh = h->params + dh.off; a.ldWh = dh.ldw; a.Hh = dh.fin;
-    a.Wl = h->params + dl.off; a.ldWl = dl.ldw; a.Hl = dl.fin;
-    a.y2 = h->eb[0].y2.p; a.ldy2 = h->eb[0].y2.ld; a.y1 = h->eb[0].y1.p; a.ldy1 = h->eb[0].y1.ld;
-    a.dY2 = h->eb[0].dY2.p; a.lddY2 = h->eb[0].dY2.ld; a.dY1 = h->eb[0].dY1.p; a.lddY1 = h->eb[0].dY1.ld;
-  }
   a.param = h->params; a.m = h->adam_m; a.v = h->adam_v; a.grad = slabs ? h->slabs : h->grad;
   a.fx_hi = h->fx_hi; a.fx_lo = h->fx_lo;
   a.state = &h->ds->adam; a.do_adam = adam && !slabs ? 1 : 0;
@@ -1862,8 +1825,7 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
   const long long rows = img ? (long long)P.Bimg : (long long)P.Bimg * kS;
   // image rows: one image per workgroup (latency-bound chains of a few rows), up to 256 workgroups
   const int row_step = img ? (int)std::max<long long>(1, cdiv(P.Bimg, 256)) : 0;
-  int want = 1;                         // (2 and 4 row tiles spill registers: knob only)
-  if (const char* e = std::getenv("IWAE_TC_RT")) want = std::atoi(e);   // tuning knob
+  const int want = h->tc_rt;            // (2 and 4 row tiles spill registers: knob only)
   iwae_handle::TcRec rec;
   for (int rt : {4, 2, 1}) {
     if (rt > want) continue;
@@ -2060,30 +2022,7 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   // Its image-row job also at small batches (B = 20: step 128.1 -> 126.4 us
   // against the row-block Gaussian backward + two few-row launches)
   const bool img_bwd = img || h->engine_img_bwd;
-  // the first encoder layer's backward inside the update launch (its short
-  // tiles wait for it there): every workgroup of that launch must be resident
-  h->upd_fuse_img = false;
-  if (img_bwd && h->upd_img && !h->upd_split && use_update(h, P) && h->enc[0].d <= 256 &&
-      h->dense[h->enc[0].head].fin <= 512) {
-    long long tiles = 0;
-    for (const DenseL& d : h->dense) tiles += cdiv(d.fin + 1, 64) * cdiv(d.fout, h->upd_tn32 ? 32 : 64);
-    h->upd_fuse_img = tiles + P.Bimg + 16 <= 240;
-  }
-  if (use_update(h, P) && img_bwd && h->upd_split && !h->dp_weighted) {
-    // two branches: the update of every layer after the first encoder layer
-    // (its inputs are complete) beside the first layer's backward, then that
-    // layer's update
-    HIPCHK(hipEventRecord(h->ev_fork, h->stream));
-    HIPCHK(hipStreamWaitEvent(h->side_stream, h->ev_fork, 0));
-    CHK(run_update(h, P, adam, 1, h->side_stream));
-    CHK(tc_run(h, P, E, 3));
-    CHK(run_update(h, P, adam, 2));
-    HIPCHK(hipEventRecord(h->ev_join, h->side_stream));
-    HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
-    if (adam) h->fx_version = h->params_version;
-    return IWAE_OK;
-  }
-  if (img_bwd && !h->upd_fuse_img) CHK(tc_run(h, P, E, 3));
+  if (img_bwd) CHK(tc_run(h, P, E, 3));
   else if (!img_bwd) CHK(fused_encoder_bwd(h, P, h->dlw, 0));
   if (use_update(h, P) && h->dp_weighted) {
     // data parallel: the fused gradient pass (B_local * g, B_local in the
@@ -2341,24 +2280,9 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   h->fx_lo = h->fx_hi + h->fx_elems;
   e = rb_setup_attributes();
   if (e == hipSuccess) e = mega_setup_attributes();
-  if (const char* w = std::getenv("IWAE_TRAIN_OUT_X3_ROWS")) h->out_x3_rows = std::atoll(w);   // tuning knob
-  if (const char* w = std::getenv("IWAE_MG_WAVES")) h->mg_waves = std::atoi(w) == 4 ? 4 : 8;   // tuning knob
   if (e == hipSuccess) e = smallm_setup_attributes();
   if (e == hipSuccess) e = tc_setup_attributes();
   if (e == hipSuccess) e = upd_setup_attributes();
-  if (const char* w = std::getenv("IWAE_UPD")) h->upd = std::atoi(w) != 0;              // A/B switch
-  if (const char* w = std::getenv("IWAE_UPD_ROWS")) h->upd_rows = std::atoll(w);        // tuning knob
-  if (const char* w = std::getenv("IWAE_UPD_DBG")) h->upd_dbg = std::atoi(w);           // timing ablations
-  if (const char* w = std::getenv("IWAE_UPD_SPLIT")) h->upd_split = std::atoi(w) != 0;  // A/B switch
-  if (const char* w = std::getenv("IWAE_UPD_TN32")) h->upd_tn32 = std::atoi(w) != 0;    // A/B switch
-  if (const char* w = std::getenv("IWAE_UPD_SLABS")) h->upd_slabs = std::atoi(w) != 0;  // A/B switch
-  if (const char* w = std::getenv("IWAE_UPD_IMG")) h->upd_img = std::atoi(w) != 0;      // A/B switch
-  if (const char* w = std::getenv("IWAE_ENGINE")) h->engine = std::atoi(w) != 0;   // A/B switch
-  if (const char* w = std::getenv("IWAE_TC_IMG")) h->engine_img = std::atoi(w) != 0;   // A/B switch
-  if (const char* w = std::getenv("IWAE_TC_IMGBWD")) h->engine_img_bwd = std::atoi(w) != 0;   // A/B switch
-  if (const char* w = std::getenv("IWAE_TC_FOLD0")) h->engine_fold0 = std::atoi(w) != 0;     // A/B switch
-  if (const char* w = std::getenv("IWAE_TC_XCD")) h->tc_xcd = std::atoi(w) != 0;       // A/B switch
-  if (const char* w = std::getenv("IWAE_TC_BOUND")) h->tc_bound = std::atoi(w) != 0;   // A/B switch
   if (e != hipSuccess) {
     g_create_error = std::string("hipFuncSetAttribute failed: ") + hipGetErrorString(e);
     iwae_destroy(h);
@@ -2413,19 +2337,39 @@ static uint64_t splitmix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+// The Philox key of the handle's current noise stream, and the device counter
+// position: each stream keeps its own position (saved / restored on a switch),
+// so switching back to a stream never replays its noise, and re-selecting the
+// current stream is a no-op (a data-parallel loop that evaluates with the
+// sharded NLL between steps keeps drawing fresh noise).
+static void derive_key(iwae_handle* h) {
+  h->seed = h->noise_stream == 0 ? h->user_seed : splitmix64(h->user_seed ^ splitmix64(h->noise_stream));
+  for (auto& kv : h->graphs) destroy_graph(kv.second);   // the key is a captured kernel argument
+  h->graphs.clear();
+}
+
 int iwae_set_noise_stream(iwae_handle* h, unsigned long long stream) {
   if (!h) return IWAE_EINVAL;
+  if (stream == h->noise_stream) return IWAE_OK;
+  uint64_t z[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(z, h->ds->rng, sizeof(z), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->stream_pos[h->noise_stream] = z[0];
+  auto it = h->stream_pos.find(stream);
+  z[0] = it == h->stream_pos.end() ? 0 : it->second;
+  z[1] = 0;
   h->noise_stream = stream;
-  return iwae_set_seed(h, h->user_seed);
+  derive_key(h);
+  HIPCHK(hipMemcpyAsync(h->ds->rng, z, sizeof(z), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return IWAE_OK;
 }
 
 int iwae_set_seed(iwae_handle* h, unsigned long long seed) {
   if (!h) return IWAE_EINVAL;
   h->user_seed = seed;
-  // Philox key of this handle's noise stream (per rank under data parallelism)
-  h->seed = h->noise_stream == 0 ? seed : splitmix64(seed ^ splitmix64(h->noise_stream));
-  for (auto& kv : h->graphs) destroy_graph(kv.second);   // seed is a captured kernel argument
-  h->graphs.clear();
+  derive_key(h);
+  h->stream_pos.clear();                 // every stream restarts from counter 0
   uint64_t z[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(h->ds->rng, z, sizeof(z), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -2455,6 +2399,47 @@ int iwae_set_precision(iwae_handle* h, int mode) {
 int iwae_set_graphs(iwae_handle* h, int enable) {
   if (!h) return IWAE_EINVAL;
   h->use_graphs = enable != 0;
+  return IWAE_OK;
+}
+
+int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
+  if (!h) return IWAE_EINVAL;
+  const bool on = value != 0;
+  switch (knob) {
+    case IWAE_KNOB_ENGINE: h->engine = on; break;
+    case IWAE_KNOB_TC_IMG: h->engine_img = on; break;
+    case IWAE_KNOB_TC_IMGBWD: h->engine_img_bwd = on; break;
+    case IWAE_KNOB_TC_FOLD0: h->engine_fold0 = on; break;
+    case IWAE_KNOB_TC_XCD: h->tc_xcd = on; break;
+    case IWAE_KNOB_TC_BOUND: h->tc_bound = on; break;
+    case IWAE_KNOB_TC_RT:
+      if (value != 1 && value != 2 && value != 4) return fail(h, IWAE_EINVAL, "TC_RT must be 1, 2 or 4");
+      h->tc_rt = (int)value;
+      break;
+    case IWAE_KNOB_UPD: h->upd = on; break;
+    case IWAE_KNOB_UPD_ROWS: h->upd_rows = std::max(0LL, value); break;
+    case IWAE_KNOB_UPD_TN32: h->upd_tn32 = on; break;
+    case IWAE_KNOB_UPD_SLABS: h->upd_slabs = on; break;
+    case IWAE_KNOB_UPD_SLAB_WG: h->upd_slab_wg = std::max(1LL, value); break;
+    case IWAE_KNOB_DW_TARGET:
+      h->dw_target = std::max(1LL, value);
+      free_workspace(h);                 // the slab layout depends on it
+      break;
+    case IWAE_KNOB_SMALLM_ROWS: h->smallm_rows = (int)std::max(0LL, std::min(value, 32LL)); break;
+    case IWAE_KNOB_OUT_X3_ROWS: h->out_x3_rows = std::max(0LL, value); break;
+    case IWAE_KNOB_MG_WAVES:
+      if (value != 4 && value != 8) return fail(h, IWAE_EINVAL, "MG_WAVES must be 4 or 8");
+      h->mg_waves = (int)value;
+      break;
+    case IWAE_KNOB_NLL_ROWS: h->nll_rows = std::max(1LL, value); break;
+    default: return fail(h, IWAE_EINVAL, "unknown tuning knob " + std::to_string(knob));
+  }
+  // captured steps and engine plans were built for the previous setting
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (auto& kv : h->graphs) destroy_graph(kv.second);
+  h->graphs.clear();
+  for (auto& kv : h->tc_plans) (void)hipFree(kv.second.dev);
+  h->tc_plans.clear();
   return IWAE_OK;
 }
 
@@ -2624,27 +2609,26 @@ int iwae_dp_unique_id(void* out128) {
 
 int iwae_dp_init(iwae_handle* h, int rank, int world, const void* uid) {
   if (!h) return IWAE_EINVAL;
+  // every argument is checked before any handle state changes: a failed call
+  // leaves the handle (communicator, weighting, noise stream) as it was
   if (world < 1 || rank < 0 || rank >= world) return fail(h, IWAE_EINVAL, "need 0 <= rank < world");
-  HIPCHK(hipStreamSynchronize(h->stream));
-  if (h->comm) {
-    (void)ncclCommDestroy(h->comm);
-    h->comm = nullptr;
-  }
-  h->dp_rank = rank;
-  h->dp_world = world;
-  h->dp_weighted = world > 1 || uid != nullptr;
-  if (h->dp_weighted && h->grad != h->grad_own)
+  const bool weighted = world > 1 || uid != nullptr;
+  if (weighted && h->grad != h->grad_own)
     return fail(h, IWAE_EINVAL, "iwae_dp_init before binding a grad buffer (then bind n + 4 floats)");
+  HIPCHK(hipStreamSynchronize(h->stream));
+  ncclComm_t comm = nullptr;
   if (uid) {
     ncclUniqueId id;
     std::memcpy(&id, uid, sizeof(id));
     HIPCHK(hipSetDevice(h->device));
-    const ncclResult_t r = ncclCommInitRank(&h->comm, world, id, rank);
-    if (r != ncclSuccess) {
-      h->comm = nullptr;
-      return fail(h, IWAE_EHIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-    }
+    const ncclResult_t r = ncclCommInitRank(&comm, world, id, rank);
+    if (r != ncclSuccess) return fail(h, IWAE_EHIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
   }
+  if (h->comm) (void)ncclCommDestroy(h->comm);
+  h->comm = comm;
+  h->dp_rank = rank;
+  h->dp_world = world;
+  h->dp_weighted = weighted;
   for (auto& kv : h->graphs) destroy_graph(kv.second);
   h->graphs.clear();
   return iwae_set_noise_stream(h, (unsigned long long)rank);
@@ -2825,8 +2809,7 @@ static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, flo
   if (!x) return fail(h, IWAE_EINVAL, "x is NULL");
   if (N <= 0 || k <= 0) return fail(h, IWAE_EINVAL, "N and k must be positive");
   // 2^20 sample rows per chunk (measured fastest: 2^17-2^20 within 10 %, smaller slower)
-  long long nll_rows = 1LL << 20;
-  if (const char* e = std::getenv("IWAE_NLL_ROWS")) nll_rows = std::max(1LL, std::atoll(e));   // tuning knob
+  const long long nll_rows = h->nll_rows;
   const long long target_rows = std::max<long long>(nll_rows, k);
   int imgs = chunk > 0 ? chunk : (int)std::max<long long>(1, target_rows / k);
   imgs = std::min(imgs, N);

@@ -26,7 +26,7 @@
 //
 // Measured (B = 20, k = 50: 186 tiles, 1000 rows): 25.6 us against 31.2 us
 // for the grouped split-K GEMM + Adam + FX-refresh launches it replaces
-// (16.5 + 9.3 + 5.4), step 137.6 -> 132.5 us.  Ablations (IWAE_UPD_DBG):
+// (16.5 + 9.3 + 5.4), step 137.6 -> 132.5 us.  Ablations (-DIWAE_UPD_ABLATE):
 // launch + first loads 3.7 us, reduction 14 us, epilogue (Adam, stores,
 // FX / GX) 8 us.  Tried and measured slower: lanes spread over 8 or 16 rows
 // per load instruction (19 us reduction), the multiply and the staging in
@@ -45,6 +45,13 @@ constexpr int UP_S = 72;                    // dwords per LDS row: 128 bf16 + 16
 constexpr int UP_PLANE = 64 * UP_S;         // dwords per plane
 constexpr int UP_BUF = 4 * UP_PLANE;        // X hi, X lo, dZ hi, dZ lo
 constexpr int UP_G = 8;                     // iterations per unrolled group (1024 rows)
+// Timing ablations (debug builds only, -DIWAE_UPD_ABLATE=<mask>; WRONG results):
+// 4 no operand loads, 8 stop after the reduction, 16 no FX / GX copies, 32 no
+// Adam, 64 no reduction (tools/upd_ablate.sh)
+#ifndef IWAE_UPD_ABLATE
+#define IWAE_UPD_ABLATE 0
+#endif
+constexpr int kUpdAblate = IWAE_UPD_ABLATE;
 
 extern __shared__ __attribute__((aligned(16))) float ups[];
 
@@ -136,7 +143,7 @@ template <int TN>
 __device__ __forceinline__ UpOff up_offsets(const UpdJob& J, int i0, int j0) {
   const int t = threadIdx.x, rg = up_rg(t), cq = up_cq(t);
   const int ci = i0 + 4 * cq, cj = j0 + (TN / 16) * cq;
-  const bool okx = ci < J.lda && !(J.dbg & 4), okz = cj < J.ldb && !(J.dbg & 4);
+  const bool okx = ci < J.lda && !(kUpdAblate & 4), okz = cj < J.ldb && !(kUpdAblate & 4);
   UpOff o;
   o.x = okx ? (unsigned)(8 * rg * J.lda + ci) * 4u : kOOB;     // kOOB + 7 rows stays out of range
   o.z = okz ? (unsigned)(8 * rg * J.ldb + cj) * 4u : kOOB;
@@ -238,7 +245,7 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
   // never carried around a loop (a loop-carried set is renamed at the back
   // edge with register copies, which drain every load in flight); loads past
   // the last row are unconditional out-of-range reads of zeros
-  const int ngrp = (J.dbg & 64) ? 0 : (J.rows + UP_G * UP_RI - 1) / (UP_G * UP_RI);
+  const int ngrp = (kUpdAblate & 64) ? 0 : (J.rows + UP_G * UP_RI - 1) / (UP_G * UP_RI);
   float* buf0 = ups;
   float* buf1 = ups + UP_BUF;
   const UpOff O = up_offsets<TN>(J, i0, j0);
@@ -313,7 +320,7 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
     adam_prefetch();
   }
   __syncthreads();
-  if (J.dbg & 8) return;
+  if (kUpdAblate & 8) return;
 
   // the four waves' tiles -> LDS, summed in wave order
   {
@@ -348,7 +355,7 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
       *reinterpret_cast<float4*>(a.grad + J.off + (long long)(i0 + ei) * J.ldw + c) =
           make_float4(a.gscale * g[4 * q], a.gscale * g[4 * q + 1], a.gscale * g[4 * q + 2], a.gscale * g[4 * q + 3]);
   }
-  if (!a.do_adam || (J.dbg & 32)) return;
+  if (!a.do_adam || (kUpdAblate & 32)) return;
 
   // Adam (adam_kernel's arithmetic)
   const float tt = (float)st.t;
@@ -377,7 +384,7 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
     }
     *reinterpret_cast<float4*>(pw + ei * PS + ej + 4 * q) = make_float4(pq[0], pq[1], pq[2], pq[3]);
   }
-  if (J.fx_off < 0 || (J.dbg & 16)) return;   // no fragment-major copies (the f32 input layer)
+  if (J.fx_off < 0 || (kUpdAblate & 16)) return;   // no fragment-major copies (the f32 input layer)
   __syncthreads();
   // FX chunks: (feature jj, 8 W_aug rows 8 ib ..) -> lane (pos & 15) + 16 ((k % 32) / 8) of step k / 32
 #pragma unroll
@@ -422,142 +429,17 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
   }
 }
 
-// The first encoder layer's backward of image b (see UpdArgs), exact f32.
-// Latency-bound chains of loads: every load of a batch is issued before the
-// first is used (UP_SB samples per thread, UP_GB float4 of a weight row).
-constexpr int UP_SB = 13, UP_GB = 25;
-// LDS: dP0 [2 d0], dY2 [Hh], the two sample groups' partial sums.
-__device__ __forceinline__ void upd_image(const UpdArgs& a, int b) {
-  const int t = threadIdx.x;
-  const int d = a.d0, kS = a.kS;
-  float* sdp = ups;                     // [2 d] dP0
-  float* sdy = ups + 512;               // [Hh] dY2
-  float* part = ups + 1024;             // [2][2 * 128] partial (dmu, dscale)
-  // dP0: thread (column c, sample parity sg); samples in a fixed order
-  const __amdgpu_buffer_rsrc_t rh = buf_rsrc(a.h1), re = buf_rsrc(a.eps1), rd = buf_rsrc(a.dlw);
-  const __amdgpu_buffer_rsrc_t rs0 = buf_rsrc(a.src[0]), rs1 = buf_rsrc(a.src[1]), rs2 = buf_rsrc(a.src[2]);
-  const int sg = t >> 7;
-  for (int c0 = 0; c0 < d; c0 += 128) {
-    const int c = c0 + (t & 127);
-    const bool live = c < d;
-    const int cc = live ? c : d - 1;
-    const float* Pr = a.P0 + (size_t)b * a.ldP0;
-    const float mu = Pr[cc], zs = Pr[d + cc];
-    const float rs = frcp(fexp(zs) + kScaleEps);
-    float dmu = 0.f, dsc = 0.f;
-    for (int s0 = sg; s0 < kS; s0 += 2 * UP_SB) {
-      float hv[UP_SB], ev[UP_SB], dl[UP_SB], G[UP_SB];
-#pragma unroll
-      for (int i = 0; i < UP_SB; ++i) {
-        const int s = s0 + 2 * i;
-        const bool ok = live && s < kS;
-        const unsigned r = (unsigned)(b * kS + (s < kS ? s : kS - 1));
-        hv[i] = bld1(rh, ok ? (r * a.ldh1 + c) * 4u : kOOB);
-        ev[i] = bld1(re, ok ? (r * a.ldeps1 + c) * 4u : kOOB);
-        dl[i] = bld1(rd, ok ? r * 4u : kOOB);
-        G[i] = (bld1(rs0, ok && a.nsrc > 0 ? (r * a.ldsrc[0] + c) * 4u : kOOB) +
-                bld1(rs1, ok && a.nsrc > 1 ? (r * a.ldsrc[1] + c) * 4u : kOOB)) +
-               bld1(rs2, ok && a.nsrc > 2 ? (r * a.ldsrc[2] + c) * 4u : kOOB);
-      }
-#pragma unroll
-      for (int i = 0; i < UP_SB; ++i) {
-        const float h = hv[i];
-        const float z = h * rs - mu * rs;
-        const float dlq = -dl[i];
-        float g = G[i];
-        if (a.stdnormal) g += dl[i] * (-h);
-        g += dlq * (-z * rs);
-        dmu += g + dlq * (z * rs);
-        dsc += g * ev[i] + dlq * ((z * z - 1.f) * rs);
-      }
-    }
-    part[sg * 256 + (t & 127)] = dmu;
-    part[sg * 256 + 128 + (t & 127)] = dsc;
-    __syncthreads();
-    if (t < 128 && live) {
-      const float m = part[t] + part[256 + t];
-      const float v = (part[128 + t] + part[256 + 128 + t]) * fexp(zs);   // dzs = dscale * exp(zs)
-      sdp[c] = m;
-      sdp[d + c] = v;
-      a.dP0[(size_t)b * a.lddP0 + c] = m;
-      a.dP0[(size_t)b * a.lddP0 + d + c] = v;
-    }
-    __syncthreads();
-  }
-  // dY2[n] = (sum_j dP0[j] Wh[n][j]) (1 - y2[n]^2): a thread per row n, its
-  // row read as float4s (every load of a batch in flight), the vector from
-  // LDS, summed in column order
-  auto gemv = [&](const float* W, int ldw, int nrow, int ncol, const float* vec, const float* y, int ldy,
-                  float* out_g, int ldo, float* out_s) __attribute__((always_inline)) {
-    const __amdgpu_buffer_rsrc_t rw = buf_rsrc(W);        // (wave-uniform base; the row is in the offset)
-    for (int n = t; n < nrow; n += UP_NT) {
-      const unsigned rb = (unsigned)n * (unsigned)ldw * 4u;
-      const int n4 = (ncol + 3) >> 2;
-      float acc = 0.f;
-      for (int q0 = 0; q0 < n4; q0 += UP_GB) {
-        float4 wv[UP_GB];
-#pragma unroll
-        for (int i = 0; i < UP_GB; ++i) wv[i] = bld4(rw, q0 + i < n4 ? rb + (unsigned)(q0 + i) * 16u : kOOB);
-#pragma unroll
-        for (int i = 0; i < UP_GB; ++i) {
-          const int j = 4 * (q0 + i);
-          if (q0 + i < n4) acc += ((wv[i].x * vec[j] + wv[i].y * vec[j + 1]) + wv[i].z * vec[j + 2]) + wv[i].w * vec[j + 3];
-        }
-      }
-      const float yv = y[(size_t)b * ldy + n];
-      const float v = acc * (1.f - yv * yv);
-      if (out_s) out_s[n] = v;
-      out_g[(size_t)b * ldo + n] = v;
-    }
-  };
-  // (the vectors' padding to a float4 is zero)
-  for (int j = 2 * d + t; j < 4 * ((2 * d + 3) / 4); j += UP_NT) sdp[j] = 0.f;
-  for (int j = a.Hh + t; j < 4 * ((a.Hh + 3) / 4); j += UP_NT) sdy[j] = 0.f;
-  __syncthreads();
-  gemv(a.Wh, a.ldWh, a.Hh, 2 * d, sdp, a.y2, a.ldy2, a.dY2, a.lddY2, sdy);
-  __syncthreads();
-  // dY1[n] = (sum_m dY2[m] Wl[n][m]) (1 - y1[n]^2)
-  gemv(a.Wl, a.ldWl, a.Hl, a.Hh, sdy, a.y1, a.ldy1, a.dY1, a.lddY1, nullptr);
-  // publish (every storing wave drained, then one agent release and the count)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(&a.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// A short tile's wait for the images (bounded: a missing producer cannot hang
-// the launch; ctr[0] then stays short of nimg and the result is wrong instead)
-__device__ __forceinline__ void upd_wait_images(const UpdArgs& a) {
-  if (threadIdx.x == 0) {
-    for (int i = 0; i < (1 << 22); ++i) {
-      if (__hip_atomic_load(&a.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)a.nimg) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-}
-
 __global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
   // tile of this workgroup: consecutive tiles (sharing an operand slice) on one XCD
   // (the long reductions -- tiles [0, nheavy) -- are spread evenly over the
   // XCDs first, the short ones after, so no XCD gets more long tiles than CUs)
-  // (then the in-launch image backward's workgroups, then the short tiles)
   const int b = blockIdx.x, x = b & 7, sl = b >> 3;
   int T;
   if (sl < a.per_xcd) {
     T = x * a.per_xcd + sl;
     if (T >= a.nheavy) return;
-  } else if (sl < a.per_xcd + a.per_img) {
-    const int im = x * a.per_img + (sl - a.per_xcd);
-    if (im < a.nimg) upd_image(a, im);
-    return;
   } else {
-    const int s2 = sl - a.per_xcd - a.per_img;
+    const int s2 = sl - a.per_xcd;
     T = a.nheavy + x * a.per_xcd2 + s2;
     if (s2 >= a.per_xcd2 || T >= a.ntiles) return;
   }
@@ -571,7 +453,6 @@ __global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
   // Adam constants (state->t was advanced for this step by the bound), read
   // now: in flight during the reduction
   const AdamState st = *a.state;
-  if (J.wait_img && a.nimg > 0) upd_wait_images(a);
   if (J.nsplit > 1) {
     // split s of the rows: this tile's partial sum into slab s
     const int per = J.tiles_m * J.tiles_n, lt = T - J.tile0, s = lt / per;
@@ -588,21 +469,11 @@ __global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
   } else {
     upd_tile<64>(a, J, st, b, T - J.tile0);
   }
-  if (J.wait_img && a.nimg > 0) {
-    // the last short tile resets the counters for the next launch (every short
-    // tile has passed its wait by then)
-    __syncthreads();
-    if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(&a.ctr[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)a.nwait - 1) {
-      __hip_atomic_store(&a.ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&a.ctr[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 hipError_t launch_update(hipStream_t st, const UpdArgs& a) {
   if (a.ntiles <= 0) return hipSuccess;
-  const unsigned grid = 8u * (unsigned)(a.per_xcd + a.per_img + a.per_xcd2);
+  const unsigned grid = 8u * (unsigned)(a.per_xcd + a.per_xcd2);
   hipLaunchKernelGGL(upd_kernel, dim3(grid), dim3(UP_NT), (size_t)2 * UP_BUF * sizeof(float), st, a);
   return hipGetLastError();
 }

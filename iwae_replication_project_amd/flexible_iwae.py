@@ -160,7 +160,7 @@ class Flexible_Model:
     def __init__(self, n_hidden_encoder, n_hidden_decoder, n_latent_encoder, n_latent_decoder,
                  dataset_bias="Binarized_MNIST", loss_function="VAE", k=50, p=1, alpha=1, beta=0.5,
                  *, k1=None, k2=None, x_dim=784, device=None, seed=None, use_graphs=True,
-                 kernel_path="auto", precision="bf16x3", **kwargs):
+                 kernel_path="auto", precision="bf16x3", tuning=None, **kwargs):
         self.dense = architecture(n_hidden_encoder, n_hidden_decoder, n_latent_encoder, n_latent_decoder, x_dim)
         loss_config(loss_function, k, p, alpha, beta, k1, k2)   # validate early
         if not torch.cuda.is_available():
@@ -210,6 +210,8 @@ class Flexible_Model:
         if precision not in precisions:
             raise ValueError(f"precision must be one of {tuple(precisions)}")
         self._call(self._lib.iwae_set_precision(h, precisions[precision]))
+        for name, value in (tuning or {}).items():
+            self.set_tuning(name, value)
         rng = np.random.default_rng(int(seed) & ((1 << 63) - 1))
         self.set_weights(glorot_weights(self.dense, rng, resolve_dataset_bias(dataset_bias, x_dim)))
         self._loss_buf = torch.zeros(1, device=self.device)
@@ -223,8 +225,18 @@ class Flexible_Model:
 
     def set_noise_stream(self, stream):
         """Select the noise stream (one per rank: Philox key derived from (seed,
-        stream); stream 0 is the seed's own) and restart its counter."""
+        stream); stream 0 is the seed's own).  Each stream continues from its
+        own counter position (re-selecting the current stream is a no-op);
+        ``set_seed`` restarts them all."""
         self._call(self._lib.iwae_set_noise_stream(self._h, int(stream) & ((1 << 64) - 1)))
+
+    def set_tuning(self, name, value):
+        """Kernel-variant / tuning knob of the library (include/iwae.h enum
+        iwae_knob, e.g. ``set_tuning("upd", 0)``): for A/B measurements and the
+        variant-agreement tests; the defaults are the measured-fastest paths."""
+        if name not in _lib.KNOBS:
+            raise ValueError(f"unknown tuning knob {name!r}; expected one of {tuple(_lib.KNOBS)}")
+        self._call(self._lib.iwae_set_tuning(self._h, _lib.KNOBS[name], int(value)))
 
     def _call(self, rc):
         _lib.check(self._lib, self._h, rc)

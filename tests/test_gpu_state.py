@@ -81,10 +81,10 @@ def test_training_statistics_rejects_ragged_batches():
 
 
 @pytest.mark.parametrize("B,k,L", [(20, 50, 2), (7, 64, 2), (33, 20, 2), (20, 5, 1)])
-def test_fused_update_matches_split_k_update(B, k, L, monkeypatch):
+def test_fused_update_matches_split_k_update(B, k, L):
     """The one-launch update (iwae_update.hip: weight gradients over all rows,
     Adam, FX / GX copies) against the split-K GEMM + Adam + FX-refresh launches
-    (IWAE_UPD=0) on the same injected noise: gradients to bf16x3 accumulation
+    (tuning knob upd = 0) on the same injected noise: gradients to bf16x3 accumulation
     order, and the next steps (which read the FX / GX copies the update wrote)
     stay on the same trajectory."""
     from iwae_replication_project_amd import Adam, Flexible_Model
@@ -97,9 +97,8 @@ def test_fused_update_matches_split_k_update(B, k, L, monkeypatch):
         m = Flexible_Model(*arch, dataset_bias=None, loss_function="IWAE", k=k, seed=9)
         m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
         return m
-    monkeypatch.setenv("IWAE_UPD", "0")
     ref = mk()
-    monkeypatch.delenv("IWAE_UPD")
+    ref.set_tuning("upd", 0)
     m = mk()
     for i in range(3):
         la = m.train_step(xs[i], eps=epss[i])["IWAE"]
@@ -119,7 +118,7 @@ def test_fused_update_matches_split_k_update(B, k, L, monkeypatch):
     assert np.abs(ma - mb).max() <= 1e-3 * np.abs(mb).max()
 
 
-def test_large_batch_slab_pass_matches_grouped_gemms(monkeypatch):
+def test_large_batch_slab_pass_matches_grouped_gemms():
     """Beyond 4096 sample rows the update kernel's split-K gradient pass (row
     chunks into the Adam slabs) replaces the grouped weight-gradient GEMMs:
     same loss, gradient and updated weights on the same injected noise."""
@@ -130,25 +129,23 @@ def test_large_batch_slab_pass_matches_grouped_gemms(monkeypatch):
     eps = [rng.standard_normal((k, B, d)).astype(np.float32) for d in ARCH2[2]]
 
     def step(flag):
-        monkeypatch.setenv("IWAE_UPD_SLABS", flag)
-        m = Flexible_Model(*ARCH2, dataset_bias=None, loss_function="IWAE", k=k, seed=13)
+        m = Flexible_Model(*ARCH2, dataset_bias=None, loss_function="IWAE", k=k, seed=13,
+                           tuning={"upd_slabs": flag})
         m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
         loss = m.train_step(x, eps=eps)["IWAE"]
-        monkeypatch.delenv("IWAE_UPD_SLABS", raising=False)
         return loss, _flat(m.get_gradients()), _flat(m.get_weights())
-    la, ga, wa = step("1")
-    lb, gb, wb = step("0")
+    la, ga, wa = step(1)
+    lb, gb, wb = step(0)
     assert la == lb                                   # the forward and bound are the same launches
     assert np.linalg.norm(ga - gb) <= 1e-5 * np.linalg.norm(ga)
     assert np.abs(wa - wb).max() <= 1e-6
 
 
-@pytest.mark.parametrize("env", ["IWAE_UPD_IMG", "IWAE_UPD_TN32", "IWAE_TC_FOLD0", "IWAE_TC_BOUND"])
-def test_train_step_variants_agree(env, monkeypatch):
-    """The measured-and-parked variants of the configs[1] step (first-layer
-    backward inside the update launch, 64x32 update tiles, first layer folded
-    into the forward jobs) and the bound's placement give the same step as the
-    default path on the same injected noise."""
+@pytest.mark.parametrize("knob", ["upd_tn32", "tc_fold0", "tc_bound"])
+def test_train_step_variants_agree(knob):
+    """The measured-and-parked variants of the configs[1] step (64x32 update
+    tiles, first layer folded into the forward jobs) and the bound's placement
+    give the same step as the default path on the same injected noise."""
     from iwae_replication_project_amd import Adam, Flexible_Model
     rng = np.random.default_rng(64)
     B, k = 20, 50
@@ -156,17 +153,15 @@ def test_train_step_variants_agree(env, monkeypatch):
     eps = [rng.standard_normal((k, B, d)).astype(np.float32) for d in ARCH2[2]]
 
     def step(flag):
-        if flag is not None:
-            monkeypatch.setenv(env, flag)
-        m = Flexible_Model(*ARCH2, dataset_bias=None, loss_function="IWAE", k=k, seed=12)
+        m = Flexible_Model(*ARCH2, dataset_bias=None, loss_function="IWAE", k=k, seed=12,
+                           tuning={} if flag is None else {knob: flag})
         m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
         loss = m.train_step(x, eps=eps)["IWAE"]
-        monkeypatch.delenv(env, raising=False)
         return loss, _flat(m.get_gradients())
     la, ga = step(None)
-    lb, gb = step("0" if env == "IWAE_TC_BOUND" else "1")
+    lb, gb = step(0 if knob == "tc_bound" else 1)
     # (the folded first layer runs l2 / head on bf16x3 products instead of exact
     # f32: both within the 1e-4 parity budget of the exact step, 5e-5 apart)
-    tol = 5e-5 if env == "IWAE_TC_FOLD0" else 1e-5
+    tol = 5e-5 if knob == "tc_fold0" else 1e-5
     assert abs(la - lb) <= tol * abs(la)
     assert np.linalg.norm(ga - gb) <= tol * np.linalg.norm(ga)

@@ -1,4 +1,4 @@
-"""NLL throughput vs chunk size (IWAE_NLL_ROWS) on the bench model (2L, k=5000)."""
+"""NLL throughput vs chunk size (tuning knob nll_rows) on the bench model (2L, k=5000)."""
 import os
 import sys
 import time
@@ -16,7 +16,7 @@ for prec in ("bf16x3", "f32"):
                        precision=prec)
     xd = m._x(x)
     for rows in (1 << 20, 1 << 18, 1 << 17, 1 << 16, 1 << 15):
-        os.environ["IWAE_NLL_ROWS"] = str(rows)
+        m.set_tuning("nll_rows", rows)
         m.log_px(xd[:64], 5000)
         torch.cuda.synchronize()
         t = time.perf_counter()
