@@ -116,7 +116,7 @@ enum iwae_knob {
   IWAE_KNOB_TC_FOLD0 = 4,      /* ... its l2 / head folded into the forward jobs (0) */
   IWAE_KNOB_TC_XCD = 5,        /* XCD-aware job placement of the engine launches (1) */
   IWAE_KNOB_TC_BOUND = 6,      /* the bound inside the engine's backward launch (1) */
-  IWAE_KNOB_TC_RT = 7,         /* 16-row tiles per engine workgroup: 1, 2 or 4 (1) */
+  IWAE_KNOB_TC_RT = 7,         /* 16-row tiles per engine workgroup below WIDE_ROWS: 1, 2 or 4 (1) */
   IWAE_KNOB_UPD = 8,           /* fused weight-gradient + Adam + FX update launch (1) */
   IWAE_KNOB_UPD_ROWS = 9,      /* ... up to this many sample rows per step (4096) */
   IWAE_KNOB_UPD_TN32 = 10,     /* ... sample-row layers in 64 x 32 tiles (0) */
@@ -126,7 +126,9 @@ enum iwae_knob {
   IWAE_KNOB_SMALLM_ROWS = 14,  /* few-row first-layer launches up to this many images, <= 32 (32) */
   IWAE_KNOB_OUT_X3_ROWS = 15,  /* row-block path: bf16x3 output layer from this many sample rows (8192) */
   IWAE_KNOB_MG_WAVES = 16,     /* NLL kernel workgroup: 8 waves / 64 rows or 4 waves / 32 rows (8) */
-  IWAE_KNOB_NLL_ROWS = 17      /* sample rows per NLL chunk (2^20) */
+  IWAE_KNOB_NLL_ROWS = 17,     /* sample rows per NLL chunk (2^20) */
+  IWAE_KNOB_WIDE_ROWS = 18,    /* engine: 32 / 64-row workgroups from this many sample rows (4097) */
+  IWAE_KNOB_DW_WIDE = 19       /* beyond UPD_ROWS: weight gradients on the 112 x 256-block kernel (1) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --

@@ -361,6 +361,25 @@ struct UpdArgs {
 hipError_t launch_update(hipStream_t st, const UpdArgs& a);
 hipError_t upd_setup_attributes();
 
+// Large-batch weight gradients into split-K slabs (iwae_dwgrad.hip): per layer,
+// workgroup blocks of 7 x 16 W_aug rows by 8 * nb x 16 columns over a row chunk.
+constexpr int kDwMT = 7;                              // 16-row tiles of W_aug rows per block
+struct DwJob {
+  const float* A; const float* B; const float* ks;   // X_aug [rows][lda] (ones column at fin), dZ [rows][ldb], dZ row scale
+  int lda, ldb, rows;
+  float* out; int ldo; long long slab_stride;        // slab s at out + s * slab_stride: [M][ldo]
+  int M, mt, nt;                                     // M = fin + 1; 16-tiles along M and along fout
+  int nb, mblocks, nblocks;                          // n-tiles per wave (1 or 2); blocks along M / N
+  int nsplit, chunk;                                 // row chunks (chunk % 32 == 0)
+  int tile0;                                         // first workgroup of the job (split-major)
+};
+constexpr int kDwMaxJobs = 20;
+struct DwArgs {
+  DwJob job[kDwMaxJobs]; int njobs, ntiles;
+};
+hipError_t launch_dw(hipStream_t st, const DwArgs& a);
+hipError_t dw_setup_attributes();
+
 // ------------------------------------------------- fused row-block kernels ----
 struct RbNoise {             // where a sampling layer's eps comes from (see eps_at)
   const float* eps_a; const float* eps_b;

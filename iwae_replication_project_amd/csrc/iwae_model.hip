@@ -179,10 +179,12 @@ struct iwae_handle {
   int upd_tn32 = 0;                  // ... sample-row layers in 64 x 32 tiles
   int upd_slabs = 1;                 // ... and beyond upd_rows its split-K gradient pass into the slabs
   long long upd_slab_wg = 512;       // sample-row workgroups of that pass
+  int dw_wide = 1;                   // ... run by the 112 x 256-block weight-gradient kernel (iwae_dwgrad.hip)
   long long dw_target = 768;         // split-K target workgroups per layer of the grouped weight-gradient GEMMs
   int smallm_rows = 32;              // first encoder layer on the few-row launches up to this many images (0: never)
   long long nll_rows = 1LL << 20;    // sample rows per NLL chunk (measured fastest: 2^17-2^20 within 10 %)
-  int tc_rt = 1;                     // row tiles of 16 per engine workgroup (2 and 4 spill registers)
+  int tc_rt = 1;                     // row tiles of 16 per engine workgroup below wide_rows
+  long long wide_rows = 4097;        // sample rows from which the engine runs 32 / 64-row workgroups
   // graphs
   bool use_graphs = false;
   // a captured train step; its first kernel reads the caller's x directly
@@ -1528,6 +1530,76 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hi
   return IWAE_OK;
 }
 
+// Large-batch weight gradients (iwae_dwgrad.hip): every layer's X_aug^T dZ in
+// 112 x (128 | 256) blocks split over row chunks into the slabs adam_kernel
+// sums; the chunks are sized so every workgroup has about the same MFMA work
+// (one round of the chip, one workgroup per CU), the heaviest layers first.
+static int run_dw(iwae_handle* h, const Plan& P) {
+  const int L = h->L, M = P.Bimg * P.kS;
+  struct WJ { int di; const Mat* A; const Mat* dZ; int rows; const float* ks; };
+  std::vector<WJ> js;
+  js.push_back({h->o3, &h->ob.y2, &h->ob.P, M, h->dpx});
+  js.push_back({h->o2, &h->ob.y1, &h->ob.dY2, M, nullptr});
+  js.push_back({h->o1, &h->h[0], &h->ob.dY1, M, nullptr});
+  for (int i = 0; i < L - 1; ++i) {
+    const StochL& S = h->dec[i];
+    js.push_back({S.head, &h->db[i].y2, &h->db[i].dP, M, nullptr});
+    js.push_back({S.l2, &h->db[i].y1, &h->db[i].dY2, M, nullptr});
+    js.push_back({S.l1, &h->h[L - 1 - i], &h->db[i].dY1, M, nullptr});
+  }
+  for (int i = L - 1; i >= 0; --i) {
+    const StochL& S = h->enc[i];
+    const int rows = i == 0 ? P.Bimg : M;
+    js.push_back({S.head, &h->eb[i].y2, &h->eb[i].dP, rows, nullptr});
+    js.push_back({S.l2, &h->eb[i].y1, &h->eb[i].dY2, rows, nullptr});
+    js.push_back({S.l1, i == 0 ? &h->x_in : &h->h[i - 1], &h->eb[i].dY1, rows, nullptr});
+  }
+  if ((int)js.size() > kDwMaxJobs) return fail(h, IWAE_EINVAL, "weight-gradient pass: too many layers");
+  DwArgs a;
+  std::memset(&a, 0, sizeof(a));
+  // MFMA work of a block per row: its m-tiles x the busiest wave's n-tiles
+  auto block_cost = [](int mt_blk, int nt_blk, int nb) {
+    const int per_wave = nb == 2 ? (nt_blk > 8 ? 2 : 1) : 1;
+    return (double)std::min(mt_blk, kDwMT) * per_wave;
+  };
+  std::vector<double> cost(js.size(), 0.0);
+  double W = 0.0;
+  for (size_t q = 0; q < js.size(); ++q) {
+    const DenseL& d = h->dense[js[q].di];
+    DwJob& J = a.job[q];
+    J.M = d.fin + 1; J.mt = (int)cdiv(J.M, 16); J.nt = (int)cdiv(d.fout, 16);
+    J.nb = J.nt > 8 ? 2 : 1;
+    J.mblocks = (int)cdiv(J.mt, kDwMT); J.nblocks = (int)cdiv(J.nt, 8 * J.nb);
+    for (int mb = 0; mb < J.mblocks; ++mb)
+      for (int nbk = 0; nbk < J.nblocks; ++nbk)
+        cost[q] += block_cost(J.mt - kDwMT * mb, std::min(8 * J.nb, J.nt - 8 * J.nb * nbk), J.nb);
+    W += cost[q] * js[q].rows;
+  }
+  const double target = W / 256.0;                 // per-workgroup work: one round of the chip
+  int tiles = 0;
+  for (size_t q = 0; q < js.size(); ++q) {
+    const WJ& w = js[q];
+    DenseL& d = h->dense[w.di];
+    DwJob& J = a.job[q];
+    J.A = w.A->p; J.lda = w.A->ld; J.B = w.dZ->p; J.ldb = w.dZ->ld; J.ks = w.ks ? w.ks : h->ones;
+    J.rows = w.rows;
+    J.out = h->slabs + d.slab_off; J.ldo = d.ldw; J.slab_stride = d.size();
+    const double per_block = cost[q] / (J.mblocks * J.nblocks);
+    long long S = std::llround(w.rows * per_block / std::max(target, 1.0));
+    S = std::max(1LL, std::min<long long>(S, d.max_splits));
+    const long long chunk = cdiv(cdiv(w.rows, S), 32) * 32;
+    S = cdiv(w.rows, chunk);
+    J.nsplit = (int)S; J.chunk = (int)chunk;
+    d.splits = (int)S;
+    J.tile0 = tiles;
+    tiles += J.mblocks * J.nblocks * J.nsplit;
+  }
+  a.njobs = (int)js.size();
+  a.ntiles = tiles;
+  HIPCHK(launch_dw(h->stream, a));
+  return IWAE_OK;
+}
+
 // ------------------------------------------------ row-chain train engine
 // Train step = first encoder layer (per image, enc0_forward) -> engine forward
 // (jobs E, O) -> bound -> engine backward (jobs O', E') -> first encoder layer
@@ -1640,6 +1712,8 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
   if (h->tc_plans.count(key)) return IWAE_OK;
   const int L = h->L, kS = P.kS;
   auto r32 = [](int x) { return (x + 31) & ~31; };
+  // wide workgroups (32 / 64 sample rows, two-set weight pipeline) for large batches
+  const bool wide = which <= 1 && (long long)P.Bimg * kS >= h->wide_rows;
   std::vector<TcBuild> jobs;
   const bool fold0 = which == 0 && use_fold0(h, P);
   auto ldF = [&](int di) { return h->dense[di].ldF; };
@@ -1705,9 +1779,10 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
       B.need(0, s0.next_k);
       TcOp& a = tc_dense_op(h, B, TC_TANH, h->o1, false, 0, 1, ldF(h->o2));
       if (first) { a.out = h->ob.y1.p; a.ld_out = h->ob.y1.ld; }
-      TcOp& b = tc_dense_op(h, B, TC_TANH, h->o2, false, 1, 2, ldF(h->o3));
+      // (y2 over h1's buffer, dead after o1: the 64-row layout fits the LDS)
+      TcOp& b = tc_dense_op(h, B, TC_TANH, h->o2, false, 1, 0, ldF(h->o3));
       if (first) { b.out = h->ob.y2.p; b.ld_out = h->ob.y2.ld; }
-      TcOp& c = tc_dense_op(h, B, TC_BERN, h->o3, false, 2, -1, 0);
+      TcOp& c = tc_dense_op(h, B, TC_BERN, h->o3, false, 0, -1, 0);
       c.out = h->ob.P.p; c.ld_out = h->ob.P.ld;
       // tiles [t0, t1): t1 caps N (whole tiles), t0 offsets each wave's first tile
       const int t0 = part * (ntile / nsplit), t1 = part + 1 == nsplit ? ntile : (part + 1) * (ntile / nsplit);
@@ -1717,6 +1792,8 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
       if (L == 1 && first) { B.J.logq = h->logq; B.J.logp = h->logp; }
       jobs.push_back(B);
     }
+    // wide launches (large batches): the output job, the longest, dispatched first
+    if (wide && jobs.size() == 2) std::swap(jobs[0], jobs[1]);
   } else if (which == 2) {
     // job I: y1 = tanh(sum of the input Dense's slabs) -> l2 tanh -> head: P0 = (mu | zs)
     TcBuild B;
@@ -1766,9 +1843,10 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
       B.need(0, g.next_k);
       TcOp& a = tc_dense_op(h, B, TC_TGRAD, h->o3, true, 0, 1, ldG(h->o2));
       a.y = h->ob.y2.p; a.ld_y = h->ob.y2.ld; a.out = h->ob.dY2.p; a.ld_out = h->ob.dY2.ld;
-      TcOp& b = tc_dense_op(h, B, TC_TGRAD, h->o2, true, 1, 2, ldG(h->o1));
+      // (dY1 over g's buffer, dead after the output layer's op)
+      TcOp& b = tc_dense_op(h, B, TC_TGRAD, h->o2, true, 1, 0, ldG(h->o1));
       b.y = h->ob.y1.p; b.ld_y = h->ob.y1.ld; b.out = h->ob.dY1.p; b.ld_out = h->ob.dY1.ld;
-      TcOp& c = tc_dense_op(h, B, TC_LIN, h->o1, true, 2, -1, 0);
+      TcOp& c = tc_dense_op(h, B, TC_LIN, h->o1, true, 0, -1, 0);
       c.out = h->dh_out[0].p; c.ld_out = h->dh_out[0].ld;
       jobs.push_back(B);
     }
@@ -1825,7 +1903,9 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
   const long long rows = img ? (long long)P.Bimg : (long long)P.Bimg * kS;
   // image rows: one image per workgroup (latency-bound chains of a few rows), up to 256 workgroups
   const int row_step = img ? (int)std::max<long long>(1, cdiv(P.Bimg, 256)) : 0;
-  const int want = h->tc_rt;            // (2 and 4 row tiles spill registers: knob only)
+  // rows per workgroup: 16 (four-set pipeline) below wide_rows, else the
+  // widest the LDS allows (two-set pipeline)
+  const int want = wide ? 4 : h->tc_rt;
   iwae_handle::TcRec rec;
   for (int rt : {4, 2, 1}) {
     if (rt > want) continue;
@@ -2045,7 +2125,8 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
     if (adam) h->fx_version = h->params_version;
     return IWAE_OK;
   }
-  if (use_update_slabs(h, P)) CHK(run_update(h, P, false, 0, nullptr, 1.f, nullptr, true));
+  if (use_update_slabs(h, P) && h->dw_wide) CHK(run_dw(h, P));
+  else if (use_update_slabs(h, P)) CHK(run_update(h, P, false, 0, nullptr, 1.f, nullptr, true));
   else CHK(weight_grads(h, P, true, true, h->dpx));
   CHK(finish_step(h, P, adam));
   if (adam) {
@@ -2283,6 +2364,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (e == hipSuccess) e = smallm_setup_attributes();
   if (e == hipSuccess) e = tc_setup_attributes();
   if (e == hipSuccess) e = upd_setup_attributes();
+  if (e == hipSuccess) e = dw_setup_attributes();
   if (e != hipSuccess) {
     g_create_error = std::string("hipFuncSetAttribute failed: ") + hipGetErrorString(e);
     iwae_destroy(h);
@@ -2432,6 +2514,8 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
       h->mg_waves = (int)value;
       break;
     case IWAE_KNOB_NLL_ROWS: h->nll_rows = std::max(1LL, value); break;
+    case IWAE_KNOB_WIDE_ROWS: h->wide_rows = std::max(0LL, value); break;
+    case IWAE_KNOB_DW_WIDE: h->dw_wide = on; break;
     default: return fail(h, IWAE_EINVAL, "unknown tuning knob " + std::to_string(knob));
   }
   // captured steps and engine plans were built for the previous setting

@@ -159,24 +159,28 @@ __device__ __forceinline__ void tc_fetch_step(__amdgpu_buffer_rsrc_t rh, __amdgp
 #endif
 }
 
-// acc[rt] += W-tile . IN[rows of rt][k0 .. k0 + 32 ns) (bf16x3)
+// acc[rt] += W-tile . IN[rows of rt][k0 .. k0 + 32 ns) (bf16x3).  RT = 1: two
+// accumulator chains (the hi x hi products; the two cross terms), so a unit's
+// dependent MFMA chain is half as long; wider tiles have RT independent
+// chains already (and the registers are needed elsewhere): one chain each.
 template <int RT>
 __device__ __forceinline__ void tc_mma(const TcBuf& IN, int k0, int ns, const TcFrag& f, tc_f32x4 (&acc)[RT]) {
 #ifdef IWAE_TC_NOMMA       // timing experiment only
   acc[0][0] += (float)f.h[0][0] + (float)f.l[TC_KS - 1][7];
   return;
 #endif
+  constexpr bool TWO = RT == 1;
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
   constexpr int RH = RT < 2 ? RT : 2;
   constexpr int NP = RT / RH;
   constexpr int NC = TC_KS * NP;
   tc_bf16x8 ah[2][RH], al[2][RH];
-  // two accumulator chains (the hi x hi products; the two cross terms): the
-  // dependent MFMA chain of a unit is half as long
-  tc_f32x4 lo[RT];
+  tc_f32x4 lo[TWO ? RT : 1];
+  if constexpr (TWO) {
 #pragma unroll
-  for (int i = 0; i < RT; ++i) lo[i] = (tc_f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < RT; ++i) lo[i] = (tc_f32x4){0.f, 0.f, 0.f, 0.f};
+  }
   auto rd = [&](int c, int b) {
     const int u = c / NP, p = c % NP;
 #pragma unroll
@@ -192,18 +196,35 @@ __device__ __forceinline__ void tc_mma(const TcBuf& IN, int k0, int ns, const Tc
     const int u = c / NP, p = c % NP, b = c & 1;
     if (u >= ns) break;
     if (c + 1 < NC && (c + 1) / NP < ns) rd(c + 1, b ^ 1);
+    if constexpr (TWO) {
 #pragma unroll
-    for (int i = 0; i < RH; ++i)
-      lo[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.l[u], ah[b][i], lo[p * RH + i], 0, 0, 0);
+      for (int i = 0; i < RH; ++i)
+        lo[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.l[u], ah[b][i], lo[p * RH + i], 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < RH; ++i)
-      acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], ah[b][i], acc[p * RH + i], 0, 0, 0);
+      for (int i = 0; i < RH; ++i)
+        acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], ah[b][i], acc[p * RH + i], 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < RH; ++i)
-      lo[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], al[b][i], lo[p * RH + i], 0, 0, 0);
+      for (int i = 0; i < RH; ++i)
+        lo[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], al[b][i], lo[p * RH + i], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < RH; ++i)
+        acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.l[u], ah[b][i], acc[p * RH + i], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < RH; ++i)
+        acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], al[b][i], acc[p * RH + i], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < RH; ++i)
+        acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], ah[b][i], acc[p * RH + i], 0, 0, 0);
+      // one chunk's fragment reads in flight at a time (hoisting them all
+      // would need the registers the wide tiles do not have)
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
+  if constexpr (TWO) {
 #pragma unroll
-  for (int i = 0; i < RT; ++i) acc[i] += lo[i];
+    for (int i = 0; i < RT; ++i) acc[i] += lo[i];
+  }
 }
 
 // per-lane row state: log q / log p partial sums (natural log), the Bernoulli
@@ -623,6 +644,58 @@ __device__ __forceinline__ int tc_dense(const TcArgs& A, CJob& J, COp& S, const 
   return Un;
 }
 
+// One Dense op of a wide workgroup (RT >= 2 row tiles: 32 or 64 rows, the
+// large-batch launches).  Each fetch unit feeds RT times the MFMAs of the
+// 16-row engine, so one unit of look-ahead covers the L2 round trip: two
+// register sets P / Q alternate by unit parity (the loop is unrolled by two,
+// so both stay statically named), unit u + 1 is requested before unit u is
+// multiplied.  No cross-op prefetch (the four-set pipeline of tc_dense spills
+// at these tile counts); an op's first unit waits one round trip.
+template <int RT>
+__device__ __forceinline__ void tc_dense2(const TcArgs& A, CJob& J, COp& S, const int kind, uint64_t base,
+                                         TcRows<RT>& R, int row0, int nrows) {
+  const TcStream q = tc_stream(S);
+  const int U = q.U;
+  const TcBuf IN = tc_buf<RT>(J, S.in_buf);
+  const TcBuf OUT = tc_buf<RT>(J, S.out_buf >= 0 ? S.out_buf : S.in_buf);
+  float4 ov[RT];
+  float2 tv[RT];
+  tc_f32x4 acc[RT];
+  TcFrag fP, fQ;
+  if (U > 0) tc_issue_u(S, q, 0, fP);
+  auto step = [&](int u, TcFrag& cur, TcFrag& nxt) {
+    const TcUnit x = tc_unit(S, u, q.nch);
+    if (x.first) {
+      switch (kind) {
+        case TC_BERN: tc_epi_loads<RT, TC_BERN>(A, S, x.t, R, row0, nrows, ov, tv); break;
+        case TC_TGRAD: tc_epi_loads<RT, TC_TGRAD>(A, S, x.t, R, row0, nrows, ov, tv); break;
+        case TC_PRIOR: tc_epi_loads<RT, TC_PRIOR>(A, S, x.t, R, row0, nrows, ov, tv); break;
+        default: break;
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt] = (tc_f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    if (u + 1 < U) tc_issue_u(S, q, u + 1, nxt);
+    tc_mma<RT>(IN, x.k0, x.ns, cur, acc);
+    if (x.last) {
+      switch (kind) {
+        case TC_TANH: tc_epilogue<RT, TC_TANH>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_TGRAD: tc_epilogue<RT, TC_TGRAD>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_LIN: tc_epilogue<RT, TC_LIN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_BERN: tc_epilogue<RT, TC_BERN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_SAMPLE: tc_epilogue<RT, TC_SAMPLE>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_HEADP: tc_epilogue<RT, TC_HEADP>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        default: tc_epilogue<RT, TC_PRIOR>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+      }
+    }
+  };
+  for (int u = 0; u < U; u += 2) {
+    step(u, fP, fQ);
+    if (u + 1 >= U) break;
+    step(u + 1, fQ, fP);
+  }
+}
+
 // Barrier between ops.  LDS only: global stores (activations for the weight
 // gradients, read by later launches) and the next op's prefetched weights stay
 // in flight.  Ops that read global data written earlier in this launch by this
@@ -1017,7 +1090,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
         !J.op[s + 1].gsync)
       Sn = &J.op[s + 1];
     int nx = 0;             // elementwise op: requests the next op's first units
-    if (kind > TC_LAST_DENSE && Sn) nx = tc_prefetch(*Sn, F);
+    if (RT == 1 && kind > TC_LAST_DENSE && Sn) nx = tc_prefetch(*Sn, F);
 
     if (kind <= TC_LAST_DENSE && S.out_buf >= 0) {
       const int width = kind == TC_SAMPLE ? S.d : S.N;
@@ -1033,7 +1106,10 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
       case TC_BERN:
       case TC_TGRAD:
       case TC_LIN:
-      case TC_HEADP: nx = tc_dense<RT>(A, J, S, kind, base, Rw, r0, nr, F, npre, Sn, UTR); break;
+      case TC_HEADP:
+        if constexpr (RT == 1) nx = tc_dense<RT>(A, J, S, kind, base, Rw, r0, nr, F, npre, Sn, UTR);
+        else tc_dense2<RT>(A, J, S, kind, base, Rw, r0, nr);
+        break;
 #ifdef IWAE_TC_SKIPELEM    // timing experiment only
       default: break;
 #else
