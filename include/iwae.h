@@ -128,7 +128,8 @@ enum iwae_knob {
   IWAE_KNOB_MG_WAVES = 16,     /* NLL kernel workgroup: 8 waves / 64 rows or 4 waves / 32 rows (8) */
   IWAE_KNOB_NLL_ROWS = 17,     /* sample rows per NLL chunk (2^20) */
   IWAE_KNOB_WIDE_ROWS = 18,    /* engine: 32 / 64-row workgroups from this many sample rows (4097) */
-  IWAE_KNOB_DW_WIDE = 19       /* beyond UPD_ROWS: weight gradients on the 112 x 256-block kernel (1) */
+  IWAE_KNOB_DW_WIDE = 19,      /* beyond UPD_ROWS: weight gradients on the 112 x 256-block kernel (1) */
+  IWAE_KNOB_LD_ALIGN = 20      /* workspace row strides: multiples of 4, 8, 16 or 32 floats (4) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --
@@ -263,7 +264,9 @@ int iwae_debug_gemm(iwae_handle* h, const float* A, int lda, const float* B, int
 /* Bytes of device workspace currently allocated by the handle. */
 double iwae_workspace_bytes(const iwae_handle* h);
 /* Launch counters (tests): what = 0 fused k-sample NLL kernel (mega_fwd_kernel)
- * launches, 1 those of them fed injected noise; -1 for an unknown id. */
+ * launches, 1 those of them fed injected noise, 2 train-engine (tc_kernel)
+ * launches issued (a captured step counts once, at capture); -1 for an
+ * unknown id. */
 long long iwae_debug_count(const iwae_handle* h, int what);
 /* Live kernel timing: bracket every launch of one kernel class with HIP events
  * on the handle's stream -- a GEMM class (kind: 0 forward, 1 backward-data,

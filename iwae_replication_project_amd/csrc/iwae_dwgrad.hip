@@ -42,6 +42,7 @@ constexpr int DW_PX = DW_XR * DW_S;           // dwords per X plane
 constexpr int DW_PZ = DW_ZR * DW_S;           // dwords per dZ plane
 constexpr int DW_BUF = 2 * DW_PX + 2 * DW_PZ; // X hi, X lo, dZ hi, dZ lo
 constexpr int DW_XCQ = DW_XR / 4;             // X column quads per staged row (28)
+constexpr int DW_G = 8;                       // iterations per unrolled group
 
 extern __shared__ __attribute__((aligned(16))) float dws[];
 
@@ -58,30 +59,33 @@ struct DwRegs {
   dw_f32x4 k0, k1;
 };
 
-// the thread's staging role for this job: 0 none, 1 X block, 2 dZ block, 3 none
-// (a lane of an X wave past the 112 columns)
+// The thread's staging block.  Roles are per wave (every buffer resource and
+// branch is wave-uniform): waves 0-1 stage X (lanes 112-127 repeat lanes
+// 96-111), waves 2-7 dZ (waves past its 128 / 256 columns repeat the first
+// ones).  A repeated block writes the same values to the same LDS words: no
+// lane ever skips the staging (an exec-masked staging branch made the
+// compiler drain every load in flight at its join).
 struct DwRole {
-  int kind, rg, cq;
+  int zw;                     // wave-uniform: 1 = this wave stages dZ
+  int rg, cq;
   unsigned off;               // byte offset of its first element within an iteration's rows
 };
 
-// (roles are per wave, so every buffer resource is wave-uniform: waves 0-1 the
-// X blocks, waves 2-5 the dZ blocks, waves 6-7 only multiply)
 __device__ __forceinline__ DwRole dw_role(const DwJob& J, int i0, int j0) {
   const int t = threadIdx.x;
   DwRole R;
-  const int nzq = 32 * J.nb;                  // dZ column quads staged (128 or 256 columns)
-  if (t < 128) {
-    R.kind = t < 4 * DW_XCQ ? 1 : 3; R.rg = t / DW_XCQ; R.cq = t % DW_XCQ;
+  R.zw = __builtin_amdgcn_readfirstlane(t >> 6) >= 2 ? 1 : 0;
+  if (!R.zw) {
+    const int u = t < 4 * DW_XCQ ? t : t - 16;
+    R.rg = u / DW_XCQ; R.cq = u % DW_XCQ;
     const int c = i0 + 4 * R.cq;
-    R.off = (R.kind == 1 && c < J.lda) ? (unsigned)(8 * R.rg * J.lda + c) * 4u : kOOB;
-  } else if (t < 128 + 4 * nzq) {
-    const int u = t - 128;
-    R.kind = 2; R.rg = u / nzq; R.cq = u % nzq;
+    R.off = c < J.lda ? (unsigned)(8 * R.rg * J.lda + c) * 4u : kOOB;
+  } else {
+    const int nzq = 32 * J.nb;                // dZ column quads staged (128 or 256 columns)
+    const int u = (t - 128) % (4 * nzq);
+    R.rg = u / nzq; R.cq = u % nzq;
     const int c = j0 + 4 * R.cq;
     R.off = c < J.ldb ? (unsigned)(8 * R.rg * J.ldb + c) * 4u : kOOB;
-  } else {
-    R.kind = 0; R.rg = 0; R.cq = 0; R.off = kOOB;
   }
   return R;
 }
@@ -90,7 +94,7 @@ __device__ __forceinline__ DwRole dw_role(const DwJob& J, int i0, int j0) {
 __device__ __forceinline__ void dw_load(const DwJob& J, const DwRole& R, int rbase, int rend, int it, DwRegs& G) {
   const int r0 = rbase + it * DW_KR;
   const unsigned left = rend > r0 ? (unsigned)(rend - r0) : 0u;
-  const bool isx = (threadIdx.x >> 6) < 2;     // wave-uniform (dw_role)
+  const bool isx = !R.zw;
   const float* base = isx ? J.A + (size_t)r0 * J.lda : J.B + (size_t)r0 * J.ldb;
   const int ld = isx ? J.lda : J.ldb;
   const __amdgpu_buffer_rsrc_t rs = buf_rsrc(base, left * (unsigned)ld * 4u);
@@ -98,7 +102,7 @@ __device__ __forceinline__ void dw_load(const DwJob& J, const DwRole& R, int rba
 #pragma unroll
   for (int q = 0; q < 8; ++q) G.v[q] = dw_ld4(rs, off + (unsigned)(q * ld) * 4u);
   const __amdgpu_buffer_rsrc_t rk = buf_rsrc(J.ks + r0, left * 4u);
-  const unsigned ko = R.kind == 2 ? (unsigned)(8 * R.rg) * 4u : kOOB;
+  const unsigned ko = R.zw ? (unsigned)(8 * R.rg) * 4u : kOOB;
   G.k0 = dw_ld4(rk, ko);
   G.k1 = dw_ld4(rk, ko + 16u);
 }
@@ -106,15 +110,13 @@ __device__ __forceinline__ void dw_load(const DwJob& J, const DwRole& R, int rba
 // column C of the block -> k-contiguous hi / lo rows of the image in `buf`
 template <int C>
 __device__ __forceinline__ void dw_stage_col(const DwRole& R, const DwRegs& G, float* buf) {
-  if (R.kind == 0 || R.kind == 3) return;
   dw_u32x4 h, l;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     dw_f32x2 x = {G.v[2 * p][C], G.v[2 * p + 1][C]};
-    if (R.kind == 2) {
-      const dw_f32x4& k = p < 2 ? G.k0 : G.k1;
-      x *= dw_f32x2{k[(2 * p) & 3], k[(2 * p + 1) & 3]};
-    }
+    const dw_f32x4& k = p < 2 ? G.k0 : G.k1;
+    const dw_f32x2 sc = {k[(2 * p) & 3], k[(2 * p + 1) & 3]};
+    if (R.zw) x *= sc;                         // (wave-uniform)
     const unsigned hb = __builtin_bit_cast(unsigned, __builtin_convertvector(x, dw_bf16x2));
     const dw_f32x2 hf = {__uint_as_float(hb << 16), __uint_as_float(hb & 0xFFFF0000u)};
     const dw_f32x2 rr = x - hf;
@@ -122,8 +124,8 @@ __device__ __forceinline__ void dw_stage_col(const DwRole& R, const DwRegs& G, f
     l[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(rr, dw_bf16x2));
   }
   const int c = 4 * R.cq + C;
-  float* hp = R.kind == 1 ? buf : buf + 2 * DW_PX;
-  const int plane = R.kind == 1 ? DW_PX : DW_PZ;
+  float* hp = R.zw ? buf + 2 * DW_PX : buf;
+  const int plane = R.zw ? DW_PZ : DW_PX;
   const int o = dw_off(c, R.rg);
   *reinterpret_cast<dw_u32x4*>(hp + o) = h;
   *reinterpret_cast<dw_u32x4*>(hp + plane + o) = l;
@@ -200,7 +202,10 @@ __global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
   float* buf1 = dws + DW_BUF;
   // iteration it multiplies image it & 1, stages iteration it + 1 from set
   // (it + 1) & 1 into the other image and then refills that set with
-  // iteration it + 3 (iteration it + 2 is in flight in the other set)
+  // iteration it + 3 (iteration it + 2 is in flight in the other set).
+  // Groups of DW_G iterations are unrolled straight-line, so the compiler's
+  // wait counts see every load in flight (a set carried around a loop back
+  // edge makes it wait for all of them); the loop runs over groups.
   DwRegs G0, G1;
   if (nit > 0) {
     dw_load(J, R, rbase, rend, 0, G0);
@@ -210,18 +215,24 @@ __global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
     dw_load(J, R, rbase, rend, 2, G0);
     __syncthreads();
   }
-  for (int it = 0; it < nit; it += 2) {
-    dw_iter(buf0, buf1, R, G1, it + 1 < nit, mt, nbw, acc);
+  auto step = [&](int it, const float* rb, float* wb, DwRegs& Gs) __attribute__((always_inline)) {
+    dw_iter(rb, wb, R, Gs, it + 1 < nit, mt, nbw, acc);
     __builtin_amdgcn_sched_barrier(0);
-    if (it + 3 < nit) dw_load(J, R, rbase, rend, it + 3, G1);
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
-    if (it + 1 >= nit) break;
-    dw_iter(buf1, buf0, R, G0, it + 2 < nit, mt, nbw, acc);
-    __builtin_amdgcn_sched_barrier(0);
-    if (it + 4 < nit) dw_load(J, R, rbase, rend, it + 4, G0);
+    // unconditional (past the chunk the range is empty: the loads return 0
+    // without touching memory): a conditional load would make the compiler
+    // assume it may be missing and wait for the older set's loads in full
+    dw_load(J, R, rbase, rend, it + 3, Gs);
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
+  };
+  for (int g0 = 0; g0 < nit; g0 += DW_G) {
+#pragma unroll
+    for (int u = 0; u < DW_G; u += 2) {
+      if (g0 + u >= nit) break;
+      step(g0 + u, buf0, buf1, G1);
+      if (g0 + u + 1 >= nit) break;
+      step(g0 + u + 1, buf1, buf0, G0);
+    }
   }
 
   // slab s: rows i < M (the layer's inputs + bias row), columns j < ldo

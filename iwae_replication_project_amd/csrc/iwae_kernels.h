@@ -543,6 +543,7 @@ struct TcJob {
   TcOp op[kTcMaxOps]; int nop;
   int buf_off[kTcMaxBufs], buf_ld[kTcMaxBufs];   // bf16 offset of the hi plane / row stride
   float* logq; float* logp; float* bern; int ld_bern, bern_col;   // per-row sums this job writes (null: none)
+  float* bce;                 // L_alpha: per-row Keras-BCE sums (same layout as bern)
 };
 struct TcPlan {              // device resident (built once per shape)
   TcJob job[kTcMaxJobs]; int njobs;
@@ -561,6 +562,7 @@ struct TcArgs {
   uint64_t seed; const uint64_t* rng_base;
   const float* eps_a[8]; const float* eps_b[8]; int Bsplit, Bimg;   // injected noise ([k][B][d]) or null
   const float* dlw; const float* dpx; float wa;
+  float wb; int need_bce;                   // L_alpha: Keras-BCE term of the output epilogue (weight wb)
   // the bound inside the backward launch (bnd_rows): every workgroup computes
   // its rows' dL/dlw and dpx into LDS at float offset bnd_lds (dpx at + 16 RT)
   // from its images' log weights, staging an image per wave at wave * bnd_ld;

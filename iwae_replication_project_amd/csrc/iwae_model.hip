@@ -143,6 +143,7 @@ struct iwae_handle {
   float *dlw2 = nullptr, *dpx2 = nullptr, *contrib = nullptr, *part = nullptr, *part2 = nullptr;
   float *run_m = nullptr, *run_s = nullptr;
   float* ebern = nullptr;            // engine: per-row Bernoulli log-likelihood, [rows][4] (cols 1-3 zero)
+  float* ebce = nullptr;             // engine: per-row Keras-BCE log-likelihood (L_alpha), same layout
   float* ones = nullptr;             // [rows] of 1.0 (the fused update's row scale of unscaled dZ)
   int ldpart = 0, npart = 0;
   float* slabs = nullptr;
@@ -156,6 +157,7 @@ struct iwae_handle {
   int mg_waves = 8;                  // mega_fwd_kernel workgroup: 8 waves (64 rows) or 4 (32 rows, 2 per CU)
   bool masked = false;               // active-unit masks in force (iwae_nll_masked only)
   long long n_mega = 0, n_mega_eps = 0;  // mega_fwd_kernel launches (all / injected noise), iwae_debug_count
+  long long n_tc = 0;                    // train-engine launches (tc_kernel), iwae_debug_count(h, 2)
   const float* mask[IWAE_MAX_LAYERS] = {};
   // row-chain train engine plans (device resident, per shape; iwae_train.hip)
   struct TcRec {
@@ -184,6 +186,7 @@ struct iwae_handle {
   int smallm_rows = 32;              // first encoder layer on the few-row launches up to this many images (0: never)
   long long nll_rows = 1LL << 20;    // sample rows per NLL chunk (measured fastest: 2^17-2^20 within 10 %)
   int tc_rt = 1;                     // row tiles of 16 per engine workgroup below wide_rows
+  int ld_align = 4;                  // workspace row strides: multiples of this many floats (4 or 32)
   long long wide_rows = 4097;        // sample rows from which the engine runs 32 / 64-row workgroups
   // graphs
   bool use_graphs = false;
@@ -310,8 +313,9 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
   struct Pending { Mat* m; size_t o; };
   std::vector<std::pair<float**, size_t>> vecs;
   std::vector<Pending> mats;
+  const int la = h->ld_align;
   auto mat = [&](Mat& m, int nrows, int width) {
-    m.ld = r4(width);
+    m.ld = (width + la - 1) / la * la;
     mats.push_back({&m, take((size_t)nrows * m.ld)});
   };
   auto vec = [&](float*& p, size_t n) { vecs.push_back({&p, take(n)}); };
@@ -373,6 +377,7 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
   vec(h->dlw, rows); vec(h->dpx, rows); vec(h->dlw2, rows); vec(h->dpx2, rows);
   vec(h->contrib, Bimg); vec(h->run_m, Bimg); vec(h->run_s, Bimg);
   vec(h->ebern, (size_t)rows * 4);
+  vec(h->ebce, (size_t)rows * 4);
   vec(h->ones, rows);
   h->fslab_S = (int)std::min<long long>(16, cdiv(h->xdim + 1, 64));
   vec(h->fslab, (size_t)h->fslab_S * Bimg * r4(h->enc[0].H + 1));
@@ -693,7 +698,10 @@ static BoundArgs make_bound_args(iwae_handle* h, const Plan& P, bool train, floa
   BoundArgs b{};
   b.part = h->part; b.part2 = P.need_bce ? h->part2 : nullptr; b.ldpart = h->ldpart; b.npart = h->npart;
   b.logp = h->logp; b.logq = h->logq;
-  if (engine) { b.part = h->ebern; b.ldpart = 4; b.npart = 1; b.part2 = nullptr; }   // row totals (cols 0-1 summed)
+  if (engine) {                     // row totals (cols 0-1 summed)
+    b.part = h->ebern; b.ldpart = 4; b.npart = 1;
+    b.part2 = P.need_bce ? h->ebce : nullptr;
+  }
   b.lw = h->lw; b.contrib = h->contrib;
   b.dlw = train ? h->dlw : nullptr; b.dpx = train ? h->dpx : nullptr;
   b.dlw2 = (train && P.piwae) ? h->dlw2 : nullptr; b.dpx2 = (train && P.piwae) ? h->dpx2 : nullptr;
@@ -1609,7 +1617,7 @@ constexpr int kTcMaxLayers = 3;      // op-table capacity: 4 ops per stochastic 
 
 static bool use_engine(const iwae_handle* h, const Plan& P) {
   if (!h->engine || !h->x3 || h->path == 1 || h->path == 2 || h->masked) return false;
-  if (P.need_bce || P.kl || P.piwae) return false;       // BCE / KL / two-weighting losses: fused row-block path
+  if (P.kl) return false;       // VAE_V1's analytic KL: fused row-block path
   if (h->L > kTcMaxLayers || h->enc[0].d > 2048) return false;   // (image-row backward: d / 4 column quads)
   return (long long)P.Bimg * P.kS <= (1LL << 18);
 }
@@ -1713,7 +1721,7 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
   const int L = h->L, kS = P.kS;
   auto r32 = [](int x) { return (x + 31) & ~31; };
   // wide workgroups (32 / 64 sample rows, two-set weight pipeline) for large batches
-  const bool wide = which <= 1 && (long long)P.Bimg * kS >= h->wide_rows;
+  const bool wide = (which <= 1 || which == 4) && (long long)P.Bimg * kS >= h->wide_rows;
   std::vector<TcBuild> jobs;
   const bool fold0 = which == 0 && use_fold0(h, P);
   auto ldF = [&](int di) { return h->dense[di].ldF; };
@@ -1789,6 +1797,7 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
       c.t0 = t0;
       if (t1 < ntile) c.N = 16 * t1;
       B.J.bern = h->ebern; B.J.ld_bern = 4; B.J.bern_col = part;
+      B.J.bce = P.need_bce ? h->ebce : nullptr;
       if (L == 1 && first) { B.J.logq = h->logq; B.J.logp = h->logp; }
       jobs.push_back(B);
     }
@@ -1834,6 +1843,11 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
     b.y = h->eb[0].y1.p; b.ld_y = h->eb[0].y1.ld; b.out = h->eb[0].dY1.p; b.ld_out = h->eb[0].dY1.ld;
     jobs.push_back(B);
   } else {
+    // which 1: the backward launch.  which 4 (PIWAE's encoder pass): the same
+    // chain run on the MIWAE weighting, storing only what the encoder's
+    // backward reads (dL/dh, the encoder layers' dZ): the decoder layers' dZ
+    // of the IWAE pass stay for their weight gradients
+    const bool dec_out = which == 1;
     // job O': (dpx g) W3^T (1 - y2^2) -> W2^T (1 - y1^2) -> W1^T = dL/dh1 (output MLP part)
     {
       TcBuild B;
@@ -1842,10 +1856,10 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
       g.y = h->ob.P.p; g.ld_y = h->ob.P.ld;
       B.need(0, g.next_k);
       TcOp& a = tc_dense_op(h, B, TC_TGRAD, h->o3, true, 0, 1, ldG(h->o2));
-      a.y = h->ob.y2.p; a.ld_y = h->ob.y2.ld; a.out = h->ob.dY2.p; a.ld_out = h->ob.dY2.ld;
+      a.y = h->ob.y2.p; a.ld_y = h->ob.y2.ld; a.out = dec_out ? h->ob.dY2.p : nullptr; a.ld_out = h->ob.dY2.ld;
       // (dY1 over g's buffer, dead after the output layer's op)
       TcOp& b = tc_dense_op(h, B, TC_TGRAD, h->o2, true, 1, 0, ldG(h->o1));
-      b.y = h->ob.y1.p; b.ld_y = h->ob.y1.ld; b.out = h->ob.dY1.p; b.ld_out = h->ob.dY1.ld;
+      b.y = h->ob.y1.p; b.ld_y = h->ob.y1.ld; b.out = dec_out ? h->ob.dY1.p : nullptr; b.ld_out = h->ob.dY1.ld;
       TcOp& c = tc_dense_op(h, B, TC_LIN, h->o1, true, 0, -1, 0);
       c.out = h->dh_out[0].p; c.ld_out = h->dh_out[0].ld;
       jobs.push_back(B);
@@ -1860,13 +1874,15 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
         g.d = D.d; g.out_buf = 0; g.next_k = ldG(D.head);
         g.P = h->db[j].P.p; g.ld_P = h->db[j].P.ld;
         g.h = h->h[t].p; g.ld_h = h->h[t].ld;
-        g.out = h->db[j].dP.p; g.ld_out = h->db[j].dP.ld;
+        g.out = dec_out ? h->db[j].dP.p : nullptr; g.ld_out = h->db[j].dP.ld;
         g.dh = h->dh_prior[t].p; g.ld_dh = h->dh_prior[t].ld;
         B.need(0, std::max(g.next_k, 2 * D.d));
         TcOp& a = tc_dense_op(h, B, TC_TGRAD, D.head, true, 0, 1, ldG(D.l2));
-        a.y = h->db[j].y2.p; a.ld_y = h->db[j].y2.ld; a.out = h->db[j].dY2.p; a.ld_out = h->db[j].dY2.ld;
+        a.y = h->db[j].y2.p; a.ld_y = h->db[j].y2.ld; a.out = dec_out ? h->db[j].dY2.p : nullptr;
+        a.ld_out = h->db[j].dY2.ld;
         TcOp& b = tc_dense_op(h, B, TC_TGRAD, D.l2, true, 1, 0, ldG(D.l1));
-        b.y = h->db[j].y1.p; b.ld_y = h->db[j].y1.ld; b.out = h->db[j].dY1.p; b.ld_out = h->db[j].dY1.ld;
+        b.y = h->db[j].y1.p; b.ld_y = h->db[j].y1.ld; b.out = dec_out ? h->db[j].dY1.p : nullptr;
+        b.ld_out = h->db[j].dY1.ld;
         TcOp& c = tc_dense_op(h, B, TC_LIN, D.l1, true, 0, -1, 0);
         c.out = h->dh_dec[src].p; c.ld_out = h->dh_dec[src].ld;
       }
@@ -1899,7 +1915,7 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
   (void)r32;
   if ((int)jobs.size() > kTcMaxJobs) return fail(h, IWAE_EINVAL, "engine: too many jobs");
   // rows per workgroup: the largest tile count the LDS allows, fewer for small batches
-  const bool img = which >= 2;
+  const bool img = which == 2 || which == 3;
   const long long rows = img ? (long long)P.Bimg : (long long)P.Bimg * kS;
   // image rows: one image per workgroup (latency-bound chains of a few rows), up to 256 workgroups
   const int row_step = img ? (int)std::max<long long>(1, cdiv(P.Bimg, 256)) : 0;
@@ -1916,9 +1932,9 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
       mx = std::max(mx, b);
     }
     acc_off = (int)((mx + 15) / 16 * 4);            // floats, 16-byte aligned
-    // per-row accumulators: log q, log p, [3][8 waves] partials, the in-launch
+    // per-row accumulators: log q, log p, [4][8 waves] partials, the in-launch
     // bound's dL/dlw and dpx
-    const size_t lds = (size_t)acc_off * sizeof(float) + (size_t)(4 + 3 * 8) * 16 * rt * sizeof(float);
+    const size_t lds = (size_t)acc_off * sizeof(float) + (size_t)(4 + 4 * 8) * 16 * rt * sizeof(float);
     if (lds <= 160 * 1024) {
       rec.rt = rt;
       rec.lds = lds;
@@ -1955,10 +1971,14 @@ static int tc_prepare(iwae_handle* h, const Plan& P) {
   CHK(tc_prepare_one(h, P, 2));
   CHK(tc_prepare_one(h, P, 3));
   CHK(tc_prepare_one(h, P, 0));
+  if (P.piwae) CHK(tc_prepare_one(h, P, 4));
   return tc_prepare_one(h, P, 1);
 }
 
-static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which, const BoundArgs* bnd = nullptr) {
+// dlw / dpx: the bound's weighting the launch reads (default: the bound's
+// first one; PIWAE's encoder pass: the MIWAE one, dlw2 / dpx2)
+static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which, const BoundArgs* bnd = nullptr,
+                  const float* dlw = nullptr, const float* dpx = nullptr) {
   auto it = h->tc_plans.find(tc_key(P, which));
   if (it == h->tc_plans.end()) return fail(h, IWAE_EINVAL, "engine plan missing");
   const iwae_handle::TcRec& rec = it->second;
@@ -1971,7 +1991,7 @@ static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which, con
     tot += rec.nb[j];
   }
   a.block_start[kTcMaxJobs] = tot;
-  a.rows = which >= 2 ? P.Bimg : P.Bimg * P.kS; a.kS = P.kS;
+  a.rows = (which == 2 || which == 3) ? P.Bimg : P.Bimg * P.kS; a.kS = P.kS;
   a.row_step = rec.row_step;
   // XCD-aware placement: the XCDs split over the jobs in proportion to their
   // workgroups, so each XCD's L2 fetches one job's weight copies (a launch that
@@ -1999,7 +2019,8 @@ static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which, con
   a.seed = h->seed; a.rng_base = &h->ds->rng[0];
   for (int i = 0; i < h->L && i < 8; ++i) { a.eps_a[i] = E.a[i]; a.eps_b[i] = E.b[i]; }
   a.Bsplit = P.Bsplit; a.Bimg = P.Bimg;
-  a.dlw = h->dlw; a.dpx = h->dpx; a.wa = P.wa;
+  a.dlw = dlw ? dlw : h->dlw; a.dpx = dpx ? dpx : h->dpx; a.wa = P.wa;
+  a.wb = P.wb; a.need_bce = P.need_bce;
   a.bnd_block = -1;
   if (bnd) {
     // the bound in this (backward) launch: its rows' dL/dlw per workgroup, the
@@ -2009,10 +2030,11 @@ static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which, con
     a.bnd_rows = 1;
     a.bnd_block = h->tc_xcd && a.xcd_slots > 0 ? 8 * a.xcd_slots : tot;
     a.bnd_ld = r4(P.kS);
-    a.bnd_lds = rec.acc_off + (2 + 3 * 8) * 16 * rec.rt;
+    a.bnd_lds = rec.acc_off + (2 + 4 * 8) * 16 * rec.rt;
     a.rng_base = nullptr;
   }
-  const bool prof = h->prof_kind == 10 + which;
+  const bool prof = which <= 1 && h->prof_kind == 10 + which;
+  h->n_tc++;
   if (prof) {
     if (h->prof_used + 2 > h->prof_ev.size()) {
       for (int i = 0; i < 256; ++i) {
@@ -2097,13 +2119,18 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
     CHK(run_bound(h, P, true, -1.f, train_loss_ptr(h), adam, true));
     CHK(tc_run(h, P, E, 1));
   }
+  // PIWAE (PDF p7): the decoder's weight gradients come from IWAE_{k1 k2} (the
+  // pass above stored their dZ), the encoder's from MIWAE(k1, k2): the
+  // backward chain again on dlw2 / dpx2, storing only the encoder path
+  const float* enc_dlw = P.piwae ? h->dlw2 : nullptr;
+  if (P.piwae) CHK(tc_run(h, P, E, 4, nullptr, h->dlw2, h->dpx2));
   // (a second stream for the first encoder layer's backward beside the other
   // weight gradients measured slower inside the captured graph: sequential).
   // Its image-row job also at small batches (B = 20: step 128.1 -> 126.4 us
   // against the row-block Gaussian backward + two few-row launches)
   const bool img_bwd = img || h->engine_img_bwd;
-  if (img_bwd) CHK(tc_run(h, P, E, 3));
-  else if (!img_bwd) CHK(fused_encoder_bwd(h, P, h->dlw, 0));
+  if (img_bwd) CHK(tc_run(h, P, E, 3, nullptr, enc_dlw));
+  else CHK(fused_encoder_bwd(h, P, P.piwae ? h->dlw2 : h->dlw, 0));
   if (use_update(h, P) && h->dp_weighted) {
     // data parallel: the fused gradient pass (B_local * g, B_local in the
     // tail), the all-reduce, then Adam and the fragment-major copies
@@ -2516,6 +2543,12 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_NLL_ROWS: h->nll_rows = std::max(1LL, value); break;
     case IWAE_KNOB_WIDE_ROWS: h->wide_rows = std::max(0LL, value); break;
     case IWAE_KNOB_DW_WIDE: h->dw_wide = on; break;
+    case IWAE_KNOB_LD_ALIGN:
+      if (value != 4 && value != 8 && value != 16 && value != 32)
+        return fail(h, IWAE_EINVAL, "LD_ALIGN must be 4, 8, 16 or 32");
+      h->ld_align = (int)value;
+      free_workspace(h);
+      break;
     default: return fail(h, IWAE_EINVAL, "unknown tuning knob " + std::to_string(knob));
   }
   // captured steps and engine plans were built for the previous setting
@@ -3114,6 +3147,7 @@ long long iwae_debug_count(const iwae_handle* h, int what) {
   switch (what) {
     case 0: return h->n_mega;
     case 1: return h->n_mega_eps;
+    case 2: return h->n_tc;
     default: return -1;
   }
 }

@@ -40,6 +40,9 @@ typedef __bf16 tc_bf16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned tc_u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int TC_NW = 8;      // waves per workgroup
+#ifndef IWAE_TC_UNCOND
+#define IWAE_TC_UNCOND 0
+#endif
 constexpr int TC_KS = 4;      // k steps of 32 per weight fetch unit (128 k)
 constexpr float kBernOff0T = 9.1327896e-7f;   // 1 - 0.999999f - 1e-7f (F:126 constants in f32)
 
@@ -110,6 +113,27 @@ __device__ __forceinline__ void tc_put1(const TcBuf& B, int o, float v) {
   const __bf16 h = (__bf16)v;
   B.hi[o] = h;
   B.lo[o] = (__bf16)(v - (float)h);
+}
+
+// Global stores of the activations the later launches read.  Wide
+// workgroups (RT >= 2, large batches) store with sc1: the lines leave the
+// XCD's L2 instead of displacing the weight fragments every workgroup
+// re-reads from it (hundreds of MB of activations stream out per launch).
+// base must be wave-uniform; idx in floats.
+template <int RT>
+__device__ __forceinline__ void tc_st4(float* base, size_t idx, float4 v) {
+  const tc_u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(u, buf_rsrc(base), (unsigned)(idx * 4), 0, RT >= 2 ? 16 : 0);
+}
+template <int RT>
+__device__ __forceinline__ void tc_st2(float* base, size_t idx, float a, float b) {
+  typedef unsigned tc_u32x2 __attribute__((ext_vector_type(2)));
+  const tc_u32x2 u = {__float_as_uint(a), __float_as_uint(b)};
+  __builtin_amdgcn_raw_buffer_store_b64(u, buf_rsrc(base), (unsigned)(idx * 4), 0, RT >= 2 ? 16 : 0);
+}
+template <int RT>
+__device__ __forceinline__ void tc_st1(float* base, size_t idx, float a) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(a), buf_rsrc(base), (unsigned)(idx * 4), 0, RT >= 2 ? 16 : 0);
 }
 
 // zero padding [width, next_k) of every row of B (ones column at width if asked)
@@ -231,7 +255,7 @@ __device__ __forceinline__ void tc_mma(const TcBuf& IN, int k0, int ns, const Tc
 // log2 sum, and the pixel offset of the row's image
 template <int RT>
 struct TcRows {
-  float q[RT], p[RT], l2[RT];
+  float q[RT], p[RT], l2[RT], b2[RT];     // b2: Keras-BCE log2 sum (L_alpha)
   unsigned xoff[RT];
 };
 
@@ -284,13 +308,13 @@ __device__ __forceinline__ void tc_store_act(COp& S, const TcBuf& OUT, int t, co
 #else
     if (S.out && row < nrows) {
 #endif
-      float* dst = S.out + (size_t)(row0 + row) * S.ld_out + f0;
+      const size_t o = (size_t)(row0 + row) * S.ld_out + f0;
       if (full) {
-        *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+        tc_st4<RT>(S.out, o, make_float4(v[0], v[1], v[2], v[3]));
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          if (f0 + i < S.N) dst[i] = v[i];
+          if (f0 + i < S.N) tc_st1<RT>(S.out, o + i, v[i]);
       }
     }
   }
@@ -334,38 +358,50 @@ __device__ __forceinline__ void tc_head(const TcArgs& A, COp& S, const TcBuf& H,
         if (j < d) {
           if (S.acc) R.q[rt] += normal_logp(h, mu[c], sc);
           if (S.stdnormal) R.p[rt] += -0.5f * (h * h) - kHalfLog2Pi;
-          if (st) {
-            S.h[(size_t)grow * S.ld_h + j] = h;
-            S.eps[(size_t)grow * S.ld_eps + j] = ec;
-            Pr[j] = mu[c];
-            Pr[d + j] = zs[c];
-          }
         }
         hv[c] = j < d ? h : (j == d ? 1.f : 0.f);
       }
+      // the lane's two columns as one 8-byte store per tensor (j0 is even and
+      // every row stride a multiple of 4 floats); a last odd column alone
+      const size_t po = (size_t)grow * S.ld_out;
+      if (st && j0 + 1 < d) {
+        tc_st2<RT>(S.h, (size_t)grow * S.ld_h + j0, hv[0], hv[1]);
+        tc_st2<RT>(S.eps, (size_t)grow * S.ld_eps + j0, e.x, e.y);
+        tc_st2<RT>(S.out, po + j0, mu[0], mu[1]);
+        if ((d & 1) == 0) {
+          tc_st2<RT>(S.out, po + d + j0, zs[0], zs[1]);
+        } else {
+          tc_st1<RT>(S.out, po + d + j0, zs[0]);
+          tc_st1<RT>(S.out, po + d + j0 + 1, zs[1]);
+        }
+      } else if (st && j0 < d) {
+        tc_st1<RT>(S.h, (size_t)grow * S.ld_h + j0, hv[0]);
+        tc_st1<RT>(S.eps, (size_t)grow * S.ld_eps + j0, e.x);
+        tc_st1<RT>(S.out, po + j0, mu[0]);
+        tc_st1<RT>(S.out, po + d + j0, zs[0]);
+      }
       tc_put1(H, row * H.ld + j0, hv[0]);
       tc_put1(H, row * H.ld + j0 + 1, hv[1]);
-    } else if (KIND == TC_HEADP) {
+    } else {
+      if (KIND != TC_HEADP) {
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int j = j0 + c;
-        if (j < d && st) {
-          Pr[j] = mu[c];
-          Pr[d + j] = zs[c];
+        for (int c = 0; c < 2; ++c) {
+          const float sc = fexp(zs[c]) + kScaleEps;
+          if (j0 + c < d) R.p[rt] += normal_logp(c == 0 ? tv[rt].x : tv[rt].y, mu[c], sc);
         }
       }
-    } else {
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int j = j0 + c;
-        if (j < d) {
-          const float sc = fexp(zs[c]) + kScaleEps;
-          R.p[rt] += normal_logp(c == 0 ? tv[rt].x : tv[rt].y, mu[c], sc);
-          if (st && Pr) {
-            Pr[j] = mu[c];
-            Pr[d + j] = zs[c];
-          }
+      const size_t po = (size_t)grow * S.ld_out;
+      if (st && Pr && j0 + 1 < d) {
+        tc_st2<RT>(S.out, po + j0, mu[0], mu[1]);
+        if ((d & 1) == 0) {
+          tc_st2<RT>(S.out, po + d + j0, zs[0], zs[1]);
+        } else {
+          tc_st1<RT>(S.out, po + d + j0, zs[0]);
+          tc_st1<RT>(S.out, po + d + j0 + 1, zs[1]);
         }
+      } else if (st && Pr && j0 < d) {
+        tc_st1<RT>(S.out, po + j0, mu[0]);
+        tc_st1<RT>(S.out, po + d + j0, zs[0]);
       }
     }
     __builtin_amdgcn_sched_barrier(0);     // one row tile at a time (register pressure)
@@ -389,11 +425,15 @@ __device__ __forceinline__ void tc_bern(const TcArgs& A, COp& S, int t, const tc
     bin = bin && (xv[rt].x == 0.f || xv[rt].x == 1.f) && (xv[rt].y == 0.f || xv[rt].y == 1.f) &&
           (xv[rt].z == 0.f || xv[rt].z == 1.f) && (xv[rt].w == 0.f || xv[rt].w == 1.f);
   const bool allbin = __all(bin);
+  // L_alpha's Keras BCE term (F:317-F:323, F:396-F:400): clip(p, eps, 1 - eps)
+  // is the identity for these probabilities (p in [1e-7, 1 - 9e-7]), so the
+  // selected BCE probability is sel + eps and its logit factor 1 / (sel + eps)
+  const bool bce = A.need_bce != 0;
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     float gv[4];
     if (allbin) {
-      float prod = 1.f;
+      float prod = 1.f, prodb = 1.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float x = f4_at(xv[rt], i);
@@ -403,9 +443,16 @@ __device__ __forceinline__ void tc_bern(const TcArgs& A, COp& S, int t, const tc
         const float sel = __builtin_fmaf(s, kProbScale, one ? kProbShift : kBernOff0T);
         prod *= (f0 + i < S.N) ? sel : 1.f;
         const float dsg = kProbScale * (s * (1.f - s));
-        gv[i] = A.wa * ((one ? dsg : -dsg) * frcp(sel));
+        float f = A.wa * frcp(sel);
+        if (bce) {
+          const float bs = sel + kKerasEps;
+          prodb *= (f0 + i < S.N) ? bs : 1.f;
+          f += A.wb * frcp(bs);
+        }
+        gv[i] = (one ? dsg : -dsg) * f;
       }
       R.l2[rt] += __builtin_amdgcn_logf(prod);
+      if (bce) R.b2[rt] += __builtin_amdgcn_logf(prodb);
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -417,7 +464,14 @@ __device__ __forceinline__ void tc_bern(const TcArgs& A, COp& S, int t, const tc
         const float v = x * __builtin_amdgcn_logf(p1) + (1.f - x) * __builtin_amdgcn_logf(p0);
         R.l2[rt] += (f0 + i < S.N) ? v : 0.f;
         const float dsg = kProbScale * (sp * (1.f - sp));
-        gv[i] = A.wa * ((x * frcp(p1) - (1.f - x) * frcp(p0)) * dsg);
+        float f = A.wa * (x * frcp(p1) - (1.f - x) * frcp(p0));
+        if (bce) {
+          const float b1 = p1 + kKerasEps, b0 = p0 + kKerasEps;
+          const float vb = x * __builtin_amdgcn_logf(b1) + (1.f - x) * __builtin_amdgcn_logf(b0);
+          R.b2[rt] += (f0 + i < S.N) ? vb : 0.f;
+          f += A.wb * (x * frcp(b1) - (1.f - x) * frcp(b0));
+        }
+        gv[i] = f * dsg;
       }
     }
     const int row = rt * 16 + r;
@@ -426,13 +480,13 @@ __device__ __forceinline__ void tc_bern(const TcArgs& A, COp& S, int t, const tc
 #else
     if (row < nrows && f0 < S.N) {
 #endif
-      float* dst = S.out + (size_t)(row0 + row) * S.ld_out + f0;
+      const size_t o = (size_t)(row0 + row) * S.ld_out + f0;
       if (f0 + 3 < S.N) {
-        *reinterpret_cast<float4*>(dst) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+        tc_st4<RT>(S.out, o, make_float4(gv[0], gv[1], gv[2], gv[3]));
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          if (f0 + i < S.N) dst[i] = gv[i];
+          if (f0 + i < S.N) tc_st1<RT>(S.out, o + i, gv[i]);
       }
     }
   }
@@ -600,10 +654,19 @@ __device__ __forceinline__ int tc_dense(const TcArgs& A, CJob& J, COp& S, const 
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) acc[rt] = (tc_f32x4){0.f, 0.f, 0.f, 0.f};
     }
+#if IWAE_TC_UNCOND
+    // requests past the op's last unit (or the next op's) are out-of-range
+    // loads of zeros: unconditional, so the wait counts stay static
+    if (handover) tc_issue_u(S, q, u + 2, nxt);
+    tc_mma<RT>(IN, x.k0, x.ns, cur, acc);
+    if (handover && Sn) tc_issue_u(*Sn, qn, u, cur);
+    if (!handover) tc_issue_u(S, q, u + 2, cur);
+#else
     if (handover && u + 2 < U) tc_issue_u(S, q, u + 2, nxt);
     tc_mma<RT>(IN, x.k0, x.ns, cur, acc);
     if (handover && u < Un) tc_issue_u(*Sn, qn, u, cur);
     if (!handover && u + 2 < U) tc_issue_u(S, q, u + 2, cur);
+#endif
 #ifdef IWAE_TC_TRACE
     if (st) {
       asm volatile("" ::"v"(acc[0][0]) : "memory");
@@ -675,7 +738,9 @@ __device__ __forceinline__ void tc_dense2(const TcArgs& A, CJob& J, COp& S, cons
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) acc[rt] = (tc_f32x4){0.f, 0.f, 0.f, 0.f};
     }
-    if (u + 1 < U) tc_issue_u(S, q, u + 1, nxt);
+    // unconditional (past the op's last unit: out-of-range loads of zeros): a
+    // conditional request makes the compiler wait for every load in flight
+    tc_issue_u(S, q, u + 1, nxt);
     tc_mma<RT>(IN, x.k0, x.ns, cur, acc);
     if (x.last) {
       switch (kind) {
@@ -723,43 +788,69 @@ __device__ __forceinline__ void tc_sample0(const TcArgs& A, CJob& J, COp& S, uin
   const TcBuf H = tc_buf<RT>(J, S.out_buf);
   const int rg = row0 + min(rr, nrows - 1);
   const bool st = S.h != nullptr && rr < nrows;
-  const float* Pp = S.P + (size_t)(rg / S.P_div) * S.ld_P;
+  // the row's image (mu | zs) as buffer loads, a batch of up to 4 column quads
+  // per thread with every load issued before the first is used (one memory
+  // round trip per batch instead of one per quad)
+  const __amdgpu_buffer_rsrc_t rP = buf_rsrc(S.P);
+  const unsigned pbase = (unsigned)((size_t)(rg / S.P_div) * S.ld_P) * 4u;
+  const bool inj = A.eps_a[S.layer] != nullptr;
   float aq = 0.f, ap = 0.f;
-  for (int gq = sub; 4 * gq < S.next_k; gq += TPR) {
-    float mu[4], zs[4];
+  for (int g0 = sub; 4 * g0 < S.next_k; g0 += 4 * TPR) {
+    float mu[4][4], zs[4][4];
+    float2 ea[4], eb[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int jc = min(4 * gq + q, d - 1);
-      mu[q] = Pp[jc];
-      zs[q] = Pp[d + jc];
-    }
-    float4 e4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (A.eps_a[S.layer]) {
-      const float2 a = tc_eps2(A, S.layer, d, rg, 4 * gq), b = tc_eps2(A, S.layer, d, rg, 4 * gq + 2);
-      e4 = make_float4(a.x, a.y, b.x, b.y);
-    } else if (4 * gq < d) {
-      e4 = philox_normal4(A.seed, base, (unsigned)rg, (unsigned)S.layer, (unsigned)gq);
-    }
-    float hv[4];
+    for (int i = 0; i < 4; ++i) {
+      const int gq = g0 + i * TPR;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = 4 * gq + q;
-      hv[q] = 0.f;
-      if (j < d) {
-        const float sc = fexp(zs[q]) + kScaleEps;
-        const float e = f4_at(e4, q);
-        hv[q] = e * sc + mu[q];
-        aq += normal_logp(hv[q], mu[q], sc);
-        ap += -0.5f * (hv[q] * hv[q]) - kHalfLog2Pi;
-        if (st) {
-          S.h[(size_t)rg * S.ld_h + j] = hv[q];
-          S.eps[(size_t)rg * S.ld_eps + j] = e;
-        }
-      } else if (j == d) {
-        hv[q] = 1.f;
+      for (int q = 0; q < 4; ++q) {
+        const int j = 4 * gq + q;
+        mu[i][q] = bld1(rP, j < d ? pbase + (unsigned)j * 4u : kOOB);
+        zs[i][q] = bld1(rP, j < d ? pbase + (unsigned)(d + j) * 4u : kOOB);
+      }
+      if (inj) {
+        ea[i] = tc_eps2(A, S.layer, d, rg, min(4 * gq, d));
+        eb[i] = tc_eps2(A, S.layer, d, rg, min(4 * gq + 2, d));
       }
     }
-    tc_put4(H, rr * H.ld + 4 * gq, hv);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int gq = g0 + i * TPR;
+      if (4 * gq >= S.next_k) break;
+      float4 e4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (inj) {
+        e4 = make_float4(ea[i].x, ea[i].y, eb[i].x, eb[i].y);
+      } else if (4 * gq < d) {
+        e4 = philox_normal4(A.seed, base, (unsigned)rg, (unsigned)S.layer, (unsigned)gq);
+      }
+      float hv[4], ev[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = 4 * gq + q;
+        hv[q] = 0.f;
+        ev[q] = f4_at(e4, q);
+        if (j < d) {
+          const float sc = fexp(zs[i][q]) + kScaleEps;
+          hv[q] = ev[q] * sc + mu[i][q];
+          aq += normal_logp(hv[q], mu[i][q], sc);
+          ap += -0.5f * (hv[q] * hv[q]) - kHalfLog2Pi;
+        } else if (j == d) {
+          hv[q] = 1.f;
+        }
+      }
+      if (st && 4 * gq + 3 < d) {
+        tc_st4<RT>(S.h, (size_t)rg * S.ld_h + 4 * gq, make_float4(hv[0], hv[1], hv[2], hv[3]));
+        tc_st4<RT>(S.eps, (size_t)rg * S.ld_eps + 4 * gq, e4);
+      } else if (st) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (4 * gq + q < d) {
+            tc_st1<RT>(S.h, (size_t)rg * S.ld_h + 4 * gq + q, hv[q]);
+            tc_st1<RT>(S.eps, (size_t)rg * S.ld_eps + 4 * gq + q, ev[q]);
+          }
+        }
+      }
+      tc_put4(H, rr * H.ld + 4 * gq, hv);
+    }
   }
   for (int o = TPR >> 1; o > 0; o >>= 1) {
     aq += __shfl_xor(aq, o);
@@ -843,7 +934,7 @@ __device__ __forceinline__ void tc_gbwd(const TcArgs& A, CJob& J, COp& S, int ro
       const float z = hv[q] * rs - mu[q] * rs;
       float dmu, dsc;
       if (KIND == TC_GBWD_PRIOR) {
-        if (st) S.dh[(size_t)rg * S.ld_dh + c] = dl * (-z * rs);
+        if (st) tc_st1<RT>(S.dh, (size_t)rg * S.ld_dh + c, dl * (-z * rs));
         dmu = dl * (z * rs);
         dsc = dl * ((z * z - 1.f) * rs);
       } else {
@@ -857,9 +948,9 @@ __device__ __forceinline__ void tc_gbwd(const TcArgs& A, CJob& J, COp& S, int ro
       const float dzs = dsc * ez;
       tc_put1(B, rr * B.ld + c, dmu);
       tc_put1(B, rr * B.ld + d + c, dzs);
-      if (st) {
-        S.out[(size_t)rg * S.ld_out + c] = dmu;
-        S.out[(size_t)rg * S.ld_out + d + c] = dzs;
+      if (st && S.out) {
+        tc_st1<RT>(S.out, (size_t)rg * S.ld_out + c, dmu);
+        tc_st1<RT>(S.out, (size_t)rg * S.ld_out + d + c, dzs);
       }
     }
   }
@@ -1031,7 +1122,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   float* rq = tcs + plan->acc_off;
   float* rp = rq + R;
-  float* red = rp + R;                  // [3][NW][R]
+  float* red = rp + R;                  // [4][NW][R]
   if (t < R) { rq[t] = 0.f; rp[t] = 0.f; }
   // this workgroup's dL/dlw and dpx (the op buffers' space stages the images'
   // log weights: nothing is in them yet).  (Inside the op loop, beside the
@@ -1043,7 +1134,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     const int row = min(rt * 16 + (lane & 15), nrows - 1);
-    Rw.q[rt] = 0.f; Rw.p[rt] = 0.f; Rw.l2[rt] = 0.f;
+    Rw.q[rt] = 0.f; Rw.p[rt] = 0.f; Rw.l2[rt] = 0.f; Rw.b2[rt] = 0.f;
     Rw.xoff[rt] = (unsigned)((row0 + row) / A.kS) * (unsigned)A.ldx * 4u;
   }
 #ifdef IWAE_TC_TRACE
@@ -1134,9 +1225,9 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
     const int r = lane & 15, g = lane >> 4;
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
-      float v[3] = {Rw.q[rt], Rw.p[rt], Rw.l2[rt]};
+      float v[4] = {Rw.q[rt], Rw.p[rt], Rw.l2[rt], Rw.b2[rt]};
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
+      for (int k = 0; k < 4; ++k) {
         v[k] += __shfl_xor(v[k], 16);
         v[k] += __shfl_xor(v[k], 32);
         if (g == 0) red[(k * TC_NW + wave) * R + rt * 16 + r] = v[k];
@@ -1145,15 +1236,16 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
   }
   __syncthreads();
   if (t < nrows) {
-    float s3[3] = {0.f, 0.f, 0.f};
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < 3; ++k)
+    for (int k = 0; k < 4; ++k)
 #pragma unroll
-      for (int w = 0; w < TC_NW; ++w) s3[k] += red[(k * TC_NW + w) * R + t];
+      for (int w = 0; w < TC_NW; ++w) s4[k] += red[(k * TC_NW + w) * R + t];
     const int rg = row0 + t;
-    if (J.logq) J.logq[rg] = rq[t] + s3[0];
-    if (J.logp) J.logp[rg] = rp[t] + s3[1];
-    if (J.bern) J.bern[(size_t)rg * J.ld_bern + J.bern_col] = kLn2 * s3[2];
+    if (J.logq) J.logq[rg] = rq[t] + s4[0];
+    if (J.logp) J.logp[rg] = rp[t] + s4[1];
+    if (J.bern) J.bern[(size_t)rg * J.ld_bern + J.bern_col] = kLn2 * s4[2];
+    if (J.bce) J.bce[(size_t)rg * J.ld_bern + J.bern_col] = kLn2 * s4[3];
   }
 }
 

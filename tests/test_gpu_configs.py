@@ -44,8 +44,9 @@ def _case(arch, B, k, seed, n_draws=1):
     return O, spec, params, mean, x, draws
 
 
-def _run(arch, loss, B, k, seed, **kw):
-    """One train step on the GPU and in the oracle; returns the comparisons."""
+def _run(arch, loss, B, k, seed, engine_launches=None, **kw):
+    """One train step on the GPU and in the oracle; returns the comparisons
+    (engine_launches: a list that receives the step's train-engine launches)."""
     from iwae_replication_project_amd import Adam, Flexible_Model
     from iwae_replication_project_amd.flexible_iwae import _split, weight_shapes
     n_draws = 2 if loss == "CIWAE" else 1
@@ -55,7 +56,10 @@ def _run(arch, loss, B, k, seed, **kw):
     m.set_weights(_split(O.flatten_params(spec, params).astype(np.float32), weight_shapes(m.dense)))
     m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
     eps_gpu = [e.astype(np.float32) for d in draws for e in d]
+    n0 = m._lib.iwae_debug_count(m._h, 2)
     loss_gpu = m.train_step(x.astype(np.float32), eps=eps_gpu)[loss]
+    if engine_launches is not None:
+        engine_launches.append(m._lib.iwae_debug_count(m._h, 2) - n0)
     okw = {n: kw[n] for n in ("p", "alpha", "beta", "k1", "k2") if n in kw}
     if loss == "CIWAE":
         okw["eps2"] = draws[1]
@@ -93,7 +97,11 @@ def test_configs0_1L_full_width_k5_b20_every_loss(loss, kw):
 def test_configs3_k64_m8_k8_beta05(loss):
     """BASELINE configs[3]: 2L, k=64 with M=K=8 (MIWAE / PIWAE), beta=0.5 (CIWAE)."""
     kw = dict(k1=8, k2=8) if loss in ("MIWAE", "PIWAE") else dict(beta=0.5)
-    _check(_run(ARCH2, loss, 20, 64, 400 + len(loss), **kw))
+    n = []
+    _check(_run(ARCH2, loss, 20, 64, 400 + len(loss), engine_launches=n, **kw))
+    # on the train engine (forward, backward and the image-row jobs; PIWAE: a
+    # second backward pass on the MIWAE weighting)
+    assert n[0] >= (4 if loss == "PIWAE" else 3), n
 
 
 def test_configs4_per_gpu_share_b512_k50():

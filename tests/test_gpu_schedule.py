@@ -55,7 +55,8 @@ def test_lr_stages_track_oracle_adam_with_injected_noise():
     D.train_schedule(m, x.astype(np.float32), stages=stages, batch_size=B, passes=lambda i: 2 if i == 2 else 1,
                      on_stage=lambda i, tot, res: seen.append((i, tot, m.optimizer.learning_rate)))
     assert [s[:2] for s in seen] == [(1, 1), (2, 3), (3, 4)]
-    assert [s[2] for s in seen] == [D.stage_learning_rate(i) for i in (1, 2, 3)] == [1e-3, 7.2e-4, 5.2e-4]
+    np.testing.assert_allclose([s[2] for s in seen], [D.stage_learning_rate(i) for i in (1, 2, 3)], rtol=1e-12)
+    np.testing.assert_allclose([s[2] for s in seen], [1e-3, 7.2e-4, 5.2e-4], rtol=1e-12)
 
     opt = O.Adam(1e-3, 0.9, 0.999, 1e-4)
     ref = []
