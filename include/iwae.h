@@ -128,7 +128,7 @@ enum iwae_knob {
   IWAE_KNOB_MG_WAVES = 16,     /* NLL kernel workgroup: 8 waves / 64 rows or 4 waves / 32 rows (8) */
   IWAE_KNOB_NLL_ROWS = 17,     /* sample rows per NLL chunk (2^20) */
   IWAE_KNOB_WIDE_ROWS = 18,    /* engine: 32 / 64-row workgroups from this many sample rows (4097) */
-  IWAE_KNOB_DW_WIDE = 19,      /* beyond UPD_ROWS: weight gradients on the 112 x 256-block kernel (1) */
+  IWAE_KNOB_DW_WIDE = 19,      /* beyond UPD_ROWS: weight gradients on the 112 x 256-block kernel (0) */
   IWAE_KNOB_LD_ALIGN = 20      /* workspace row strides: multiples of 4, 8, 16 or 32 floats (4) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);

@@ -181,7 +181,8 @@ struct iwae_handle {
   int upd_tn32 = 0;                  // ... sample-row layers in 64 x 32 tiles
   int upd_slabs = 1;                 // ... and beyond upd_rows its split-K gradient pass into the slabs
   long long upd_slab_wg = 512;       // sample-row workgroups of that pass
-  int dw_wide = 1;                   // ... run by the 112 x 256-block weight-gradient kernel (iwae_dwgrad.hip)
+  int dw_wide = 0;                   // ... run by the 112 x 256-block weight-gradient kernel (iwae_dwgrad.hip;
+                                     // measured slower than the update kernel's pass: 223 vs 190 us at B = 512)
   long long dw_target = 768;         // split-K target workgroups per layer of the grouped weight-gradient GEMMs
   int smallm_rows = 32;              // first encoder layer on the few-row launches up to this many images (0: never)
   long long nll_rows = 1LL << 20;    // sample rows per NLL chunk (measured fastest: 2^17-2^20 within 10 %)

@@ -188,7 +188,7 @@ def test_wide_engine_and_dw_kernel_match_the_16_row_engine(B):
     rng = np.random.default_rng(66)
     x = (rng.random((B, 784)) < 0.2).astype(np.float32)
     eps = [rng.standard_normal((50, B, d)).astype(np.float32) for d in ARCH2[2]]
-    la, ga, wa = _run_steps({}, x, eps)
+    la, ga, wa = _run_steps({"dw_wide": 1}, x, eps)
     lb, gb, wb = _run_steps({"wide_rows": 1 << 30, "dw_wide": 0}, x, eps)
     assert abs(la[0] - lb[0]) <= 1e-6 * abs(lb[0])
     assert np.linalg.norm(ga - gb) <= 2e-5 * np.linalg.norm(gb)
@@ -203,13 +203,14 @@ def test_dw_kernel_graph_replays_and_data_parallel_tail():
     grouped weight-gradient GEMMs."""
     rng = np.random.default_rng(67)
     x = (rng.random((100, 784)) < 0.2).astype(np.float32)
-    la, ga, wa = _run_steps({}, x, steps=3)
-    lb, gb, wb = _run_steps({"upd_slabs": 0}, x, steps=3)
-    assert la[0] == lb[0]                              # same forward, same Philox draw
-    np.testing.assert_allclose(la, lb, rtol=1e-4)
-    assert np.linalg.norm(ga - gb) <= 3e-3 * np.linalg.norm(gb)
-    assert np.abs(wa - wb).max() < 3e-3
-    lc, gc, wc = _run_steps({}, x, steps=3, dp=True)
+    for tune in ({"dw_wide": 1}, {"dw_wide": 0}):
+        la, ga, wa = _run_steps(tune, x, steps=3)
+        lb, gb, wb = _run_steps({"upd_slabs": 0}, x, steps=3)
+        assert la[0] == lb[0]                          # same forward, same Philox draw
+        np.testing.assert_allclose(la, lb, rtol=1e-4)
+        assert np.linalg.norm(ga - gb) <= 3e-3 * np.linalg.norm(gb)
+        assert np.abs(wa - wb).max() < 3e-3
+    lc, gc, wc = _run_steps(tune, x, steps=3, dp=True)
     np.testing.assert_allclose(lc, la, rtol=1e-6)
     assert np.linalg.norm(gc - ga) <= 1e-4 * np.linalg.norm(ga)
     assert np.abs(wc - wa).max() < 1e-5
