@@ -176,6 +176,7 @@ def main():
     ap.add_argument("--nll-k", type=int, default=5000)
     ap.add_argument("--no-nll", action="store_true")
     ap.add_argument("--no-large-batch", action="store_true")
+    ap.add_argument("--no-stats", action="store_true")
     ap.add_argument("--large-batch-steps", type=int, default=20)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -377,6 +378,26 @@ def main():
                    tflops=round(NLL_FLOP_PER_IMAGE * (args.nll_k / 5000) * args.nll_images / el2 / 1e12, 3),
                    precision="bf16x3")
 
+    # ---- get_training_statistics (F:496-F:526) over the 10k synthetic test images
+    # at the model's k: VAE, IWAE, E_q log p(x|h), both KLs, reconstruction loss
+    # (chunks of 2000 images), two k=5000 NLL passes over all images (F:515,
+    # F:518), 1000 encoder draws for the unit activity (F:521), LL_pruned (F:524)
+    stats = None
+    if not args.no_stats and world == 1:
+        xt, _ = synthetic_images(args.nll_images, 99)
+        xs = model._x(xt)
+        model.get_training_statistics(xs[:200], K, batch_size=10)     # warm the shapes' workspaces
+        torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        res, res2 = model.get_training_statistics(xs, K, batch_size=10)
+        torch.cuda.synchronize()
+        el5 = time.perf_counter() - t4
+        stats = dict(value=round(args.nll_images / el5, 1), unit="images/s", seconds=round(el5, 4),
+                     images=args.nll_images, k=K, batch_size=10, nll=round(res["NLL"], 4),
+                     active_units=res2["number_of_active_units"],
+                     workload="get_training_statistics (F:496-F:526) over the synthetic test set, batched "
+                              "(per-batch reductions kept; two k=5000 NLL passes over all images)")
+
     # ---- configs[0]: 1 stochastic layer 784-200-200-50, IWAE k=5, batch 20 per GPU
     c0 = None
     if not args.no_c0:
@@ -434,6 +455,7 @@ def main():
             "loss": round(loss, 4),
             "nll": nll,
             "large_batch": large,
+            "training_statistics": stats,
             "configs0_train": c0,
             "roofline": roofline,
             "cpu_baseline": cpu,

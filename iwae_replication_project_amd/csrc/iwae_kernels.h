@@ -357,6 +357,10 @@ struct UpdArgs {
   const AdamState* state; int do_adam;
   float gscale;                                       // gradient written as gscale * dW (data parallel: B_local)
   float* tail; float tail_val;                        // data parallel: *tail = tail_val (B_local), or null
+  // apply mode (data parallel, after the all-reduce): no reduction; the tile's
+  // gradient is read from grad, scaled by 1 / *scale_dev (or gscale), written
+  // back, then Adam and the FX / GX copies as usual
+  int apply; const float* scale_dev;
 };
 hipError_t launch_update(hipStream_t st, const UpdArgs& a);
 hipError_t upd_setup_attributes();

@@ -53,6 +53,9 @@ constexpr int MG_KS = 8;             // k steps of 32 per weight fetch (256 k)
 #define IWAE_MG_PF 2
 #endif
 constexpr int MG_PF = IWAE_MG_PF;    // steps of the next column tile requested during the current one
+#ifndef IWAE_MG_UNCOND     // unconditional fragment loads: measured 62.9 K vs 63.8 K images/s, off
+#define IWAE_MG_UNCOND 0
+#endif
 
 extern __shared__ __attribute__((aligned(16))) float mgs[];
 
@@ -119,11 +122,20 @@ __device__ __forceinline__ unsigned mg_frag_base(const MgStage& S, int t, int k0
 }
 // k step u of the fragment: 1 KiB further (an invalid tile's kOOB + 1024 u
 // stays beyond the buffer: it reads 0)
+// (IWAE_MG_UNCOND: unconditional, a step past ns reading zeros out of range,
+// so the compiler's wait counts stay static -- measured slower here: the
+// extra fragment registers cost more than the waits)
 __device__ __forceinline__ void mg_fetch_step(__amdgpu_buffer_rsrc_t rh, __amdgpu_buffer_rsrc_t rl, unsigned vb,
                                               int u, int ns, MgFrag& f) {
+#if IWAE_MG_UNCOND
+  const unsigned v = u < ns ? vb : kOOB;
+  f.h[u] = mg_as_bf16x8(__builtin_amdgcn_raw_buffer_load_b128(rh, v, 1024 * u, 0));
+  f.l[u] = mg_as_bf16x8(__builtin_amdgcn_raw_buffer_load_b128(rl, v, 1024 * u, 0));
+#else
   if (u >= ns) return;
   f.h[u] = mg_as_bf16x8(__builtin_amdgcn_raw_buffer_load_b128(rh, vb, 1024 * u, 0));
   f.l[u] = mg_as_bf16x8(__builtin_amdgcn_raw_buffer_load_b128(rl, vb, 1024 * u, 0));
+#endif
 }
 // A fragments of column tile t over k in [k0, k0 + 256): 8 steps of 32, hi and lo
 __device__ __forceinline__ void mg_fetch(const MgStage& S, __amdgpu_buffer_rsrc_t rh, __amdgpu_buffer_rsrc_t rl,
@@ -176,7 +188,11 @@ __device__ __forceinline__ void mg_mma(const MgBuf& IN, int k0, int ns, MgFrag& 
 #pragma unroll
     for (int i = 0; i < RH; ++i)
       acc[p * RH + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[u], ah[b][i], acc[p * RH + i], 0, 0, 0);
+#if IWAE_MG_UNCOND
+    if (p == NP - 1 && u < MG_PF) mg_fetch_step(rh, rl, pf ? pf_vb : kOOB, u, pf_ns, f);
+#else
     if (p == NP - 1 && u < MG_PF && pf) mg_fetch_step(rh, rl, pf_vb, u, pf_ns, f);
+#endif
   }
 }
 

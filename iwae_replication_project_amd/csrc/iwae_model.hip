@@ -93,7 +93,7 @@ struct iwae_handle {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t side_stream = nullptr;   // second branch of a train step (the fused update's sample-row tiles)
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_mid = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
   iwae_config cfg{};
@@ -1406,6 +1406,11 @@ static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const
 // bf16x3 products, and up to upd_rows sample rows (one workgroup reduces a
 // tile over all rows: beyond that the split-K GEMM + Adam launches parallelise
 // better).
+static bool upd_tiles_ok(const iwae_handle* h) {
+  long long tiles = 0;
+  for (const DenseL& d : h->dense) tiles += cdiv(d.fin + 1, 64) * cdiv(d.fout, h->upd_tn32 ? 32 : 64);
+  return tiles <= kUpdMaxTiles && (int)h->dense.size() <= kUpdMaxJobs;
+}
 static bool use_update(const iwae_handle* h, const Plan& P) {
   if (!h->upd || !h->x3 || (long long)P.Bimg * P.kS > h->upd_rows) return false;
   long long tiles = 0;
@@ -1424,8 +1429,14 @@ static bool use_update_slabs(const iwae_handle* h, const Plan& P) {
          (int)h->dense.size() <= kUpdMaxJobs;
 }
 
-static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hipStream_t st = nullptr,
-                      float gscale = 1.f, float* tail = nullptr, bool slabs = false) {
+// bucket: 0 every layer, 1 the output MLP only, 2 every layer but the output
+// MLP (the data-parallel step's two all-reduce buckets: the output MLP is the
+// last range of the parameter buffer).  apply: data parallel after the
+// all-reduce -- no reduction, Adam + FX / GX from the summed gradient in the
+// buffer times 1 / *scale_dev.
+static int run_update(iwae_handle* h, const Plan& P, bool adam, int bucket = 0, hipStream_t st = nullptr,
+                      float gscale = 1.f, float* tail = nullptr, bool slabs = false, bool apply = false,
+                      const float* scale_dev = nullptr) {
   if (!st) st = h->stream;
   const int L = h->L, M = P.Bimg * P.kS;
   constexpr long long UP_ROWS_ITER = 128;      // rows per reduction iteration of the update kernel
@@ -1447,12 +1458,11 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hi
   js.push_back({h->o1, &h->h[0], &h->ob.dY1, M, nullptr});
   js.push_back({h->o2, &h->ob.y1, &h->ob.dY2, M, nullptr});
   js.push_back({h->o3, &h->ob.y2, &h->ob.P, M, h->dpx});
-  if (part != 0) {
-    const StochL& S0 = h->enc[0];
+  if (bucket != 0) {
     std::vector<WJ> keep;
     for (const WJ& w : js) {
-      const bool first = w.di == S0.l1 || w.di == S0.l2 || w.di == S0.head;
-      if (first == (part == 2)) keep.push_back(w);
+      const bool out = w.di == h->o1 || w.di == h->o2 || w.di == h->o3;
+      if (out == (bucket == 1)) keep.push_back(w);
     }
     js.swap(keep);
   }
@@ -1511,10 +1521,11 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int part = 0, hi
   a.per_xcd2 = (int)cdiv(tiles - heavy, 8);
   a.param = h->params; a.m = h->adam_m; a.v = h->adam_v; a.grad = slabs ? h->slabs : h->grad;
   a.fx_hi = h->fx_hi; a.fx_lo = h->fx_lo;
-  a.state = &h->ds->adam; a.do_adam = adam && !slabs ? 1 : 0;
-  a.gscale = slabs ? 1.f : gscale; a.tail = slabs ? nullptr : tail; a.tail_val = gscale;
+  a.state = &h->ds->adam; a.do_adam = (adam || apply) && !slabs ? 1 : 0;
+  a.gscale = slabs ? 1.f : gscale; a.tail = (slabs || apply) ? nullptr : tail; a.tail_val = gscale;
+  a.apply = apply ? 1 : 0; a.scale_dev = scale_dev;
   HIPCHK(launch_update(st, a));
-  if (adam && part != 1) h->params_version++;
+  if (a.do_adam) h->params_version++;
   if (h->prof_kind == 15 && adam && !h->prof_have) {
     // replays repeat this step's update on scratch copies of the parameters,
     // moments and fragment-major copies: the model is untouched
@@ -2136,14 +2147,29 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
     // data parallel: the fused gradient pass (B_local * g, B_local in the
     // tail), the all-reduce, then Adam and the fragment-major copies
     float* tail = h->grad + h->nparam_int;
-    CHK(run_update(h, P, false, 0, nullptr, (float)P.B, tail));
-    if (!adam) return IWAE_OK;
+    if (!adam) return run_update(h, P, false, 0, nullptr, (float)P.B, tail);
     if (!h->comm) return fail(h, IWAE_EINVAL, "data parallel without a library communicator");
-    if (ncclAllReduce(h->grad, h->grad, (size_t)h->nparam_int + 4, ncclFloat32, ncclSum, h->comm, h->stream) !=
-        ncclSuccess)
+    // two buckets whose gradient passes run side by side (each pass alone is a
+    // latency chain on a fraction of the CUs): the output MLP's (the last
+    // range of the buffer, with the tail) on the step's stream, then its
+    // all-reduce while the other layers' pass may still run on the side
+    // stream; then their all-reduce; then ONE launch of Adam and the FX / GX
+    // copies from the summed buffer (the update kernel's apply mode, in place
+    // of the Adam and FX-refresh launches).  Both all-reduces on one stream:
+    // collectives of one communicator stay ordered.
+    const long long o0 = h->dense[h->o1].off;
+    HIPCHK(hipEventRecord(h->ev_fork, h->stream));
+    HIPCHK(hipStreamWaitEvent(h->side_stream, h->ev_fork, 0));
+    CHK(run_update(h, P, false, 2, h->side_stream, (float)P.B, nullptr));
+    HIPCHK(hipEventRecord(h->ev_join, h->side_stream));
+    CHK(run_update(h, P, false, 1, nullptr, (float)P.B, tail));
+    if (ncclAllReduce(h->grad + o0, h->grad + o0, (size_t)(h->nparam_int - o0) + 4, ncclFloat32, ncclSum, h->comm,
+                      h->stream) != ncclSuccess)
+      return fail(h, IWAE_EHIP, "ncclAllReduce of the gradient (output MLP bucket) failed");
+    HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+    if (ncclAllReduce(h->grad, h->grad, (size_t)o0, ncclFloat32, ncclSum, h->comm, h->stream) != ncclSuccess)
       return fail(h, IWAE_EHIP, "ncclAllReduce of the gradient failed");
-    CHK(run_adam(h, false, true, true, 0.f, false, tail));
-    CHK(run_fx(h));
+    CHK(run_update(h, P, true, 0, nullptr, 1.f, nullptr, false, true, tail));
     h->fx_version = h->params_version;
     return IWAE_OK;
   }
@@ -2156,6 +2182,19 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   if (use_update_slabs(h, P) && h->dw_wide) CHK(run_dw(h, P));
   else if (use_update_slabs(h, P)) CHK(run_update(h, P, false, 0, nullptr, 1.f, nullptr, true));
   else CHK(weight_grads(h, P, true, true, h->dpx));
+  if (h->dp_weighted && adam && h->upd && upd_tiles_ok(h)) {
+    // data parallel: the slabs summed into B_local * g (+ tail), the
+    // all-reduce, then Adam + the FX / GX copies in one update launch
+    float* tail = h->grad + h->nparam_int;
+    CHK(run_adam(h, true, true, false, (float)P.B, false, nullptr, tail));
+    if (!h->comm) return fail(h, IWAE_EINVAL, "data parallel without a library communicator");
+    if (ncclAllReduce(h->grad, h->grad, (size_t)h->nparam_int + 4, ncclFloat32, ncclSum, h->comm, h->stream) !=
+        ncclSuccess)
+      return fail(h, IWAE_EHIP, "ncclAllReduce of the gradient failed");
+    CHK(run_update(h, P, true, 0, nullptr, 1.f, nullptr, false, true, tail));
+    h->fx_version = h->params_version;
+    return IWAE_OK;
+  }
   CHK(finish_step(h, P, adam));
   if (adam) {
     // the next step's engine reads the updated weights' fragment-major copies
@@ -2354,6 +2393,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_mid, hipEventDisableTiming);
   const size_t pb = (size_t)h->nparam_int * sizeof(float);
   // the row-block kernels fetch whole padded k ranges (up to 255 rows, or 256
   // floats of a row, past a matrix's end): keep that inside a zeroed tail
@@ -2423,6 +2463,7 @@ void iwae_destroy(iwae_handle* h) {
   if (h->side_stream) (void)hipStreamDestroy(h->side_stream);
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  if (h->ev_mid) (void)hipEventDestroy(h->ev_mid);
   delete h;
 }
 

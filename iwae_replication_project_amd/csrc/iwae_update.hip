@@ -15,7 +15,7 @@
 // 16 lanes; the buffer resource advances by 128 rows per iteration so rows
 // past the last read 0), transposes it in registers and writes k-contiguous
 // bf16 hi / lo rows into LDS (ds_write_b128, row stride 72 dwords = 8 mod 16,
-// 8-row blocks XOR-swizzled by (row >> 3) & 7).  Wave w multiplies k step w
+// 8-row blocks XOR-swizzled by (row >> 2) & 7).  Wave w multiplies k step w
 // (32 rows) of the iteration into its own copy of the whole 64 x 64 tile (16
 // accumulator tiles of v_mfma_f32_16x16x32_bf16, bf16x3: a_hi b_hi + a_hi b_lo
 // + a_lo b_hi), so each LDS byte is read once; the next iteration's split and
@@ -55,9 +55,13 @@ constexpr int kUpdAblate = IWAE_UPD_ABLATE;
 
 extern __shared__ __attribute__((aligned(16))) float ups[];
 
-// dword offset of row n's 8-row block `blk` in a plane (blocks XOR-swizzled by
-// (n >> 3) & 7: the column writes of sixteen lanes spread over the banks)
-__device__ __forceinline__ int up_off(int n, int blk) { return n * UP_S + 4 * (blk ^ ((n >> 3) & 7)); }
+// dword offset of row n's 8-row block `blk` in a plane, blocks XOR-swizzled by
+// (n >> 2) & 7: the transposed staging writes (ds_write_b128, eight lanes of a
+// column set per LDS cycle, consecutive lanes four rows apart) and the
+// fragment reads (ds_read_b128) are both conflict-free on gfx950's lane groups
+// (the earlier (n >> 3) & 7 swizzle left both 2-way: 47 % of the LDS cycles
+// were bank conflicts, profiles/r02g_pmc_summary.txt)
+__device__ __forceinline__ int up_off(int n, int blk) { return n * UP_S + 4 * (blk ^ ((n >> 2) & 7)); }
 // staging lane map: thread t loads rows 8 rg .. 8 rg + 7 of columns 4 cq ..
 // 4 cq + 3; sixteen consecutive lanes read one row's 256 contiguous bytes
 // (measured: lanes spread over more rows per load instruction were slower)
@@ -245,7 +249,8 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
   // never carried around a loop (a loop-carried set is renamed at the back
   // edge with register copies, which drain every load in flight); loads past
   // the last row are unconditional out-of-range reads of zeros
-  const int ngrp = (kUpdAblate & 64) ? 0 : (J.rows + UP_G * UP_RI - 1) / (UP_G * UP_RI);
+  // (apply mode: no reduction, the gradient comes from the buffer)
+  const int ngrp = ((kUpdAblate & 64) || a.apply) ? 0 : (J.rows + UP_G * UP_RI - 1) / (UP_G * UP_RI);
   float* buf0 = ups;
   float* buf1 = ups + UP_BUF;
   const UpOff O = up_offsets<TN>(J, i0, j0);
@@ -322,6 +327,21 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
   __syncthreads();
   if (kUpdAblate & 8) return;
 
+  float g[EJ];
+  float wsc = a.gscale;
+  if (a.apply) {
+    // data parallel, after the all-reduce: the summed gradient of the tile's
+    // elements times 1 / (sum of the ranks' batch sizes)
+    const float sc = a.scale_dev ? 1.f / *a.scale_dev : a.gscale;
+    const __amdgpu_buffer_rsrc_t rg = buf_rsrc(a.grad + J.off);
+#pragma unroll
+    for (int q = 0; q < EJ / 4; ++q) {
+      const int c = j0 + ej + 4 * q;
+      const float4 v = bld4(rg, (erow && c < J.ldw) ? (unsigned)((i0 + ei) * J.ldw + c) * 4u : kOOB);
+      g[4 * q] = v.x * sc; g[4 * q + 1] = v.y * sc; g[4 * q + 2] = v.z * sc; g[4 * q + 3] = v.w * sc;
+    }
+    wsc = 1.f;
+  } else {
   // the four waves' tiles -> LDS, summed in wave order
   {
     const int lane = t & 63, w = t >> 6;
@@ -334,7 +354,6 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
         for (int q = 0; q < 4; ++q) part[(16 * si + 4 * (lane >> 4) + q) * PS + 16 * sj + (lane & 15)] = acc[si][sj][q];
   }
   __syncthreads();
-  float g[EJ];
 #pragma unroll
   for (int q = 0; q < EJ / 4; ++q) {
     float4 s = *reinterpret_cast<const float4*>(ups + ei * PS + ej + 4 * q);
@@ -345,6 +364,7 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
     }
     g[4 * q] = s.x; g[4 * q + 1] = s.y; g[4 * q + 2] = s.z; g[4 * q + 3] = s.w;
   }
+  }
   // gradient buffer (get_gradients, the SNR harness; data parallel: B_local
   // times the gradient, all-reduced before Adam)
   if (a.tail && b == 0 && t == 0) *a.tail = a.tail_val;
@@ -353,7 +373,7 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
     const int c = j0 + ej + 4 * q;
     if (erow && c < J.ldw)
       *reinterpret_cast<float4*>(a.grad + J.off + (long long)(i0 + ei) * J.ldw + c) =
-          make_float4(a.gscale * g[4 * q], a.gscale * g[4 * q + 1], a.gscale * g[4 * q + 2], a.gscale * g[4 * q + 3]);
+          make_float4(wsc * g[4 * q], wsc * g[4 * q + 1], wsc * g[4 * q + 2], wsc * g[4 * q + 3]);
   }
   if (!a.do_adam || (kUpdAblate & 32)) return;
 

@@ -613,11 +613,22 @@ class Flexible_Model:
         active_units, _, _ = self.get_active_units(variances, eigen_values, threshold)
         return float(-self.log_px_masked(x, active_units, n_samples, eps).mean().item())
 
-    def get_training_statistics(self, x, k, batch_size=10):
+    def get_training_statistics(self, x, k, batch_size=10, batched=True, chunk_images=2000):
         """F:496-F:526: (res, res2) with the reference's keys.  res: batch
         means of VAE, IWAE, NLL (k=5000), E_q log p(x|h), both KL terms,
         reconstruction_loss, and LL_pruned (on the first batch); res2: active
-        units (1000 draws over all of x), their counts, PCA counts, variances."""
+        units (1000 draws over all of x), their counts, PCA counts, variances.
+
+        batched=False runs the reference's loop literally: per batch of
+        batch_size images (F:512) one launch series per statistic -- for 10k
+        images, 2,000 k=5000 NLL calls of 10 images each (F:515, F:518).
+        batched=True (default) evaluates each statistic over many batches per
+        call (chunk_images, a multiple of batch_size; the k=5000 NLLs over all
+        images at once, chunked by the library) and keeps the per-batch
+        reduction: every statistic is a mean over images (equal batches), so
+        the mean of the batch means is the chunk-size-weighted mean of the
+        chunk means.  Each statistic still gets its own independent draw (the
+        reference's separate get_L / get_NLL calls), per image."""
         xd = self._x(x)
         N = xd.shape[0]
         if batch_size <= 0 or N == 0 or N % batch_size != 0:
@@ -629,17 +640,35 @@ class Flexible_Model:
         res["D_kl(q(h|x),p(h))"] = 0.0
         res["D_kl(q(h|x),p(h|x))"] = 0.0
         res["reconstruction_loss"] = 0.0
-        for i in range(nb):
-            b = xd[i * batch_size:(i + 1) * batch_size]
-            vae = self.get_L(b, k)
-            res["VAE"] += vae / nb
-            res["IWAE"] += self.get_L_k(b, k) / nb
-            res["NLL"] += self.get_NLL(b) / nb
-            eq = self.get_E_qhIx_log_pxIh(b, k)
-            res["E_q(h|x)[log(p(x|h))]"] += eq / nb
-            res["D_kl(q(h|x),p(h))"] += (eq - self.get_L(b, k)) / nb
-            res["D_kl(q(h|x),p(h|x))"] += -1 * (self.get_L(b, k) + self.get_NLL(b)) / nb
-            res["reconstruction_loss"] += self.get_reconstruction_loss(b) / nb
+        if batched:
+            step = max(batch_size, (int(chunk_images) // batch_size) * batch_size)
+            for lo in range(0, N, step):
+                b = xd[lo:lo + step]
+                w = b.shape[0] / N                 # (its batches) / nb
+                vae = self.get_L(b, k)
+                res["VAE"] += vae * w
+                res["IWAE"] += self.get_L_k(b, k) * w
+                eq = self.get_E_qhIx_log_pxIh(b, k)
+                res["E_q(h|x)[log(p(x|h))]"] += eq * w
+                res["D_kl(q(h|x),p(h))"] += (eq - self.get_L(b, k)) * w
+                res["D_kl(q(h|x),p(h|x))"] += -1 * self.get_L(b, k) * w
+                res["reconstruction_loss"] += self.get_reconstruction_loss(b) * w
+            nll1 = self.get_NLL(xd)                 # F:515, every batch in one launch series
+            nll2 = self.get_NLL(xd)                 # F:518's second, independent estimate
+            res["NLL"] = nll1
+            res["D_kl(q(h|x),p(h|x))"] += -1 * nll2          # -(get_L + get_NLL), F:412
+        else:
+            for i in range(nb):
+                b = xd[i * batch_size:(i + 1) * batch_size]
+                vae = self.get_L(b, k)
+                res["VAE"] += vae / nb
+                res["IWAE"] += self.get_L_k(b, k) / nb
+                res["NLL"] += self.get_NLL(b) / nb
+                eq = self.get_E_qhIx_log_pxIh(b, k)
+                res["E_q(h|x)[log(p(x|h))]"] += eq / nb
+                res["D_kl(q(h|x),p(h))"] += (eq - self.get_L(b, k)) / nb
+                res["D_kl(q(h|x),p(h|x))"] += -1 * (self.get_L(b, k) + self.get_NLL(b)) / nb
+                res["reconstruction_loss"] += self.get_reconstruction_loss(b) / nb
         res2 = {}
         variances, eigen_values = self.get_levels_of_units_activity(xd, 1000)
         res2["active_units"], res2["number_of_active_units"], res2["number_of_PCA_active_units"] = \

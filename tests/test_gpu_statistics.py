@@ -148,3 +148,28 @@ def test_training_statistics_has_the_reference_keys():
     assert [len(a) for a in res2["active_units"]] == list(spec.n_latent_encoder)
     assert res2["number_of_active_units"] == [sum(a) for a in res2["active_units"]]
     assert len(res2["number_of_PCA_active_units"]) == spec.L and len(res2["variances"]) == spec.L
+
+
+def test_batched_training_statistics_keep_the_per_batch_reductions(monkeypatch):
+    """The batched statistics (many batches per call, every k=5000 NLL over
+    all images in one launch series) equal the reference loop's mean of batch
+    means: with each per-call statistic replaced by a deterministic function
+    of its images (the mean pixel), both paths give the same numbers; on the
+    real model both give finite estimates within the NLL's sampling noise."""
+    O, spec, params, m, x, rng = _setup(ARCHS[1], 12, 40)
+
+    def fake(b, *a, **kw):
+        return float(m._x(b).double().mean().item())
+    for name in ("get_L", "get_L_k", "get_NLL", "get_E_qhIx_log_pxIh", "get_reconstruction_loss"):
+        monkeypatch.setattr(m, name, fake)
+    monkeypatch.setattr(m, "get_NLL_without_inactive_units", lambda b, *a, **kw: 1.0)
+    ra, _ = m.get_training_statistics(x, 5, batch_size=10, batched=False)
+    rb, _ = m.get_training_statistics(x, 5, batch_size=10, batched=True, chunk_images=20)
+    for key in ra:
+        assert abs(ra[key] - rb[key]) <= 1e-9 * max(1.0, abs(ra[key])), (key, ra[key], rb[key])
+    monkeypatch.undo()
+    r1, _ = m.get_training_statistics(x, 5, batch_size=10, batched=False)
+    r2, _ = m.get_training_statistics(x, 5, batch_size=10, batched=True)
+    assert abs(r1["NLL"] - r2["NLL"]) < 0.5, (r1["NLL"], r2["NLL"])
+    for key in r2:
+        assert np.isfinite(r2[key]), key

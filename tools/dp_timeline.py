@@ -1,7 +1,8 @@
 """One configs[1] train step through the library's data-parallel path (RCCL
 communicator owned by the handle, world size 1 on one GPU) for a rocprofv3
 kernel trace: shows where the gradient all-reduce sits in the captured step
-(after the grouped weight-gradient GEMM, before Adam).
+(two buckets: the output MLP bucket all-reduced on a side stream beside the
+other layers' gradient pass, then one Adam + FX / GX launch).
     rocprofv3 --kernel-trace -d gpurun_out/dp -o run -- python tools/dp_timeline.py"""
 import os
 import sys

@@ -1,8 +1,9 @@
 """Config C4: gradient SNR over R noise draws for the 2L model at
 k = 64 (IWAE, PIWAE / MIWAE with M = K = 8, CIWAE with beta = 0.5: two
 independent draws per estimate, F:382-F:383), batch 20; prints draws/s and
-the median SNR of the encoder and decoder parameters.  Under torchrun the R
-draws are split over the ranks (one all-reduce of the moments)."""
+the median SNR of the encoder and decoder parameters, and the train step's
+time for the same loss (graph-replayed Philox steps, Adam included).  Under
+torchrun the R draws are split over the ranks (one all-reduce of the moments)."""
 import os
 import sys
 import time
@@ -30,5 +31,19 @@ for loss, kw in (("IWAE", {}), ("PIWAE", dict(k1=8, k2=8)), ("MIWAE", dict(k1=8,
     flat = [np.asarray(s).ravel() for s in snr]
     enc = np.concatenate([f for f, nm in zip(flat, names) if nm.startswith("enc")])
     dec = np.concatenate([f for f, nm in zip(flat, names) if not nm.startswith("enc")])
+    from iwae_replication_project_amd import Adam
+    m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+    xd = m._x(x)
+    n0 = m._lib.iwae_debug_count(m._h, 2)
+    for _ in range(10):
+        m.train_step(xd, sync=False)
+    engine = m._lib.iwae_debug_count(m._h, 2) > n0
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(200):
+        m.train_step(xd, sync=False)
+    torch.cuda.synchronize()
+    st = (time.perf_counter() - t) / 200
     print(f"{loss:6s} k=64 R={R}: {R / el:8.1f} draws/s  median SNR encoder {np.median(enc[np.isfinite(enc)]):.3f}"
-          f"  decoder {np.median(dec[np.isfinite(dec)]):.3f}", flush=True)
+          f"  decoder {np.median(dec[np.isfinite(dec)]):.3f}   train step {st * 1e3:.4f} ms "
+          f"({20 * 64 / st / 1e6:.2f} M image*samples/s, engine {engine})", flush=True)
