@@ -494,6 +494,41 @@ struct MgLaunch {
 hipError_t launch_mega_fwd(hipStream_t st, const MgLaunch& L, int rt, int waves, size_t lds_bytes);
 hipError_t mega_setup_attributes();
 
+// ------------------------------- weight-ring k-sample forward (NLL) ----
+// nring_kernel (iwae_nring.hip): the same per-row work as mega_fwd_kernel for
+// 1- and 2-layer models, activations of 16 rows per wave in registers, the
+// weights shared by the workgroup's 8 waves (128 rows) through an LDS ring of
+// NR_D slots filled by LDS-DMA from FX, one (column tile, k <= 256) unit per
+// slot.  Stage order in st[]: e1, e2, eh (SAMPLE h2), p1, p2, ph (PRIOR of
+// h1), o1, o2, ob (Bernoulli); a 1-layer model uses st[6..8] only.
+constexpr int NR_D = 8;
+constexpr int kNrMaxUnits = 512;
+struct NrUnit {
+  unsigned off;              // FX byte offset of (column tile, k step 0), both planes
+  int ns;                    // k steps of 32 (<= 8)
+};
+struct NrStage {
+  int ntile, ns, N;          // column tiles, k steps of the input, output features (heads: 8 * ceil(d / 4))
+  int d, layer, stdnormal;   // head stages
+  int next_ns;               // tanh stages: k steps of the reader (ones column at N, zeros up to it)
+};
+struct NrLaunch {
+  const __bf16* fx_hi; const __bf16* fx_lo; unsigned fx_bytes;
+  const NrUnit* units; int nunits;                // the units in consumption order (device memory)
+  int L;
+  NrStage st[9];
+  int rows, kS;                                   // sample rows of the launch (kS >= 128), samples per image
+  const float* P0; int ldP0; int d0;              // first encoder layer's (mu | zs) per image
+  const float* x; int ldx; int xdim;              // pixels [images][ldx], xdim <= 800
+  uint64_t seed; const uint64_t* rng_base;
+  const float* eps[8]; int eps_N, eps_i0, eps_s0; // injected noise (MgLaunch's convention) or null
+  float* lw;                                      // out: log w per row
+};
+bool nring_shape_ok(const NrLaunch& L);   // L, stage ns filled: an instantiated shape
+hipError_t launch_nring(hipStream_t st, const NrLaunch& L);
+hipError_t nring_setup_attributes();
+size_t nring_lds_bytes();
+
 // ---------------------------------------- row-chain train engine (bf16x3) ----
 // The small- and large-batch train step's per-sample-row work (everything
 // after the first encoder layer, forward and backward) as chains of ops run by

@@ -155,6 +155,10 @@ struct iwae_handle {
   int x3 = 1;                        // tiled GEMMs: 1 bf16x3 products (default), 0 exact f32 MFMA
   int nll_fused = 1;                 // NLL: fused k-sample forward (mega_fwd_kernel) when it fits
   int mg_waves = 8;                  // mega_fwd_kernel workgroup: 8 waves (64 rows) or 4 (32 rows, 2 per CU)
+  int nring = 1;                     // NLL: the weight-ring kernel (nring_kernel) where its shapes apply
+  NrUnit* nr_units = nullptr;        // its unit table (device, built once: FX offsets are fixed per model)
+  int nr_nunits = 0;
+  long long n_nring = 0;             // nring_kernel launches, iwae_debug_count
   bool masked = false;               // active-unit masks in force (iwae_nll_masked only)
   long long n_mega = 0, n_mega_eps = 0;  // mega_fwd_kernel launches (all / injected noise), iwae_debug_count
   long long n_tc = 0;                    // train-engine launches (tc_kernel), iwae_debug_count(h, 2)
@@ -2429,6 +2433,7 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   h->fx_lo = h->fx_hi + h->fx_elems;
   e = rb_setup_attributes();
   if (e == hipSuccess) e = mega_setup_attributes();
+  if (e == hipSuccess) e = nring_setup_attributes();
   if (e == hipSuccess) e = smallm_setup_attributes();
   if (e == hipSuccess) e = tc_setup_attributes();
   if (e == hipSuccess) e = upd_setup_attributes();
@@ -2455,6 +2460,7 @@ void iwae_destroy(iwae_handle* h) {
   if (h->adam_v) (void)hipFree(h->adam_v);
   if (h->grad_own) (void)hipFree(h->grad_own);
   if (h->ds) (void)hipFree(h->ds);
+  if (h->nr_units) (void)hipFree(h->nr_units);
   if (h->wsplit_hi) (void)hipFree(h->wsplit_hi);
   if (h->fx_hi) (void)hipFree(h->fx_hi);
   if (h->prof_scratch) (void)hipFree(h->prof_scratch);
@@ -2585,6 +2591,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_NLL_ROWS: h->nll_rows = std::max(1LL, value); break;
     case IWAE_KNOB_WIDE_ROWS: h->wide_rows = std::max(0LL, value); break;
     case IWAE_KNOB_DW_WIDE: h->dw_wide = on; break;
+    case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_LD_ALIGN:
       if (value != 4 && value != 8 && value != 16 && value != 32)
         return fail(h, IWAE_EINVAL, "LD_ALIGN must be 4, 8, 16 or 32");
@@ -2952,6 +2959,62 @@ static bool mega_plan(iwae_handle* h, MgLaunch& M, int& rt, int& waves, size_t& 
   return false;
 }
 
+// Plan of nring_kernel (iwae_nring.hip): stages and the unit table in
+// consumption order.  False when the model is not one of the kernel's
+// instantiated shapes (mega_fwd_kernel runs instead).
+static bool nring_plan(iwae_handle* h, NrLaunch& R) {
+  const int L = h->L;
+  std::memset(&R, 0, sizeof(R));
+  if (!h->nring || (L != 1 && L != 2) || h->xdim > 800) return false;
+  std::vector<NrUnit> units;
+  auto stage = [&](int si, int di, int N, int next_k) {
+    const DenseL& d = h->dense[di];
+    NrStage& S = R.st[si];
+    S.N = N;
+    S.ntile = (N + 15) / 16;
+    S.ns = d.ldF / 32;
+    S.next_ns = next_k / 32;
+    for (int t = 0; t < S.ntile; ++t)
+      units.push_back(NrUnit{(unsigned)((d.fx_off + (long long)t * S.ns * 512) * (long long)sizeof(__bf16)), S.ns});
+    return S.ns <= 8 && d.ldF % 32 == 0;
+  };
+  auto r32 = [](int x) { return (x + 31) & ~31; };
+  bool ok = true;
+  if (L == 2) {
+    const StochL& E = h->enc[1];
+    const StochL& D = h->dec[0];
+    ok = ok && stage(0, E.l1, h->dense[E.l1].fout, h->dense[E.l2].ldF);
+    ok = ok && stage(1, E.l2, h->dense[E.l2].fout, h->dense[E.head].ldF);
+    ok = ok && stage(2, E.head, 8 * ((E.d + 3) / 4), 0);
+    R.st[2].d = E.d; R.st[2].layer = 1; R.st[2].stdnormal = 1;
+    ok = ok && stage(3, D.l1, h->dense[D.l1].fout, h->dense[D.l2].ldF);
+    ok = ok && stage(4, D.l2, h->dense[D.l2].fout, h->dense[D.head].ldF);
+    ok = ok && stage(5, D.head, 8 * ((D.d + 3) / 4), 0);
+    R.st[5].d = D.d; R.st[5].layer = 0; R.st[5].stdnormal = 0;
+    // the h2 pair layout holds 8 * 4 * H2 columns, h1's 8 * 4 * H1 (ones column included)
+    ok = ok && r32(E.d + 1) == h->dense[D.l1].ldF && r32(h->enc[0].d + 1) == h->dense[E.l1].ldF;
+  }
+  ok = ok && stage(6, h->o1, h->dense[h->o1].fout, h->dense[h->o2].ldF);
+  ok = ok && stage(7, h->o2, h->dense[h->o2].fout, h->dense[h->o3].ldF);
+  ok = ok && stage(8, h->o3, h->dense[h->o3].fout, 0);
+  ok = ok && r32(h->enc[0].d + 1) == h->dense[h->o1].ldF && (int)units.size() + NR_D <= kNrMaxUnits;
+  R.L = L;
+  R.d0 = h->enc[0].d;
+  R.xdim = h->xdim;
+  R.nunits = (int)units.size();
+  if (!ok || !nring_shape_ok(R)) return false;
+  if (!h->nr_units) {
+    if (hipMalloc(&h->nr_units, kNrMaxUnits * sizeof(NrUnit)) != hipSuccess) return false;
+    if (hipMemcpy(h->nr_units, units.data(), units.size() * sizeof(NrUnit), hipMemcpyHostToDevice) != hipSuccess)
+      return false;
+    h->nr_nunits = (int)units.size();
+  }
+  R.units = h->nr_units;
+  R.fx_hi = h->fx_hi; R.fx_lo = h->fx_lo;
+  R.fx_bytes = (unsigned)(h->fx_elems * (long long)sizeof(__bf16));
+  return true;
+}
+
 // chunked k-sample NLL over N images; accumulates per-image (m, s)
 // eps (optional, parity): L buffers [k][N][d_i]; only the fused kernel takes
 // them chunk by chunk (the caller checks nll_mega_ok first)
@@ -2983,6 +3046,10 @@ static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, flo
   if (eps && !mega) return fail(h, IWAE_EINVAL, "injected-noise NLL chunks need the fused kernel");
   for (int i = 0; i < 8; ++i) MG.eps[i] = (eps && i < h->L) ? eps[i] : nullptr;
   MG.eps_N = N;
+  NrLaunch NR;
+  const bool ring = mega && nring_plan(h, NR);
+  for (int i = 0; i < 8; ++i) NR.eps[i] = MG.eps[i];
+  NR.eps_N = N;
   const size_t wbytes = (size_t)h->xdim * sizeof(float);
   for (int i0 = 0; i0 < N; i0 += imgs) {
     const int n = std::min(imgs, N - i0);
@@ -3003,7 +3070,17 @@ static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, flo
         MG.x = h->x_in.p; MG.ldx = h->x_in.ld;
         MG.seed = h->seed; MG.rng_base = &h->ds->rng[0];
         MG.lw = h->lw;
-        HIPCHK(launch_mega_fwd(h->stream, MG, mg_rt, mg_waves, mg_lds));
+        if (ring && P.kS >= 128) {
+          // the weight-ring kernel (same rows, same noise; 128 rows per workgroup
+          // span at most two images)
+          NR.rows = MG.rows; NR.kS = MG.kS; NR.eps_i0 = i0; NR.eps_s0 = s0;
+          NR.P0 = MG.P0; NR.ldP0 = MG.ldP0; NR.x = MG.x; NR.ldx = MG.ldx;
+          NR.seed = MG.seed; NR.rng_base = MG.rng_base; NR.lw = MG.lw;
+          HIPCHK(launch_nring(h->stream, NR));
+          ++h->n_nring;
+        } else {
+          HIPCHK(launch_mega_fwd(h->stream, MG, mg_rt, mg_waves, mg_lds));
+        }
         ++h->n_mega;
         if (eps) ++h->n_mega_eps;
         a.lw = h->lw;
@@ -3190,6 +3267,7 @@ long long iwae_debug_count(const iwae_handle* h, int what) {
     case 0: return h->n_mega;
     case 1: return h->n_mega_eps;
     case 2: return h->n_tc;
+    case 3: return h->n_nring;
     default: return -1;
   }
 }

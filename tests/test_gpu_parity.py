@@ -425,6 +425,38 @@ def test_fused_nll_kernel_matches_layerwise_path(arch, pixels):
     np.testing.assert_allclose(b, a, rtol=2e-5, atol=2e-3)
 
 
+@pytest.mark.parametrize("arch", [([200, 100], [100, 200], [100, 50], [100, 784]),    # configs[1..4]
+                                  ([200], [200], [50], [784])])                          # configs[0]
+@pytest.mark.parametrize("pixels", ["binary", "fractional"])
+@pytest.mark.parametrize("k", [700, 5000, 100])
+def test_weight_ring_nll_kernel_matches_register_streaming_kernel(arch, pixels, k):
+    """The weight-ring NLL kernel (nring_kernel: activations of 16 rows per wave
+    in registers, weights shared by 128 rows through an LDS-DMA ring) against
+    mega_fwd_kernel on the same Philox noise and weights: same products in the
+    same order, so per-image log p(x) agree to float rounding.  k=700 puts
+    image boundaries inside workgroups and a ragged last workgroup; k=100
+    (< 128 samples per image) runs mega_fwd_kernel on both sides (counter)."""
+    he, hd, le, ld = arch
+    rng = np.random.default_rng(29)
+    x = rng.random((5, 784)).astype(np.float32)
+    if pixels == "binary":
+        x = (x < 0.25).astype(np.float32)
+    out = {}
+    for ring in (0, 1):
+        m = make_model(he, hd, le, ld, seed=43)
+        if ring == 0:
+            w0 = m.get_weights()
+        else:
+            m.set_weights(w0)
+        m.set_tuning("nring", ring)
+        n0 = m._lib.iwae_debug_count(m._h, 3)
+        out[ring] = m.log_px(x, k).cpu().numpy().astype(np.float64)
+        launches = m._lib.iwae_debug_count(m._h, 3) - n0
+        assert (launches > 0) == (ring == 1 and k >= 128), (ring, k, launches)
+    assert np.all(np.isfinite(out[1]))
+    np.testing.assert_allclose(out[1], out[0], rtol=1e-5, atol=2e-4)
+
+
 def test_nll_chunking_and_sample_split_are_consistent():
     O, spec, params, m, x, rng = _concentrated_model(4, (64, 32), (32, 16))
     a = m.log_px(x, 3000, chunk=6).cpu().numpy()

@@ -7,4 +7,4 @@ cd "$(dirname "$0")/.."
 mkdir -p tools/_dbg
 S=iwae_replication_project_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -Wno-unused-result \
-  -o tools/_dbg/${OUT:-libiwae_dbg.so} $S/iwae_gemm.hip $S/iwae_elem.hip $S/iwae_fused.hip $S/iwae_mega.hip $S/iwae_train.hip $S/iwae_update.hip $S/iwae_dwgrad.hip $S/iwae_model.hip -lrccl "$@"
+  -o tools/_dbg/${OUT:-libiwae_dbg.so} $S/iwae_gemm.hip $S/iwae_elem.hip $S/iwae_fused.hip $S/iwae_mega.hip $S/iwae_nring.hip $S/iwae_train.hip $S/iwae_update.hip $S/iwae_dwgrad.hip $S/iwae_model.hip -lrccl "$@"
