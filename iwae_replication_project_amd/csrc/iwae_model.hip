@@ -2997,7 +2997,7 @@ static bool nring_plan(iwae_handle* h, NrLaunch& R) {
   ok = ok && stage(6, h->o1, h->dense[h->o1].fout, h->dense[h->o2].ldF);
   ok = ok && stage(7, h->o2, h->dense[h->o2].fout, h->dense[h->o3].ldF);
   ok = ok && stage(8, h->o3, h->dense[h->o3].fout, 0);
-  ok = ok && r32(h->enc[0].d + 1) == h->dense[h->o1].ldF && (int)units.size() + NR_D <= kNrMaxUnits;
+  ok = ok && r32(h->enc[0].d + 1) == h->dense[h->o1].ldF && (int)units.size() + NR_D <= kNrMaxUnits - 8;
   R.L = L;
   R.d0 = h->enc[0].d;
   R.xdim = h->xdim;

@@ -51,6 +51,11 @@ typedef unsigned nr_u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void nr_lds_void;
 
 constexpr int NR_W = 8;                       // waves, 16 rows each
+#ifndef IWAE_NR_G
+#define IWAE_NR_G 2
+#endif
+constexpr int NR_G = IWAE_NR_G;               // units per ring synchronization (1, 2 or 4)
+static_assert(NR_G == 1 || NR_G == 2 || NR_G == 4, "NR_G");
 constexpr int NR_ROWS = 16 * NR_W;            // rows per workgroup
 constexpr int NR_SLOT_BF16 = 8 * 2 * 512;     // one slot: 8 k steps x (hi, lo) x 64 lanes x 8 bf16
 constexpr int NR_PIXLD = 800;                 // floats per image in the pixel cache (>= xdim <= 800)
@@ -94,6 +99,11 @@ __device__ __forceinline__ float nr_normal_logp(float h, float mu, float sc) {
   const float z = h * rs - mu * rs;
   return -0.5f * (z * z) - (kHalfLog2Pi + kLn2 * __builtin_amdgcn_logf(sc));
 }
+
+// Materialize a running sum here.  lw is only read at the end of the kernel,
+// so without this hipcc sinks a stage's whole log-density computation there
+// and keeps its operands (h, mu, scale of every tile) live across the ring.
+__device__ __forceinline__ void nr_keep(float& v) { asm volatile("" : "+v"(v)); }
 
 // split 8 f32 into the hi / lo bf16 planes of one fragment
 __device__ __forceinline__ void nr_split8(const float (&v)[8], nr_bf16x8& h, nr_bf16x8& l) {
@@ -169,17 +179,6 @@ struct NrCtx {
   int u;                             // next unit to multiply
 };
 
-// LDS reads the compiler does not see.  hipcc tracks LDS-DMA writes as
-// pending on vmcnt and waits vmcnt(0) before an ordinary ds_read it cannot
-// tell apart from the ring slots (the pixel cache, the unit table): these
-// reads are ordered by the ring's own waits instead (their bytes were written
-// before the first barrier and never change).
-__device__ __forceinline__ nr_f32x4 nr_lds_rd4(unsigned addr) {
-  nr_f32x4 v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
-}
-
 // LDS-DMA of one unit into slot `slot`: this wave's k step, both planes (out
 // of range past the unit's k steps or the last unit: the pieces still count
 // in vmcnt, so every wave issues exactly two per unit)
@@ -187,24 +186,64 @@ __device__ __forceinline__ void nr_issue(const NrCtx& C, int slot, unsigned off,
   const int w = nr_wave(), lane = threadIdx.x & 63;
   const unsigned voff = w < ns ? off + (unsigned)w * 1024u + (unsigned)lane * 16u : kOOB;
   __bf16* dst = reinterpret_cast<__bf16*>(nrs) + slot * NR_SLOT_BF16 + w * 1024;
+#ifdef IWAE_NR_NODMA      // timing experiment only (wrong results): no weight stream
+  if (voff != 0x12345u) return;
+#endif
   __builtin_amdgcn_raw_ptr_buffer_load_lds(C.rh, (nr_lds_void*)dst, 16, voff, 0, 0, 0);
   __builtin_amdgcn_raw_ptr_buffer_load_lds(C.rl, (nr_lds_void*)(dst + 512), 16, voff, 0, 0, 0);
 }
 
-// Advance the ring to unit C.u; returns its slot.  The table entry of the unit
-// to request is read before the barrier (its lgkmcnt(0) retires the read).
+// Advance the ring to unit C.u; returns its slot.  The ring is synchronized
+// once per NR_G units (a group): at a group's first unit every wave waits for
+// its own pieces of the group's units (counted vmcnt), then lgkmcnt(0) (its
+// reads of the previous group's slots are done), then the barrier; after it
+// the group's slots are complete and the previous group's slots are free, and
+// each wave requests the NR_G units NR_D - NR_G ahead into them.
+// The table entries of those units are read by ds_read_b64 in the SAME asm
+// statement as the waits: hipcc takes an asm output as ready when the
+// statement ends, so an LDS read in one statement and its wait in a later
+// one lets the compiler copy the register before the data has arrived.  (The
+// table and the pixel cache are read in asm, or plain with hipcc's own
+// vmcnt(0), because hipcc cannot tell them apart from the DMA-written slots.)
 __device__ __forceinline__ const __bf16* nr_next(NrCtx& C) {
-  const int nu = C.u + NR_D - 1;
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-  u32x2 e;
   NR_TR(C.u, 0)
-  asm volatile("ds_read_b64 %0, %1" : "=v"(e) : "v"(NR_TAB_B + 8u * (unsigned)nu));
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (NR_D - 2)) : "memory");
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" : "+v"(e)::"memory");
+  if ((C.u & (NR_G - 1)) == 0) {
+    const int nu = C.u + NR_D - NR_G;            // the first unit to request
+    const unsigned ta = NR_TAB_B + 8u * (unsigned)nu;
+    u32x2 e0, e1, e2, e3;
+    // younger than this group's pieces: the units of the groups after it
+    if (NR_G == 4)
+      asm volatile("ds_read_b64 %0, %4\n\tds_read_b64 %1, %4 offset:8\n\tds_read_b64 %2, %4 offset:16\n\t"
+                   "ds_read_b64 %3, %4 offset:24\n\ts_waitcnt vmcnt(%5)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier"
+                   : "=&v"(e0), "=&v"(e1), "=&v"(e2), "=&v"(e3)
+                   : "v"(ta), "n"(2 * (NR_D - 2 * NR_G))
+                   : "memory");
+    else if (NR_G == 2)
+      asm volatile("ds_read_b64 %0, %2\n\tds_read_b64 %1, %2 offset:8\n\ts_waitcnt vmcnt(%3)\n\t"
+                   "s_waitcnt lgkmcnt(0)\n\ts_barrier"
+                   : "=&v"(e0), "=&v"(e1)
+                   : "v"(ta), "n"(2 * (NR_D - 2 * NR_G))
+                   : "memory");
+    else
+      asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt vmcnt(%2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier"
+                   : "=&v"(e0)
+                   : "v"(ta), "n"(2 * (NR_D - 2 * NR_G))
+                   : "memory");
+    nr_issue(C, nu % NR_D, __builtin_amdgcn_readfirstlane(e0[0]), (int)__builtin_amdgcn_readfirstlane(e0[1]));
+    if (NR_G >= 2)
+      nr_issue(C, (nu + 1) % NR_D, __builtin_amdgcn_readfirstlane(e1[0]), (int)__builtin_amdgcn_readfirstlane(e1[1]));
+    if (NR_G >= 4) {
+      nr_issue(C, (nu + 2) % NR_D, __builtin_amdgcn_readfirstlane(e2[0]), (int)__builtin_amdgcn_readfirstlane(e2[1]));
+      nr_issue(C, (nu + 3) % NR_D, __builtin_amdgcn_readfirstlane(e3[0]), (int)__builtin_amdgcn_readfirstlane(e3[1]));
+    }
+  }
   NR_TR(C.u, 1)
-  nr_issue(C, nu % NR_D, __builtin_amdgcn_readfirstlane(e[0]), (int)__builtin_amdgcn_readfirstlane(e[1]));
   const __bf16* slot = reinterpret_cast<const __bf16*>(nrs) + (C.u % NR_D) * NR_SLOT_BF16;
   ++C.u;
+  // one scheduling region per phase: nothing of a later unit's epilogue
+  // (e.g. its Philox draws, which do not depend on the MFMAs) is hoisted here
+  __builtin_amdgcn_sched_barrier(0);
   return slot;
 }
 
@@ -217,6 +256,10 @@ __device__ __forceinline__ nr_f32x4 nr_mma(const __bf16* slot, const NrFrag& IN,
   const int lane = threadIdx.x & 63;
   nr_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   nr_bf16x8 wh[3], wl[3];
+#ifdef IWAE_NR_NOMMA      // timing experiment only (wrong results): no LDS reads, no MFMAs
+  acc[0] = (float)IN.h[0][0] + (float)slot[lane];
+  return acc;
+#endif
   auto rd = [&](int s) {
     wh[s % 3] = *reinterpret_cast<const nr_bf16x8*>(slot + s * 1024 + lane * 8);
     wl[s % 3] = *reinterpret_cast<const nr_bf16x8*>(slot + s * 1024 + 512 + lane * 8);
@@ -243,42 +286,46 @@ __device__ __forceinline__ nr_f32x4 nr_mma(const __bf16* slot, const NrFrag& IN,
   return acc;
 }
 
+// Every stage below is software-pipelined by one unit: in the phase of unit
+// t (after its barrier) the wave issues unit t's ds_reads and MFMAs and runs
+// the epilogue of unit t - 1, whose accumulator is complete, so the epilogue's
+// VALU work fills the MFMA gaps (and the other wave of the SIMD is never
+// left with all the MFMAs while this one is in its epilogue).  Tile counts
+// are compile-time, so the loops unroll and no branch splits a phase.
+
 // tanh Dense layer: OUT = [tanh(IN . W) | 1 | 0 ...] as the next layer's B
-// fragments (the ones column at feature N, zeros up to the reader's last k
-// step).  A runtime loop over the reader's k steps (two column tiles each);
-// only the store of the packed step into OUT is a switch (registers are
-// addressed statically).
-template <int NSI>
-__device__ __forceinline__ void nr_tanh_tile(NrCtx& C, const NrStage& S, const NrFrag& IN, int t, float (&v)[4]) {
+// fragments (the ones column at feature N, zeros up to the reader's NSO k
+// steps).  NT column tiles (<= 2 NSO); the remaining tiles are the padding.
+template <int NSI, int NSO, int NT>
+__device__ __forceinline__ void nr_dense_tanh(NrCtx& C, const NrStage& S, const NrFrag& IN, NrFrag& OUT) {
+  static_assert(NT <= 2 * NSO, "tiles beyond the reader's k steps");
   const int g = (threadIdx.x & 63) >> 4;
-  if (t < S.ntile) {
-    const __bf16* slot = nr_next(C);
-    const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
+  float va[4];
+  auto epi = [&](int t, const nr_f32x4& a, bool real) {
+    float v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = 16 * t + 4 * g + i;
-      v[i] = f < S.N ? nr_tanh(acc[i]) : (f == S.N ? 1.f : 0.f);
+      v[i] = (real && f < S.N) ? nr_tanh(a[i]) : (f == S.N ? 1.f : 0.f);
     }
-  } else {
+    if (t & 1) {
+      nr_pack(va, v, OUT.h[t >> 1], OUT.l[t >> 1]);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = (16 * t + 4 * g + i == S.N) ? 1.f : 0.f;
-  }
-}
-template <int NSI, int NSO>
-__device__ __forceinline__ void nr_dense_tanh(NrCtx& C, const NrStage& S, const NrFrag& IN, NrFrag& OUT) {
-#pragma unroll 1
-  for (int sp = 0; sp < NSO; ++sp) {
-    float va[4], vb[4];
-    nr_tanh_tile<NSI>(C, S, IN, 2 * sp, va);
-    nr_tanh_tile<NSI>(C, S, IN, 2 * sp + 1, vb);
-    nr_bf16x8 oh, ol;
-    nr_pack(va, vb, oh, ol);
-    switch (sp) {
-#define NR_OUT(n) case n: if (n < NSO) { OUT.h[n] = oh; OUT.l[n] = ol; } break;
-      NR_OUT(0) NR_OUT(1) NR_OUT(2) NR_OUT(3) NR_OUT(4) NR_OUT(5) NR_OUT(6) NR_OUT(7)
-#undef NR_OUT
+      for (int i = 0; i < 4; ++i) va[i] = v[i];
     }
+  };
+  nr_f32x4 prev = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const __bf16* slot = nr_next(C);
+    const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
+    if (t > 0) epi(t - 1, prev, true);
+    prev = acc;
   }
+  epi(NT - 1, prev, true);
+#pragma unroll
+  for (int t = NT; t < 2 * NSO; ++t) epi(t, prev, false);
 }
 
 // head epilogue: (mu, zs) of the lane's two latent columns j0, j0 + 1
@@ -290,123 +337,213 @@ __device__ __forceinline__ void nr_head_pairs(const nr_f32x4& acc, float (&mu)[2
 }
 
 // sampling head (F:66-F:73): h = eps * (exp(zs) + 1e-6) + mu into hp (pair
-// layout; ones column at d), lw += -log q(h) (+ log N(h; 0, 1) on the top layer)
-template <int NSI, int NT, bool INJ>
-__device__ __forceinline__ void nr_head_sample(NrCtx& C, const NrLaunch& A, const NrStage& S, const NrFrag& IN,
-                                               float2 (&hp)[NT], uint64_t base, int grow, float& lw) {
-  const int lane = threadIdx.x & 63, g = lane >> 4;
+// layout; ones column at d; NT real tiles, padding tiles up to NP), lw +=
+// -log q(h) (+ log N(h; 0, 1) on the top layer).  ep: the noise pairs in
+// the same layout, drawn in the prologue (nr_noise_pairs).
+template <int NSI, int NT, int NP>
+__device__ __forceinline__ void nr_head_sample(NrCtx& C, const NrStage& S, const NrFrag& IN, const float2 (&ep)[NP],
+                                               float2 (&hp)[NP], float& lw) {
+  const int g = (threadIdx.x & 63) >> 4;
   const int d = S.d;
+  auto epi = [&](int t, const nr_f32x4& acc) {
+    const int j0 = 8 * t + 2 * g;
+    float mu[2], zs[2];
+    nr_head_pairs(acc, mu, zs);
+    float hv[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int j = j0 + c;
+      const float sc = fexp(zs[c]) + kScaleEps;
+      const float h = (c == 0 ? ep[t].x : ep[t].y) * sc + mu[c];
+      float contrib = -nr_normal_logp(h, mu[c], sc);
+      if (S.stdnormal) contrib += -0.5f * (h * h) - kHalfLog2Pi;
+      lw += j < d ? contrib : 0.f;
+      hv[c] = j < d ? h : (j == d ? 1.f : 0.f);
+    }
+    hp[t] = make_float2(hv[0], hv[1]);
+  };
+  nr_f32x4 prev = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const int q = 2 * t + (g >> 1);
-    const int j0 = 4 * q + 2 * (g & 1);
-    if (t < S.ntile) {
-      const __bf16* slot = nr_next(C);
-      const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
-      float mu[2], zs[2];
-      nr_head_pairs(acc, mu, zs);
-      float2 e;
-      if (INJ) {
-        const size_t eo = ((size_t)(A.eps_s0 + grow % A.kS) * A.eps_N + (A.eps_i0 + grow / A.kS)) * d;
-        const float* ep = A.eps[S.layer] + eo;
-        e.x = j0 < d ? ep[j0] : 0.f;
-        e.y = j0 + 1 < d ? ep[j0 + 1] : 0.f;
-      } else {
-        e = philox_normal2(A.seed, base, (unsigned)grow, (unsigned)S.layer, (unsigned)q, (g & 1) != 0);
-      }
-      float hv[2];
+    const __bf16* slot = nr_next(C);
+    const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
+    if (t > 0) epi(t - 1, prev);
+    prev = acc;
+  }
+  epi(NT - 1, prev);
+  nr_keep(lw);
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int j = j0 + c;
-        const float sc = fexp(zs[c]) + kScaleEps;
-        const float h = (c == 0 ? e.x : e.y) * sc + mu[c];
-        float contrib = -nr_normal_logp(h, mu[c], sc);
-        if (S.stdnormal) contrib += -0.5f * (h * h) - kHalfLog2Pi;
-        lw += j < d ? contrib : 0.f;
-        hv[c] = j < d ? h : (j == d ? 1.f : 0.f);
-      }
-      hp[t] = make_float2(hv[0], hv[1]);
-    } else {
-      hp[t] = make_float2(j0 == d ? 1.f : 0.f, j0 + 1 == d ? 1.f : 0.f);
+  for (int t = NT; t < NP; ++t) {
+    const int j0 = 8 * t + 2 * g;
+    hp[t] = make_float2(j0 == d ? 1.f : 0.f, j0 + 1 == d ? 1.f : 0.f);
+  }
+}
+
+// The noise of a row's latent layer in the head pair layout (lane group g of
+// tile t: columns 8t + 2g, + 1), Philox4x32-10 (the stream every path draws:
+// philox_normal4(seed, base, row, layer, quad q) = columns 4q .. 4q + 3).  One
+// Philox call per lane per two tiles: lane group g draws quad 2t + (g >> 1) +
+// 2 (g & 1) of the pair (t, t + 1), and one v_permlane16_swap of its two
+// halves with the partner group g ^ 1 hands every lane the halves it needs
+// (philox_normal2 per tile would draw every quad twice).  Injected noise
+// ([k][eps_N][d] per layer) is read instead when eps is set.  Columns past d
+// read / draw anything (the users mask them).
+template <int NP>
+__device__ __forceinline__ void nr_noise_pairs(const NrLaunch& A, const float* eps, int layer, int d, uint64_t base,
+                                               int grow, float2 (&ep)[NP]) {
+  const int g = (threadIdx.x & 63) >> 4;
+  if (eps) {
+    const float* er = eps + ((size_t)(A.eps_s0 + grow % A.kS) * A.eps_N + (A.eps_i0 + grow / A.kS)) * d;
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      const int j0 = 8 * t + 2 * g;
+      ep[t] = make_float2(er[min(j0, d - 1)], er[min(j0 + 1, d - 1)]);
     }
+    return;
+  }
+  const int nq = (d + 3) >> 2;
+#pragma unroll
+  for (int t = 0; t < NP; t += 2) {
+    if (2 * t >= nq) {                             // no real column in tiles t, t + 1 (uniform)
+      ep[t] = make_float2(0.f, 0.f);
+      if (t + 1 < NP) ep[t + 1] = make_float2(0.f, 0.f);
+      continue;
+    }
+    const int q = 2 * t + (g >> 1) + 2 * (g & 1);
+    const float4 n = philox_normal4(A.seed, base, (unsigned)grow, (unsigned)layer, (unsigned)q);
+    const auto sx = __builtin_amdgcn_permlane16_swap(__float_as_uint(n.x), __float_as_uint(n.z), false, false);
+    const auto sy = __builtin_amdgcn_permlane16_swap(__float_as_uint(n.y), __float_as_uint(n.w), false, false);
+    ep[t] = make_float2(__uint_as_float(sx[0]), __uint_as_float(sy[0]));
+    if (t + 1 < NP) ep[t + 1] = make_float2(__uint_as_float(sx[1]), __uint_as_float(sy[1]));
   }
 }
 
 // prior head (F:138-F:141): lw += log N(target; mu, exp(zs) + 1e-6) over the
-// target's pair layout
-template <int NSI, int NT>
-__device__ __forceinline__ void nr_head_prior(NrCtx& C, const NrStage& S, const NrFrag& IN, const float2 (&tp)[NT],
+// target's pair layout (NT tiles)
+template <int NSI, int NT, int NP>
+__device__ __forceinline__ void nr_head_prior(NrCtx& C, const NrStage& S, const NrFrag& IN, const float2 (&tp)[NP],
                                               float& lw) {
   const int g = (threadIdx.x & 63) >> 4;
   const int d = S.d;
+  auto epi = [&](int t, const nr_f32x4& acc) {
+    float mu[2], zs[2];
+    nr_head_pairs(acc, mu, zs);
+    const int j0 = 8 * t + 2 * g;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const float sc = fexp(zs[c]) + kScaleEps;
+      const float v = nr_normal_logp(c == 0 ? tp[t].x : tp[t].y, mu[c], sc);
+      lw += j0 + c < d ? v : 0.f;
+    }
+  };
+  nr_f32x4 prev = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    if (t < S.ntile) {
-      const __bf16* slot = nr_next(C);
-      const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
-      float mu[2], zs[2];
-      nr_head_pairs(acc, mu, zs);
-      const int j0 = 8 * t + 2 * g;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const float sc = fexp(zs[c]) + kScaleEps;
-        const float v = nr_normal_logp(c == 0 ? tp[t].x : tp[t].y, mu[c], sc);
-        lw += j0 + c < d ? v : 0.f;
-      }
-    }
+    const __bf16* slot = nr_next(C);
+    const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
+    if (t > 0) epi(t - 1, prev);
+    prev = acc;
   }
+  epi(NT - 1, prev);
+  nr_keep(lw);
 }
 
 // Bernoulli output layer (F:123-F:129): log2 of the selected probabilities,
-// four multiplied before one log (mega_fwd_kernel's mg_bern); the pixels come
-// from the workgroup's LDS image cache
+// four multiplied before one log (mega_fwd_kernel's mg_bern).
+// Binarized pixels (every pixel of the workgroup's images 0 or 1, the MNIST /
+// OMNIGLOT case) come from registers: seven words of pixel bits per lane,
+// made in the prologue in the order the pipelined epilogues consume them
+// (word m = the tiles whose epilogue runs in phases 8m .. 8m + 7, 4 bits per
+// tile), shifted down one word every eight phases.  Fractional pixels take
+// the two-log form with plain LDS reads of the image cache (hipcc then drains
+// the DMA ring before each read: correct, slower; test inputs only).
 constexpr float kNrBernOff0 = 9.1327896e-7f;   // 1 - 0.999999f - 1e-7f (f32 constants, F:126)
+// (the shapes' output width is a whole number of tiles: no column mask)
+__device__ __forceinline__ void nr_bern_bin(const NrStage& S, int t, const nr_f32x4& acc, unsigned nib, float& l2) {
+  float prod = 1.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bool one = (nib >> i) & 1u;
+    const float z = one ? acc[i] : -acc[i];
+    const float s = frcp(1.f + fexp(-z));
+    prod *= __builtin_fmaf(s, kProbScale, one ? kProbShift : kNrBernOff0);
+  }
+  l2 += __builtin_amdgcn_logf(prod);
+}
+__device__ __forceinline__ void nr_bern_frac(const NrStage& S, int t, const nr_f32x4& acc, const float* px,
+                                             float& l2) {
+  const int f0 = 16 * t + 4 * ((threadIdx.x & 63) >> 4);
+  const float4 xv = *reinterpret_cast<const float4*>(px + f0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float x = f4_at(xv, i);
+    const float e = fexp(-acc[i]);
+    const float sp = frcp(1.f + e);
+    const float p1 = __builtin_fmaf(sp, kProbScale, kProbShift);
+    const float p0 = __builtin_fmaf(e * sp, kProbScale, kNrBernOff0);
+    const float v = x * __builtin_amdgcn_logf(p1) + (1.f - x) * __builtin_amdgcn_logf(p0);
+    l2 += (f0 + i < S.N) ? v : 0.f;
+  }
+}
+template <int NSI, int NTB>
+__device__ __forceinline__ void nr_dense_bern_bin(NrCtx& C, const NrStage& S, const NrFrag& IN,
+                                                  unsigned (&W)[(NTB + 8) / 8], float& l2) {
+  constexpr int NW = (NTB + 8) / 8;
+  nr_f32x4 prev = {0.f, 0.f, 0.f, 0.f};
+  int t = 0;
+#pragma unroll 1
+  for (int m = 0; m < NTB / 8; ++m) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j, ++t) {
+      const __bf16* slot = nr_next(C);
+      const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
+      if (t > 0) nr_bern_bin(S, t - 1, prev, (W[0] >> (4 * j)) & 15u, l2);
+      prev = acc;
+    }
+#pragma unroll
+    for (int w = 0; w + 1 < NW; ++w) W[w] = W[w + 1];
+  }
+#pragma unroll
+  for (int j = 0; j < NTB % 8; ++j, ++t) {
+    const __bf16* slot = nr_next(C);
+    const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
+    if (t > 0) nr_bern_bin(S, t - 1, prev, (W[0] >> (4 * j)) & 15u, l2);
+    prev = acc;
+  }
+  nr_bern_bin(S, t - 1, prev, (W[0] >> (4 * (NTB % 8))) & 15u, l2);
+}
 template <int NSI>
-__device__ __forceinline__ void nr_dense_bern(NrCtx& C, const NrStage& S, const NrFrag& IN, unsigned px,
-                                              float& l2) {
-  const int g = (threadIdx.x & 63) >> 4;
+__device__ __forceinline__ void nr_dense_bern_frac(NrCtx& C, const NrStage& S, const NrFrag& IN, const float* px,
+                                                   float& l2) {
+  nr_f32x4 prev = {0.f, 0.f, 0.f, 0.f};
   for (int t = 0; t < S.ntile; ++t) {
     const __bf16* slot = nr_next(C);
     const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
-    const int f0 = 16 * t + 4 * g;
-    nr_f32x4 xq = nr_lds_rd4(px + 4u * (unsigned)f0);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xq));
-    const float4 xv = make_float4(xq[0], xq[1], xq[2], xq[3]);
-    const bool bin = (xv.x == 0.f || xv.x == 1.f) && (xv.y == 0.f || xv.y == 1.f) && (xv.z == 0.f || xv.z == 1.f) &&
-                     (xv.w == 0.f || xv.w == 1.f);
-    if (__all(bin)) {
-      float prod = 1.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float x = f4_at(xv, i);
-        const bool one = x != 0.f;
-        const float z = one ? acc[i] : -acc[i];
-        const float s = frcp(1.f + fexp(-z));
-        const float p = __builtin_fmaf(s, kProbScale, one ? kProbShift : kNrBernOff0);
-        prod *= (f0 + i < S.N) ? p : 1.f;
-      }
-      l2 += __builtin_amdgcn_logf(prod);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float x = f4_at(xv, i);
-        const float e = fexp(-acc[i]);
-        const float sp = frcp(1.f + e);
-        const float p1 = __builtin_fmaf(sp, kProbScale, kProbShift);
-        const float p0 = __builtin_fmaf(e * sp, kProbScale, kNrBernOff0);
-        const float v = x * __builtin_amdgcn_logf(p1) + (1.f - x) * __builtin_amdgcn_logf(p0);
-        l2 += (f0 + i < S.N) ? v : 0.f;
-      }
-    }
+    if (t > 0) nr_bern_frac(S, t - 1, prev, px, l2);
+    prev = acc;
   }
+  nr_bern_frac(S, S.ntile - 1, prev, px, l2);
 }
 
-// The step counts are compile-time (every register is addressed statically,
-// so only the fragments a stage really uses are live): H1 = k steps of h1
-// (d0 + 1), EH / PH / OH = of the encoder / prior / output hidden layers
-// (width + 1), H2 = of h2 (d1 + 1).  L2: two stochastic layers.
-template <int H1, int EH, int H2, int PH, int OH, bool L2, bool INJ>
+// Instantiated model shapes: k steps (of 32) of h1 (d0 + 1), of the encoder /
+// prior / output hidden layers (width + 1) and of h2 (d1 + 1), and column
+// tiles of the tanh layers and heads.
+struct NrShapeDef {
+  int L, H1, EH, NTE, NTEH, H2, PH, NTP, NTPH, OH, NTO, NTB;
+};
+constexpr NrShapeDef kNrShapes[] = {
+    {2, 4, 4, 7, 7, 2, 4, 7, 13, 7, 13, 49},     // 2L 784-200-200-100-100-50 (configs[1..4])
+    {1, 2, 0, 0, 0, 0, 0, 0, 0, 7, 13, 49},      // 1L 784-200-200-50 (configs[0])
+};
+constexpr int kNrNumShapes = sizeof(kNrShapes) / sizeof(kNrShapes[0]);
+
+// The shape is compile-time (every register is addressed statically, so only
+// the fragments a stage really uses are live).  INJ: injected noise.
+template <int SH, bool INJ>
 __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
+  constexpr NrShapeDef P = kNrShapes[SH];
+  constexpr bool L2 = P.L == 2;
+  constexpr int H1 = P.H1;
   constexpr int NT0 = 4 * H1;                        // h1 pair-layout tiles
   const int t = threadIdx.x, lane = t & 63, wave = nr_wave();
   const int r = lane & 15, g = lane >> 4;
@@ -416,57 +553,136 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
   const uint64_t base = A.rng_base ? *A.rng_base : 0ull;
   NR_TR(kNrMaxUnits - 1, 0)
   float* pix = nrs + NR_PIX_B / 4;                     // [2][NR_PIXLD] floats after the ring
-  // ---- pixels of the workgroup's (at most two) images into LDS
   const int img_a = row0 / A.kS;
+  // ---- every global load of the prologue is issued (and consumed) before the
+  // first DMA: a plain load in flight beside the ring would make hipcc drain it
+  // (1) the pixels of the workgroup's (at most two) images and the unit table
+  //     into LDS, the workgroup's "all pixels binary" flag
+  bool allbin;
   {
     const int last = min(row0 + NR_ROWS, A.rows) - 1;
     const int nimg = last / A.kS - img_a + 1;          // 1 or 2 (kS >= NR_ROWS)
-    for (int e = t; e < 2 * NR_PIXLD; e += NR_W * 64) {
+    constexpr int NPX = (2 * NR_PIXLD + NR_W * 64 - 1) / (NR_W * 64);
+    float pv[NPX];
+#pragma unroll
+    for (int i = 0; i < NPX; ++i) {
+      const int e = t + i * NR_W * 64;
       const int im = e / NR_PIXLD, c = e - im * NR_PIXLD;
-      pix[e] = (im < nimg && c < A.xdim) ? A.x[(size_t)(img_a + im) * A.ldx + c] : 0.f;
+      pv[i] = (e < 2 * NR_PIXLD && im < nimg && c < A.xdim) ? A.x[(size_t)(img_a + im) * A.ldx + c] : 0.f;
     }
-  }
-  // ---- the unit table into LDS (entries past the last unit: zero)
-  {
     unsigned* tab = reinterpret_cast<unsigned*>(nrs) + NR_TAB_B / 4;
-    for (int e = t; e < kNrMaxUnits; e += NR_W * 64) {
+    for (int e = t; e < kNrMaxUnits - 8; e += NR_W * 64) {
       const bool ok = e < A.nunits;
       tab[2 * e] = ok ? A.units[e].off : 0u;
       tab[2 * e + 1] = ok ? (unsigned)A.units[e].ns : 0u;
     }
+    bool bin = true;
+#pragma unroll
+    for (int i = 0; i < NPX; ++i) {
+      const int e = t + i * NR_W * 64;
+      if (e < 2 * NR_PIXLD) pix[e] = pv[i];
+      bin = bin && (pv[i] == 0.f || pv[i] == 1.f);
+    }
+    // workgroup AND of the waves' flags through the unit table's last entries
+    // (never read: the host keeps nunits + NR_D <= kNrMaxUnits - 8); this
+    // kernel declares no other LDS object (a second __shared__ object, e.g.
+    // __syncthreads_and's, would add static LDS beyond the 160 KiB dynamic one)
+    unsigned* flags = reinterpret_cast<unsigned*>(nrs) + NR_TAB_B / 4 + 2 * (kNrMaxUnits - 8);
+    const bool wbin = __all(bin);
+    if (lane == 0) flags[wave] = wbin ? 1u : 0u;
+    __syncthreads();                             // before the first DMA: a plain barrier
+    allbin = true;
+#pragma unroll
+    for (int w = 0; w < NR_W; ++w) allbin = allbin && flags[w] != 0u;
   }
-  // ---- prologue: h1 = eps * s0 + mu0 of the row's image in the pair layout,
-  // log q(h1 | x) (and log N(h1; 0, 1) for a one-layer model)
+  // (2) the row's image (mu, zs) in the h1 pair layout (lane group g of tile
+  //     t: columns 8t + 2g, + 1), materialized before the first DMA
+  constexpr int NTR0 = NT0;
+  float mu0[NTR0][2], zs0[NTR0][2];
+  {
+    const int d = A.d0;
+    const float* Pp = A.P0 + (size_t)(grow / A.kS) * A.ldP0;
+#pragma unroll
+    for (int tt = 0; tt < NTR0; ++tt)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int j = min(8 * tt + 2 * g + c, d - 1);
+        mu0[tt][c] = Pp[j];
+        zs0[tt][c] = Pp[d + j];
+      }
+#pragma unroll
+    for (int tt = 0; tt < NTR0; ++tt)
+      asm volatile("" : "+v"(mu0[tt][0]), "+v"(mu0[tt][1]), "+v"(zs0[tt][0]), "+v"(zs0[tt][1]));
+  }
+  // (3) injected noise (parity runs) the same way; Philox noise is drawn below
+  float2 ep1[NT0];
+  float2 ep2[L2 ? 4 * P.H2 : 1];
+  if (INJ) {
+    nr_noise_pairs(A, A.eps[0], 0, A.d0, 0ull, grow, ep1);
+    if constexpr (L2) nr_noise_pairs(A, A.eps[1], 1, A.st[2].d, 0ull, grow, ep2);
+#pragma unroll
+    for (int tt = 0; tt < NT0; ++tt) asm volatile("" : "+v"(ep1[tt].x), "+v"(ep1[tt].y));
+    if constexpr (L2) {
+#pragma unroll
+      for (int tt = 0; tt < 4 * P.H2; ++tt) asm volatile("" : "+v"(ep2[tt].x), "+v"(ep2[tt].y));
+    }
+  }
+  // pixel bits of this row's image in the Bernoulli epilogues' order: the
+  // epilogue of tile t (columns 16 t + 4 g .. + 3) runs in phase t + 1
+  unsigned pw[(P.NTB + 8) / 8];
+  {
+    const float* pr = pix + (grow / A.kS - img_a) * NR_PIXLD + 4 * g;
+#pragma unroll
+    for (int w = 0; w < (P.NTB + 8) / 8; ++w) {
+      unsigned b = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tt = 8 * w + j - 1;                  // the tile whose epilogue runs in phase 8 w + j
+        if (tt >= 0 && tt < P.NTB) {
+          const float4 xv = *reinterpret_cast<const float4*>(pr + 16 * tt);
+          b |= (xv.x != 0.f ? 1u : 0u) << (4 * j);
+          b |= (xv.y != 0.f ? 2u : 0u) << (4 * j);
+          b |= (xv.z != 0.f ? 4u : 0u) << (4 * j);
+          b |= (xv.w != 0.f ? 8u : 0u) << (4 * j);
+        }
+      }
+      pw[w] = b;
+      asm volatile("" : "+v"(pw[w]));            // built here, not sunk into the ring
+    }
+  }
+  NR_TR(kNrMaxUnits - 1, 1)
+  // ---- the ring: the first NR_D - NR_G units (whole groups); the Philox draws
+  // and the h1 sampling below overlap their flight
+  NrCtx C;
+  C.rh = buf_rsrc(A.fx_hi, A.fx_bytes);
+  C.rl = buf_rsrc(A.fx_lo, A.fx_bytes);
+  C.u = 0;
+  {
+    const unsigned* tab = reinterpret_cast<const unsigned*>(nrs) + NR_TAB_B / 4;
+#pragma unroll
+    for (int i = 0; i < NR_D - NR_G; ++i)
+      nr_issue(C, i, __builtin_amdgcn_readfirstlane(tab[2 * i]), (int)__builtin_amdgcn_readfirstlane(tab[2 * i + 1]));
+  }
+  if (!INJ) {
+    nr_noise_pairs(A, nullptr, 0, A.d0, base, grow, ep1);
+    if constexpr (L2) nr_noise_pairs(A, nullptr, 1, A.st[2].d, base, grow, ep2);
+  }
+  // ---- h1 = eps * s0 + mu0 of the row's image in the pair layout, log q(h1 | x)
+  // (and log N(h1; 0, 1) for a one-layer model)
   float lw = 0.f, l2 = 0.f;
   float2 hp1[NT0];
   {
     const int d = A.d0;
-    const float* Pp = A.P0 + (size_t)(grow / A.kS) * A.ldP0;
-    const float* ep = A.eps[0] ? A.eps[0] + ((size_t)(A.eps_s0 + grow % A.kS) * A.eps_N + (A.eps_i0 + grow / A.kS)) * d
-                               : nullptr;
-    float mu[NT0][2], zs[NT0][2], ev[NT0][2];
-#pragma unroll
-    for (int tt = 0; tt < NT0; ++tt)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int j = min(8 * tt + 2 * g + c, d - 1);
-        mu[tt][c] = Pp[j];
-        zs[tt][c] = Pp[d + j];
-        ev[tt][c] = ep ? ep[j] : 0.f;
-      }
 #pragma unroll
     for (int tt = 0; tt < NT0; ++tt) {
-      const int q = 2 * tt + (g >> 1);
       const int j0 = 8 * tt + 2 * g;
-      float2 e = make_float2(ev[tt][0], ev[tt][1]);
-      if (!ep) e = philox_normal2(A.seed, base, (unsigned)grow, 0u, (unsigned)q, (g & 1) != 0);
       float hv[2];
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int j = j0 + c;
-        const float sc = fexp(zs[tt][c]) + kScaleEps;
-        const float h = (c == 0 ? e.x : e.y) * sc + mu[tt][c];
-        float contrib = -nr_normal_logp(h, mu[tt][c], sc);
+        const float sc = fexp(zs0[tt][c]) + kScaleEps;
+        const float h = (c == 0 ? ep1[tt].x : ep1[tt].y) * sc + mu0[tt][c];
+        float contrib = -nr_normal_logp(h, mu0[tt][c], sc);
         if (!L2) contrib += -0.5f * (h * h) - kHalfLog2Pi;
         lw += j < d ? contrib : 0.f;
         hv[c] = j < d ? h : (j == d ? 1.f : 0.f);
@@ -474,35 +690,26 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
       hp1[tt] = make_float2(hv[0], hv[1]);
     }
   }
-  const unsigned px = NR_PIX_B + 4u * (unsigned)((grow / A.kS - img_a) * NR_PIXLD);   // this row's image
-  NR_TR(kNrMaxUnits - 1, 1)
-  // ---- the ring: the first NR_D - 1 units
-  NrCtx C;
-  C.rh = buf_rsrc(A.fx_hi, A.fx_bytes);
-  C.rl = buf_rsrc(A.fx_lo, A.fx_bytes);
-  C.u = 0;
-#pragma unroll
-  for (int i = 0; i < NR_D - 1; ++i) {
-    const int ns = i < A.nunits ? A.units[i].ns : 0;
-    nr_issue(C, i, i < A.nunits ? A.units[i].off : 0u, ns);
-  }
+  nr_keep(lw);
 
   NrFrag X, Y;
   if constexpr (L2) {
+    constexpr int EH = P.EH, H2 = P.H2, PH = P.PH;
     nr_pairs_to_frag<NT0, H1>(hp1, X);
-    nr_dense_tanh<H1, EH>(C, A.st[0], X, Y);
-    nr_dense_tanh<EH, EH>(C, A.st[1], Y, X);
+    nr_dense_tanh<H1, EH, P.NTE>(C, A.st[0], X, Y);
+    nr_dense_tanh<EH, EH, P.NTE>(C, A.st[1], Y, X);
     float2 hp2[4 * H2];
-    nr_head_sample<EH, 4 * H2, INJ>(C, A, A.st[2], X, hp2, base, grow, lw);
+    nr_head_sample<EH, P.NTEH, 4 * H2>(C, A.st[2], X, ep2, hp2, lw);
     nr_pairs_to_frag<4 * H2, H2>(hp2, X);
-    nr_dense_tanh<H2, PH>(C, A.st[3], X, Y);
-    nr_dense_tanh<PH, PH>(C, A.st[4], Y, X);
-    nr_head_prior<PH, NT0>(C, A.st[5], X, hp1, lw);
+    nr_dense_tanh<H2, PH, P.NTP>(C, A.st[3], X, Y);
+    nr_dense_tanh<PH, PH, P.NTP>(C, A.st[4], Y, X);
+    nr_head_prior<PH, P.NTPH, NT0>(C, A.st[5], X, hp1, lw);
   }
   nr_pairs_to_frag<NT0, H1>(hp1, X);
-  nr_dense_tanh<H1, OH>(C, A.st[6], X, Y);
-  nr_dense_tanh<OH, OH>(C, A.st[7], Y, X);
-  nr_dense_bern<OH>(C, A.st[8], X, px, l2);
+  nr_dense_tanh<H1, P.OH, P.NTO>(C, A.st[6], X, Y);
+  nr_dense_tanh<P.OH, P.OH, P.NTO>(C, A.st[7], Y, X);
+  if (allbin) nr_dense_bern_bin<P.OH, P.NTB>(C, A.st[8], X, pw, l2);
+  else nr_dense_bern_frac<P.OH>(C, A.st[8], X, pix + (grow / A.kS - img_a) * NR_PIXLD, l2);
   // the trailing (out-of-range) DMA pieces land before the workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // ---- log w of the row: sum over the four lane groups
@@ -514,49 +721,51 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
 
 size_t nring_lds_bytes() { return (size_t)NR_TAB_B + 8 * kNrMaxUnits; }
 
-// The instantiated shapes (k steps of h1, encoder hidden, h2, prior hidden,
-// output hidden): the 2L 784-200-200-100-100-50 family of configs[1..4] and
-// the 1L 784-200-200-50 of configs[0]; any other model runs mega_fwd_kernel.
-#define NR_SHAPES(X) X(4, 4, 2, 4, 7, true) X(2, 1, 1, 1, 7, false) X(4, 1, 1, 1, 7, false)
-
-bool nring_shape_ok(const NrLaunch& L) {
-  const int h1 = L.st[6].ns, oh = L.st[7].ns;
-  const int eh = L.L == 2 ? L.st[1].ns : 1, h2 = L.L == 2 ? L.st[3].ns : 1, ph = L.L == 2 ? L.st[4].ns : 1;
-#define NR_MATCH(a, b, c, d, e, l2) if (L.L == (l2 ? 2 : 1) && h1 == a && eh == b && h2 == c && ph == d && oh == e) return true;
-  NR_SHAPES(NR_MATCH)
-#undef NR_MATCH
-  return false;
+// host: the shape id of a plan (stage ns / ntile filled), or -1 (mega_fwd_kernel runs)
+static int nring_shape_id(const NrLaunch& L) {
+  for (int i = 0; i < kNrNumShapes; ++i) {
+    const NrShapeDef& P = kNrShapes[i];
+    if (L.L != P.L) continue;
+    bool ok = L.st[8].N == 16 * P.NTB && L.st[8].ntile == P.NTB && L.st[6].ns == P.H1 && L.st[6].ntile == P.NTO && L.st[6].next_ns == P.OH && L.st[7].ns == P.OH &&
+              L.st[7].ntile == P.NTO && L.st[7].next_ns == P.OH && L.st[8].ns == P.OH && 4 * P.H1 * 8 >= L.d0 + 1;
+    if (P.L == 2)
+      ok = ok && L.st[0].ns == P.H1 && L.st[0].ntile == P.NTE && L.st[0].next_ns == P.EH && L.st[1].ns == P.EH &&
+           L.st[1].ntile == P.NTE && L.st[1].next_ns == P.EH && L.st[2].ns == P.EH && L.st[2].ntile == P.NTEH &&
+           4 * P.H2 * 8 >= L.st[2].d + 1 && L.st[3].ns == P.H2 && L.st[3].ntile == P.NTP && L.st[3].next_ns == P.PH &&
+           L.st[4].ns == P.PH && L.st[4].ntile == P.NTP && L.st[4].next_ns == P.PH && L.st[5].ns == P.PH &&
+           L.st[5].ntile == P.NTPH && L.st[5].d == L.d0 && P.NTPH <= 4 * P.H1;
+    if (ok) return i;
+  }
+  return -1;
 }
+bool nring_shape_ok(const NrLaunch& L) { return nring_shape_id(L) >= 0; }
 
 hipError_t launch_nring(hipStream_t st, const NrLaunch& L) {
   if (L.rows <= 0) return hipSuccess;
   const dim3 grid((L.rows + NR_ROWS - 1) / NR_ROWS), block(NR_W * 64);
   const size_t lds = nring_lds_bytes();
-  const int h1 = L.st[6].ns, oh = L.st[7].ns;
-  const int eh = L.L == 2 ? L.st[1].ns : 1, h2 = L.L == 2 ? L.st[3].ns : 1, ph = L.L == 2 ? L.st[4].ns : 1;
-#define NR_LAUNCH(a, b, c, d, e, l2)                                                           \
-  if (L.L == (l2 ? 2 : 1) && h1 == a && eh == b && h2 == c && ph == d && oh == e) {             \
-    if (L.eps[0]) hipLaunchKernelGGL((nring_kernel<a, b, c, d, e, l2, true>), grid, block, lds, st, L);  \
-    else hipLaunchKernelGGL((nring_kernel<a, b, c, d, e, l2, false>), grid, block, lds, st, L);         \
-    return hipGetLastError();                                                                   \
+  const bool inj = L.eps[0] != nullptr;
+  switch (nring_shape_id(L)) {
+    case 0:
+      if (inj) hipLaunchKernelGGL((nring_kernel<0, true>), grid, block, lds, st, L);
+      else hipLaunchKernelGGL((nring_kernel<0, false>), grid, block, lds, st, L);
+      break;
+    case 1:
+      if (inj) hipLaunchKernelGGL((nring_kernel<1, true>), grid, block, lds, st, L);
+      else hipLaunchKernelGGL((nring_kernel<1, false>), grid, block, lds, st, L);
+      break;
+    default: return hipErrorInvalidValue;
   }
-  NR_SHAPES(NR_LAUNCH)
-#undef NR_LAUNCH
-  return hipErrorInvalidValue;
+  return hipGetLastError();
 }
 
 hipError_t nring_setup_attributes() {
-#define NR_ATTR(a, b, c, d, e, l2)                                                                     \
-  {                                                                                                    \
-    hipError_t err = hipFuncSetAttribute((const void*)nring_kernel<a, b, c, d, e, l2, false>,          \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);       \
-    if (err != hipSuccess) return err;                                                                 \
-    err = hipFuncSetAttribute((const void*)nring_kernel<a, b, c, d, e, l2, true>,                      \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                  \
-    if (err != hipSuccess) return err;                                                                 \
+  const void* fns[] = {(const void*)nring_kernel<0, false>, (const void*)nring_kernel<0, true>,
+                       (const void*)nring_kernel<1, false>, (const void*)nring_kernel<1, true>};
+  for (const void* f : fns) {
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
   }
-  NR_SHAPES(NR_ATTR)
-#undef NR_ATTR
   return hipSuccess;
 }
 
