@@ -130,7 +130,9 @@ enum iwae_knob {
   IWAE_KNOB_WIDE_ROWS = 18,    /* engine: 32 / 64-row workgroups from this many sample rows (4097) */
   IWAE_KNOB_DW_WIDE = 19,      /* beyond UPD_ROWS: weight gradients on the 112 x 256-block kernel (0) */
   IWAE_KNOB_LD_ALIGN = 20,     /* workspace row strides: multiples of 4, 8, 16 or 32 floats (4) */
-  IWAE_KNOB_NRING = 21         /* NLL: the weight-ring kernel where its model shapes apply (1) */
+  IWAE_KNOB_NRING = 21,        /* NLL: the weight-ring kernel where its model shapes apply (1) */
+  IWAE_KNOB_NRING_TRAIN = 22,  /* train-step forward on the weight-ring kernel (1) ... */
+  IWAE_KNOB_NRING_TRAIN_ROWS = 23  /* ... from this many sample rows (4096) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --
@@ -267,8 +269,8 @@ double iwae_workspace_bytes(const iwae_handle* h);
 /* Launch counters (tests): what = 0 fused k-sample NLL kernel (mega_fwd_kernel)
  * launches, 1 those of them fed injected noise, 2 train-engine (tc_kernel)
  * launches issued (a captured step counts once, at capture), 3 NLL chunks run
- * by the weight-ring kernel (nring_kernel, a subset of 0); -1 for an unknown
- * id. */
+ * by the weight-ring kernel (nring_kernel, a subset of 0), 4 train-step
+ * forwards run by it in train mode; -1 for an unknown id. */
 long long iwae_debug_count(const iwae_handle* h, int what);
 /* Live kernel timing: bracket every launch of one kernel class with HIP events
  * on the handle's stream -- a GEMM class (kind: 0 forward, 1 backward-data,

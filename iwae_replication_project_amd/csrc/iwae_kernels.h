@@ -511,6 +511,10 @@ struct NrStage {
   int ntile, ns, N;          // column tiles, k steps of the input, output features (heads: 8 * ceil(d / 4))
   int d, layer, stdnormal;   // head stages
   int next_ns;               // tanh stages: k steps of the reader (ones column at N, zeros up to it)
+  // train mode: the f32 stores (the train engine's TcOp fields of the same op)
+  float* out; int ld_out;    // tanh y, head (mu | zs), Bernoulli g
+  float* h; int ld_h;        // sampling head: h, eps
+  float* eps; int ld_eps;
 };
 struct NrLaunch {
   const __bf16* fx_hi; const __bf16* fx_lo; unsigned fx_bytes;
@@ -523,6 +527,12 @@ struct NrLaunch {
   uint64_t seed; const uint64_t* rng_base;
   const float* eps[8]; int eps_N, eps_i0, eps_s0; // injected noise (MgLaunch's convention) or null
   float* lw;                                      // out: log w per row
+  // train mode (the forward of a train step): h1 / eps1 stores, per-row log q,
+  // log p and the Bernoulli sum (bern[row * ld_bern]), g's weight wa
+  int train;
+  float* h1; int ld_h1; float* e1; int ld_e1;
+  float* logq; float* logp; float* bern; int ld_bern;
+  float wa;
 };
 bool nring_shape_ok(const NrLaunch& L);   // L, stage ns filled: an instantiated shape
 hipError_t launch_nring(hipStream_t st, const NrLaunch& L);

@@ -156,9 +156,12 @@ struct iwae_handle {
   int nll_fused = 1;                 // NLL: fused k-sample forward (mega_fwd_kernel) when it fits
   int mg_waves = 8;                  // mega_fwd_kernel workgroup: 8 waves (64 rows) or 4 (32 rows, 2 per CU)
   int nring = 1;                     // NLL: the weight-ring kernel (nring_kernel) where its shapes apply
+  int nring_train = 1;               // train-step forward on it (train mode) ...
+  long long nr_train_rows = 4096;    // ... from this many sample rows
   NrUnit* nr_units = nullptr;        // its unit table (device, built once: FX offsets are fixed per model)
   int nr_nunits = 0;
   long long n_nring = 0;             // nring_kernel launches, iwae_debug_count
+  long long n_nring_train = 0;       // ... of them train-step forwards
   bool masked = false;               // active-unit masks in force (iwae_nll_masked only)
   long long n_mega = 0, n_mega_eps = 0;  // mega_fwd_kernel launches (all / injected noise), iwae_debug_count
   long long n_tc = 0;                    // train-engine launches (tc_kernel), iwae_debug_count(h, 2)
@@ -2109,6 +2112,9 @@ static bool use_tc_bound(iwae_handle* h, const Plan& P) {
   return (long long)it->second.acc_off >= 64 + 8LL * r4(P.kS);
 }
 
+static bool nring_train_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool& ran);
+static bool nring_plan(iwae_handle* h, NrLaunch& R);
+
 static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
   // The first encoder layer's l2 / head: up to 32 images the few-row N-split
   // launches (one 16-column tile per workgroup; at B = 20 the image-row jobs,
@@ -2127,7 +2133,9 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   } else {
     CHK(enc0_forward(h, P));
   }
-  CHK(tc_run(h, P, E, 0));
+  bool ring = false;
+  if (!nring_train_forward(h, P, E, ring)) return fail(h, IWAE_EHIP, "weight-ring train forward launch failed");
+  if (!ring) CHK(tc_run(h, P, E, 0));
   if (use_tc_bound(h, P)) {
     const BoundArgs b = make_bound_args(h, P, true, -1.f, train_loss_ptr(h), adam, true);
     CHK(tc_run(h, P, E, 1, &b));
@@ -2264,6 +2272,8 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
     // fragment-major copies current before the step; the step itself refreshes them after its Adam
     CHK(ensure_fx(h));
     CHK(tc_prepare(h, P));
+    NrLaunch nr;                        // the ring kernel's unit table: allocated here, not inside a capture
+    (void)nring_plan(h, nr);
   }
   const bool direct = P.Bimg == P.B && (engine || use_fused(h, P)) && smallm_ok(h, P.Bimg);
   if (!direct) CHK(copy_x(h, P, x));
@@ -2592,6 +2602,8 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_WIDE_ROWS: h->wide_rows = std::max(0LL, value); break;
     case IWAE_KNOB_DW_WIDE: h->dw_wide = on; break;
     case IWAE_KNOB_NRING: h->nring = on; break;
+    case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
+    case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;
     case IWAE_KNOB_LD_ALIGN:
       if (value != 4 && value != 8 && value != 16 && value != 32)
         return fail(h, IWAE_EINVAL, "LD_ALIGN must be 4, 8, 16 or 32");
@@ -3015,6 +3027,46 @@ static bool nring_plan(iwae_handle* h, NrLaunch& R) {
   return true;
 }
 
+// The train step's forward (the engine's forward launch: job E and the output
+// job) on the weight-ring kernel in train mode: large batches (the engine's
+// 32 / 64-row workgroups re-stream their job's weights per tile of rows; here
+// 128 rows share one stream), the model shapes nring_kernel instantiates,
+// Philox or single-buffer injected noise, no Keras-BCE epilogue (L_alpha).
+// Writes what tc_run(which 0) writes.  False: run the engine's launch.
+static bool nring_train_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool& ran) {
+  ran = false;
+  const long long rows = (long long)P.Bimg * P.kS;
+  if (!h->nring_train || !h->x3 || rows < h->nr_train_rows || P.kS < 43 || P.need_bce || use_fold0(h, P) ||
+      P.Bsplit != P.Bimg)
+    return true;
+  if (E.a[0] && (h->L >= 2 && !E.a[1])) return true;
+  NrLaunch NR;
+  if (!nring_plan(h, NR)) return true;
+  if (ensure_fx(h) != IWAE_OK) return false;
+  const int L = h->L;
+  auto out = [](NrStage& S, const Mat& m) { S.out = m.p; S.ld_out = m.ld; };
+  if (L == 2) {
+    out(NR.st[0], h->eb[1].y1); out(NR.st[1], h->eb[1].y2); out(NR.st[2], h->eb[1].P);
+    NR.st[2].h = h->h[1].p; NR.st[2].ld_h = h->h[1].ld; NR.st[2].eps = h->eps_st[1].p; NR.st[2].ld_eps = h->eps_st[1].ld;
+    out(NR.st[3], h->db[0].y1); out(NR.st[4], h->db[0].y2); out(NR.st[5], h->db[0].P);
+  }
+  out(NR.st[6], h->ob.y1); out(NR.st[7], h->ob.y2); out(NR.st[8], h->ob.P);
+  NR.train = 1;
+  NR.h1 = h->h[0].p; NR.ld_h1 = h->h[0].ld; NR.e1 = h->eps_st[0].p; NR.ld_e1 = h->eps_st[0].ld;
+  NR.logq = h->logq; NR.logp = h->logp; NR.bern = h->ebern; NR.ld_bern = 4;
+  NR.wa = P.wa;
+  NR.rows = (int)rows; NR.kS = P.kS;
+  NR.P0 = h->eb[0].P.p; NR.ldP0 = h->eb[0].P.ld;
+  NR.x = h->x_in.p; NR.ldx = h->x_in.ld;
+  NR.seed = h->seed; NR.rng_base = &h->ds->rng[0];
+  for (int i = 0; i < 8; ++i) NR.eps[i] = i < L ? E.a[i] : nullptr;
+  NR.eps_N = P.Bimg; NR.eps_i0 = 0; NR.eps_s0 = 0;
+  if (launch_nring(h->stream, NR) != hipSuccess) return false;
+  ++h->n_nring_train;
+  ran = true;
+  return true;
+}
+
 // chunked k-sample NLL over N images; accumulates per-image (m, s)
 // eps (optional, parity): L buffers [k][N][d_i]; only the fused kernel takes
 // them chunk by chunk (the caller checks nll_mega_ok first)
@@ -3268,6 +3320,7 @@ long long iwae_debug_count(const iwae_handle* h, int what) {
     case 1: return h->n_mega_eps;
     case 2: return h->n_tc;
     case 3: return h->n_nring;
+    case 4: return h->n_nring_train;
     default: return -1;
   }
 }

@@ -59,6 +59,8 @@ static_assert(NR_G == 1 || NR_G == 2 || NR_G == 4, "NR_G");
 constexpr int NR_ROWS = 16 * NR_W;            // rows per workgroup
 constexpr int NR_SLOT_BF16 = 8 * 2 * 512;     // one slot: 8 k steps x (hi, lo) x 64 lanes x 8 bf16
 constexpr int NR_PIXLD = 800;                 // floats per image in the pixel cache (>= xdim <= 800)
+constexpr int NR_PIXIMG = 4;                  // images in the pixel cache: 128 rows span <= 4 at kS >= 43
+constexpr int NR_SEPI = 4;                    // train mode: stores per epilogue (real + out-of-range padding)
 
 extern __shared__ __attribute__((aligned(16))) float nrs[];
 
@@ -172,7 +174,17 @@ __device__ __forceinline__ void nr_pairs_to_frag(const float2 (&hp)[NT], NrFrag&
 // the ring, then the pixel cache [2][NR_PIXLD] floats, then the unit table
 // [kNrMaxUnits] (off, ns) pairs (zero past the last unit: ns 0 = no pieces)
 constexpr unsigned NR_PIX_B = NR_D * NR_SLOT_BF16 * 2;
-constexpr unsigned NR_TAB_B = NR_PIX_B + 2 * NR_PIXLD * 4;
+constexpr unsigned NR_TAB_B = NR_PIX_B + NR_PIXIMG * NR_PIXLD * 4;
+
+// a wave's row: its index, whether it exists, the log-density sums (natural
+// log q, log p; the Bernoulli sum in log2) and a resource that drops every
+// access (the train-mode store padding)
+struct NrRow {
+  int grow;
+  bool valid;
+  float q, p, l2;
+  __amdgpu_buffer_rsrc_t nul;
+};
 
 struct NrCtx {
   __amdgpu_buffer_rsrc_t rh, rl;     // FX hi / lo planes
@@ -205,7 +217,11 @@ __device__ __forceinline__ void nr_issue(const NrCtx& C, int slot, unsigned off,
 // one lets the compiler copy the register before the data has arrived.  (The
 // table and the pixel cache are read in asm, or plain with hipcc's own
 // vmcnt(0), because hipcc cannot tell them apart from the DMA-written slots.)
+template <bool TR>
 __device__ __forceinline__ const __bf16* nr_next(NrCtx& C) {
+  // younger than a group's pieces at its wait: the pieces of the two groups
+  // requested after it and (TR) the stores of the three groups since
+  constexpr int NV = 2 * (NR_D - 2 * NR_G) + (TR ? 3 * NR_G * NR_SEPI : 0);
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
   NR_TR(C.u, 0)
   if ((C.u & (NR_G - 1)) == 0) {
@@ -217,18 +233,18 @@ __device__ __forceinline__ const __bf16* nr_next(NrCtx& C) {
       asm volatile("ds_read_b64 %0, %4\n\tds_read_b64 %1, %4 offset:8\n\tds_read_b64 %2, %4 offset:16\n\t"
                    "ds_read_b64 %3, %4 offset:24\n\ts_waitcnt vmcnt(%5)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier"
                    : "=&v"(e0), "=&v"(e1), "=&v"(e2), "=&v"(e3)
-                   : "v"(ta), "n"(2 * (NR_D - 2 * NR_G))
+                   : "v"(ta), "n"(NV)
                    : "memory");
     else if (NR_G == 2)
       asm volatile("ds_read_b64 %0, %2\n\tds_read_b64 %1, %2 offset:8\n\ts_waitcnt vmcnt(%3)\n\t"
                    "s_waitcnt lgkmcnt(0)\n\ts_barrier"
                    : "=&v"(e0), "=&v"(e1)
-                   : "v"(ta), "n"(2 * (NR_D - 2 * NR_G))
+                   : "v"(ta), "n"(NV)
                    : "memory");
     else
       asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt vmcnt(%2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier"
                    : "=&v"(e0)
-                   : "v"(ta), "n"(2 * (NR_D - 2 * NR_G))
+                   : "v"(ta), "n"(NV)
                    : "memory");
     nr_issue(C, nu % NR_D, __builtin_amdgcn_readfirstlane(e0[0]), (int)__builtin_amdgcn_readfirstlane(e0[1]));
     if (NR_G >= 2)
@@ -237,6 +253,7 @@ __device__ __forceinline__ const __bf16* nr_next(NrCtx& C) {
       nr_issue(C, (nu + 2) % NR_D, __builtin_amdgcn_readfirstlane(e2[0]), (int)__builtin_amdgcn_readfirstlane(e2[1]));
       nr_issue(C, (nu + 3) % NR_D, __builtin_amdgcn_readfirstlane(e3[0]), (int)__builtin_amdgcn_readfirstlane(e3[1]));
     }
+    asm volatile("" ::: "memory");               // the phase's stores stay after the group's requests
   }
   NR_TR(C.u, 1)
   const __bf16* slot = reinterpret_cast<const __bf16*>(nrs) + (C.u % NR_D) * NR_SLOT_BF16;
@@ -289,24 +306,54 @@ __device__ __forceinline__ nr_f32x4 nr_mma(const __bf16* slot, const NrFrag& IN,
 // Every stage below is software-pipelined by one unit: in the phase of unit
 // t (after its barrier) the wave issues unit t's ds_reads and MFMAs and runs
 // the epilogue of unit t - 1, whose accumulator is complete, so the epilogue's
-// VALU work fills the MFMA gaps (and the other wave of the SIMD is never
-// left with all the MFMAs while this one is in its epilogue).  Tile counts
-// are compile-time, so the loops unroll and no branch splits a phase.
+// VALU work fills the MFMA gaps.  A stage's LAST epilogue runs in the next
+// stage's first phase, before that stage's MFMAs (it completes their input):
+// each stage takes the previous stage's pending epilogue (`pend`) and returns
+// its own.  So every phase runs exactly one epilogue, and in train mode
+// (TR: the forward of a train step, which stores its activations for the
+// backward) every epilogue issues exactly NR_SEPI stores (padded with
+// out-of-range ones): the ring's counted vmcnt needs a fixed number of vector
+// memory operations per group.  Tile counts are compile-time, so the loops
+// unroll and no branch splits a phase.
+
+// train-mode stores: buffer stores through a resource of the tensor, a row
+// past the launch or a column past the width (OOB offset) is dropped
+__device__ __forceinline__ void nr_st4(const float* base, unsigned off, const float (&v)[4]) {
+  const nr_u32x4 u = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+  __builtin_amdgcn_raw_buffer_store_b128(u, buf_rsrc(base), off, 0, 0);
+}
+__device__ __forceinline__ void nr_st2(const float* base, unsigned off, float a, float b) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 u = {__float_as_uint(a), __float_as_uint(b)};
+  __builtin_amdgcn_raw_buffer_store_b64(u, buf_rsrc(base), off, 0, 0);
+}
+// n out-of-range stores: they count in vmcnt like the real ones
+template <int NPAD>
+__device__ __forceinline__ void nr_st_pad(const NrRow& R) {
+#pragma unroll
+  for (int i = 0; i < NPAD; ++i) __builtin_amdgcn_raw_buffer_store_b32(0u, R.nul, kOOB, 0, 0);
+}
 
 // tanh Dense layer: OUT = [tanh(IN . W) | 1 | 0 ...] as the next layer's B
 // fragments (the ones column at feature N, zeros up to the reader's NSO k
-// steps).  NT column tiles (<= 2 NSO); the remaining tiles are the padding.
-template <int NSI, int NSO, int NT>
-__device__ __forceinline__ void nr_dense_tanh(NrCtx& C, const NrStage& S, const NrFrag& IN, NrFrag& OUT) {
+// steps); NT column tiles (<= 2 NSO), the rest is the padding.  TR: y stored.
+template <int NSI, int NSO, int NT, bool TR, class Pend>
+__device__ __forceinline__ auto nr_dense_tanh(NrCtx& C, const NrStage& S, const NrFrag& IN, NrFrag& OUT, NrRow& R,
+                                              Pend pend) {
   static_assert(NT <= 2 * NSO, "tiles beyond the reader's k steps");
   const int g = (threadIdx.x & 63) >> 4;
-  float va[4];
-  auto epi = [&](int t, const nr_f32x4& a, bool real) {
+  auto epi = [&S, &OUT, &R, g](int t, const nr_f32x4& a, float (&va)[4], bool real) {
     float v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = 16 * t + 4 * g + i;
-      v[i] = (real && f < S.N) ? nr_tanh(a[i]) : (f == S.N ? 1.f : 0.f);
+      // (train mode: the train engine's tanh, whose outputs the backward's TGRAD reads)
+      v[i] = (real && f < S.N) ? (TR ? ftanh(a[i]) : nr_tanh(a[i])) : (f == S.N ? 1.f : 0.f);
+    }
+    if (TR && real) {
+      const int f0 = 16 * t + 4 * g;
+      nr_st4(S.out, (R.valid && f0 < S.N) ? (unsigned)(R.grow * S.ld_out + f0) * 4u : kOOB, v);
+      nr_st_pad<NR_SEPI - 1>(R);
     }
     if (t & 1) {
       nr_pack(va, v, OUT.h[t >> 1], OUT.l[t >> 1]);
@@ -315,17 +362,21 @@ __device__ __forceinline__ void nr_dense_tanh(NrCtx& C, const NrStage& S, const 
       for (int i = 0; i < 4; ++i) va[i] = v[i];
     }
   };
+  float va[4] = {0.f, 0.f, 0.f, 0.f};
   nr_f32x4 prev = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const __bf16* slot = nr_next(C);
+    const __bf16* slot = nr_next<TR>(C);
+    if (t == 0) pend();
     const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
-    if (t > 0) epi(t - 1, prev, true);
+    if (t > 0) epi(t - 1, prev, va, true);
     prev = acc;
   }
-  epi(NT - 1, prev, true);
+  return [epi, prev, va]() mutable {
+    epi(NT - 1, prev, va, true);
 #pragma unroll
-  for (int t = NT; t < 2 * NSO; ++t) epi(t, prev, false);
+    for (int t = NT; t < 2 * NSO; ++t) epi(t, prev, va, false);
+  };
 }
 
 // head epilogue: (mu, zs) of the lane's two latent columns j0, j0 + 1
@@ -337,15 +388,16 @@ __device__ __forceinline__ void nr_head_pairs(const nr_f32x4& acc, float (&mu)[2
 }
 
 // sampling head (F:66-F:73): h = eps * (exp(zs) + 1e-6) + mu into hp (pair
-// layout; ones column at d; NT real tiles, padding tiles up to NP), lw +=
-// -log q(h) (+ log N(h; 0, 1) on the top layer).  ep: the noise pairs in
-// the same layout, drawn in the prologue (nr_noise_pairs).
-template <int NSI, int NT, int NP>
-__device__ __forceinline__ void nr_head_sample(NrCtx& C, const NrStage& S, const NrFrag& IN, const float2 (&ep)[NP],
-                                               float2 (&hp)[NP], float& lw) {
+// layout; ones column at d; NT real tiles, padding tiles up to NP), log q(h)
+// into R.q (+ log N(h; 0, 1) into R.p on the top layer).  ep: the noise
+// pairs in the same layout, drawn in the prologue (nr_noise_pairs).  TR: h,
+// eps, mu, zs stored (d even).
+template <int NSI, int NT, int NP, bool TR, class Pend>
+__device__ __forceinline__ auto nr_head_sample(NrCtx& C, const NrStage& S, const NrFrag& IN, const float2 (&ep)[NP],
+                                               float2 (&hp)[NP], NrRow& R, Pend pend) {
   const int g = (threadIdx.x & 63) >> 4;
-  const int d = S.d;
-  auto epi = [&](int t, const nr_f32x4& acc) {
+  auto epi = [&S, &ep, &hp, &R, g](int t, const nr_f32x4& acc) {
+    const int d = S.d;
     const int j0 = 8 * t + 2 * g;
     float mu[2], zs[2];
     nr_head_pairs(acc, mu, zs);
@@ -355,28 +407,39 @@ __device__ __forceinline__ void nr_head_sample(NrCtx& C, const NrStage& S, const
       const int j = j0 + c;
       const float sc = fexp(zs[c]) + kScaleEps;
       const float h = (c == 0 ? ep[t].x : ep[t].y) * sc + mu[c];
-      float contrib = -nr_normal_logp(h, mu[c], sc);
-      if (S.stdnormal) contrib += -0.5f * (h * h) - kHalfLog2Pi;
-      lw += j < d ? contrib : 0.f;
+      R.q += j < d ? nr_normal_logp(h, mu[c], sc) : 0.f;
+      if (S.stdnormal) R.p += j < d ? -0.5f * (h * h) - kHalfLog2Pi : 0.f;
       hv[c] = j < d ? h : (j == d ? 1.f : 0.f);
     }
     hp[t] = make_float2(hv[0], hv[1]);
+    if (TR) {
+      const bool ok = R.valid && j0 < d;
+      nr_st2(S.h, ok ? (unsigned)(R.grow * S.ld_h + j0) * 4u : kOOB, hv[0], hv[1]);
+      nr_st2(S.eps, ok ? (unsigned)(R.grow * S.ld_eps + j0) * 4u : kOOB, ep[t].x, ep[t].y);
+      nr_st2(S.out, ok ? (unsigned)(R.grow * S.ld_out + j0) * 4u : kOOB, mu[0], mu[1]);
+      nr_st2(S.out, ok ? (unsigned)(R.grow * S.ld_out + d + j0) * 4u : kOOB, zs[0], zs[1]);
+      nr_st_pad<NR_SEPI - 4>(R);
+    }
   };
   nr_f32x4 prev = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const __bf16* slot = nr_next(C);
+    const __bf16* slot = nr_next<TR>(C);
+    if (t == 0) pend();
     const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
     if (t > 0) epi(t - 1, prev);
     prev = acc;
   }
-  epi(NT - 1, prev);
-  nr_keep(lw);
+  return [epi, prev, &S, &hp, &R, g]() mutable {
+    epi(NT - 1, prev);
+    nr_keep(R.q);
+    nr_keep(R.p);
 #pragma unroll
-  for (int t = NT; t < NP; ++t) {
-    const int j0 = 8 * t + 2 * g;
-    hp[t] = make_float2(j0 == d ? 1.f : 0.f, j0 + 1 == d ? 1.f : 0.f);
-  }
+    for (int t = NT; t < NP; ++t) {
+      const int j0 = 8 * t + 2 * g;
+      hp[t] = make_float2(j0 == S.d ? 1.f : 0.f, j0 + 1 == S.d ? 1.f : 0.f);
+    }
+  };
 }
 
 // The noise of a row's latent layer in the head pair layout (lane group g of
@@ -418,14 +481,14 @@ __device__ __forceinline__ void nr_noise_pairs(const NrLaunch& A, const float* e
   }
 }
 
-// prior head (F:138-F:141): lw += log N(target; mu, exp(zs) + 1e-6) over the
-// target's pair layout (NT tiles)
-template <int NSI, int NT, int NP>
-__device__ __forceinline__ void nr_head_prior(NrCtx& C, const NrStage& S, const NrFrag& IN, const float2 (&tp)[NP],
-                                              float& lw) {
+// prior head (F:138-F:141): log N(target; mu, exp(zs) + 1e-6) into R.p over
+// the target's pair layout (NT tiles).  TR: mu, zs stored.
+template <int NSI, int NT, int NP, bool TR, class Pend>
+__device__ __forceinline__ auto nr_head_prior(NrCtx& C, const NrStage& S, const NrFrag& IN, const float2 (&tp)[NP],
+                                              NrRow& R, Pend pend) {
   const int g = (threadIdx.x & 63) >> 4;
-  const int d = S.d;
-  auto epi = [&](int t, const nr_f32x4& acc) {
+  auto epi = [&S, &tp, &R, g](int t, const nr_f32x4& acc) {
+    const int d = S.d;
     float mu[2], zs[2];
     nr_head_pairs(acc, mu, zs);
     const int j0 = 8 * t + 2 * g;
@@ -433,23 +496,33 @@ __device__ __forceinline__ void nr_head_prior(NrCtx& C, const NrStage& S, const 
     for (int c = 0; c < 2; ++c) {
       const float sc = fexp(zs[c]) + kScaleEps;
       const float v = nr_normal_logp(c == 0 ? tp[t].x : tp[t].y, mu[c], sc);
-      lw += j0 + c < d ? v : 0.f;
+      R.p += j0 + c < d ? v : 0.f;
+    }
+    if (TR) {
+      const bool ok = R.valid && j0 < d;
+      nr_st2(S.out, ok ? (unsigned)(R.grow * S.ld_out + j0) * 4u : kOOB, mu[0], mu[1]);
+      nr_st2(S.out, ok ? (unsigned)(R.grow * S.ld_out + d + j0) * 4u : kOOB, zs[0], zs[1]);
+      nr_st_pad<NR_SEPI - 2>(R);
     }
   };
   nr_f32x4 prev = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const __bf16* slot = nr_next(C);
+    const __bf16* slot = nr_next<TR>(C);
+    if (t == 0) pend();
     const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
     if (t > 0) epi(t - 1, prev);
     prev = acc;
   }
-  epi(NT - 1, prev);
-  nr_keep(lw);
+  return [epi, prev, &R]() mutable {
+    epi(NT - 1, prev);
+    nr_keep(R.p);
+  };
 }
 
 // Bernoulli output layer (F:123-F:129): log2 of the selected probabilities,
-// four multiplied before one log (mega_fwd_kernel's mg_bern).
+// four multiplied before one log (mega_fwd_kernel's mg_bern).  TR: also
+// g = wa * dlog p / dlogit stored for the backward (tc_bern's formula).
 // Binarized pixels (every pixel of the workgroup's images 0 or 1, the MNIST /
 // OMNIGLOT case) come from registers: seven words of pixel bits per lane,
 // made in the prologue in the order the pipelined epilogues consume them
@@ -459,21 +532,35 @@ __device__ __forceinline__ void nr_head_prior(NrCtx& C, const NrStage& S, const 
 // the DMA ring before each read: correct, slower; test inputs only).
 constexpr float kNrBernOff0 = 9.1327896e-7f;   // 1 - 0.999999f - 1e-7f (f32 constants, F:126)
 // (the shapes' output width is a whole number of tiles: no column mask)
-__device__ __forceinline__ void nr_bern_bin(const NrStage& S, int t, const nr_f32x4& acc, unsigned nib, float& l2) {
-  float prod = 1.f;
+template <bool TR>
+__device__ __forceinline__ void nr_bern_bin(const NrStage& S, int t, const nr_f32x4& acc, unsigned nib, NrRow& R,
+                                            float wa) {
+  float prod = 1.f, gv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const bool one = (nib >> i) & 1u;
     const float z = one ? acc[i] : -acc[i];
     const float s = frcp(1.f + fexp(-z));
-    prod *= __builtin_fmaf(s, kProbScale, one ? kProbShift : kNrBernOff0);
+    const float sel = __builtin_fmaf(s, kProbScale, one ? kProbShift : kNrBernOff0);
+    prod *= sel;
+    if (TR) {
+      const float dsg = kProbScale * (s * (1.f - s));
+      gv[i] = (one ? dsg : -dsg) * (wa * frcp(sel));
+    }
   }
-  l2 += __builtin_amdgcn_logf(prod);
+  R.l2 += __builtin_amdgcn_logf(prod);
+  if (TR) {
+    const int f0 = 16 * t + 4 * ((threadIdx.x & 63) >> 4);
+    nr_st4(S.out, R.valid ? (unsigned)(R.grow * S.ld_out + f0) * 4u : kOOB, gv);
+    nr_st_pad<NR_SEPI - 1>(R);
+  }
 }
-__device__ __forceinline__ void nr_bern_frac(const NrStage& S, int t, const nr_f32x4& acc, const float* px,
-                                             float& l2) {
+template <bool TR>
+__device__ __forceinline__ void nr_bern_frac(const NrStage& S, int t, const nr_f32x4& acc, const float* px, NrRow& R,
+                                             float wa) {
   const int f0 = 16 * t + 4 * ((threadIdx.x & 63) >> 4);
   const float4 xv = *reinterpret_cast<const float4*>(px + f0);
+  float gv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float x = f4_at(xv, i);
@@ -482,52 +569,67 @@ __device__ __forceinline__ void nr_bern_frac(const NrStage& S, int t, const nr_f
     const float p1 = __builtin_fmaf(sp, kProbScale, kProbShift);
     const float p0 = __builtin_fmaf(e * sp, kProbScale, kNrBernOff0);
     const float v = x * __builtin_amdgcn_logf(p1) + (1.f - x) * __builtin_amdgcn_logf(p0);
-    l2 += (f0 + i < S.N) ? v : 0.f;
+    R.l2 += (f0 + i < S.N) ? v : 0.f;
+    if (TR) gv[i] = (wa * (x * frcp(p1) - (1.f - x) * frcp(p0))) * (kProbScale * (sp * (1.f - sp)));
+  }
+  if (TR) {
+    nr_st4(S.out, (R.valid && f0 < S.N) ? (unsigned)(R.grow * S.ld_out + f0) * 4u : kOOB, gv);
+    nr_st_pad<NR_SEPI - 1>(R);
   }
 }
-template <int NSI, int NTB>
+template <int NSI, int NTB, bool TR, class Pend>
 __device__ __forceinline__ void nr_dense_bern_bin(NrCtx& C, const NrStage& S, const NrFrag& IN,
-                                                  unsigned (&W)[(NTB + 8) / 8], float& l2) {
+                                                  unsigned (&W)[(NTB + 8) / 8], NrRow& R, float wa, Pend pend) {
   constexpr int NW = (NTB + 8) / 8;
   nr_f32x4 prev = {0.f, 0.f, 0.f, 0.f};
   int t = 0;
+  {
+    const __bf16* slot = nr_next<TR>(C);
+    pend();
+    prev = nr_mma<NSI>(slot, IN, C.u - 1);
+    ++t;
+  }
 #pragma unroll 1
   for (int m = 0; m < NTB / 8; ++m) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j, ++t) {
-      const __bf16* slot = nr_next(C);
+    for (int j = 1; j < 9; ++j, ++t) {
+      if (j == 8 && m + 1 == NTB / 8 && NTB % 8 == 0) break;
+      const __bf16* slot = nr_next<TR>(C);
       const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
-      if (t > 0) nr_bern_bin(S, t - 1, prev, (W[0] >> (4 * j)) & 15u, l2);
+      nr_bern_bin<TR>(S, t - 1, prev, (W[0] >> (4 * (j & 7))) & 15u, R, wa);
       prev = acc;
-    }
+      if (j == 7) {
 #pragma unroll
-    for (int w = 0; w + 1 < NW; ++w) W[w] = W[w + 1];
+        for (int w = 0; w + 1 < NW; ++w) W[w] = W[w + 1];
+      }
+    }
   }
 #pragma unroll
-  for (int j = 0; j < NTB % 8; ++j, ++t) {
-    const __bf16* slot = nr_next(C);
+  for (int j = 1; j < NTB % 8; ++j, ++t) {
+    const __bf16* slot = nr_next<TR>(C);
     const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
-    if (t > 0) nr_bern_bin(S, t - 1, prev, (W[0] >> (4 * j)) & 15u, l2);
+    nr_bern_bin<TR>(S, t - 1, prev, (W[0] >> (4 * j)) & 15u, R, wa);
     prev = acc;
   }
-  nr_bern_bin(S, t - 1, prev, (W[0] >> (4 * (NTB % 8))) & 15u, l2);
+  nr_bern_bin<TR>(S, t - 1, prev, (W[0] >> (4 * (NTB % 8))) & 15u, R, wa);
 }
-template <int NSI>
+template <int NSI, bool TR, class Pend>
 __device__ __forceinline__ void nr_dense_bern_frac(NrCtx& C, const NrStage& S, const NrFrag& IN, const float* px,
-                                                   float& l2) {
+                                                   NrRow& R, float wa, Pend pend) {
   nr_f32x4 prev = {0.f, 0.f, 0.f, 0.f};
   for (int t = 0; t < S.ntile; ++t) {
-    const __bf16* slot = nr_next(C);
+    const __bf16* slot = nr_next<TR>(C);
+    if (t == 0) pend();
     const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
-    if (t > 0) nr_bern_frac(S, t - 1, prev, px, l2);
+    if (t > 0) nr_bern_frac<TR>(S, t - 1, prev, px, R, wa);
     prev = acc;
   }
-  nr_bern_frac(S, S.ntile - 1, prev, px, l2);
+  nr_bern_frac<TR>(S, S.ntile - 1, prev, px, R, wa);
 }
 
 // Instantiated model shapes: k steps (of 32) of h1 (d0 + 1), of the encoder /
 // prior / output hidden layers (width + 1) and of h2 (d1 + 1), and column
-// tiles of the tanh layers and heads.
+// tiles of the tanh layers, heads and the Bernoulli layer.
 struct NrShapeDef {
   int L, H1, EH, NTE, NTEH, H2, PH, NTP, NTPH, OH, NTO, NTB;
 };
@@ -538,8 +640,13 @@ constexpr NrShapeDef kNrShapes[] = {
 constexpr int kNrNumShapes = sizeof(kNrShapes) / sizeof(kNrShapes[0]);
 
 // The shape is compile-time (every register is addressed statically, so only
-// the fragments a stage really uses are live).  INJ: injected noise.
-template <int SH, bool INJ>
+// the fragments a stage really uses are live).  INJ: injected noise.  TR: the
+// forward of a train step (the train engine's job E and output job in one
+// launch): the activations the backward launches and the weight gradients
+// read are stored (h1 / eps1 in the prologue, every tanh output, the heads'
+// (mu | zs), h2 / eps2, the Bernoulli g), and per row log q, log p and the
+// Bernoulli sum instead of log w.
+template <int SH, bool INJ, bool TR>
 __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
   constexpr NrShapeDef P = kNrShapes[SH];
   constexpr bool L2 = P.L == 2;
@@ -548,27 +655,32 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
   const int t = threadIdx.x, lane = t & 63, wave = nr_wave();
   const int r = lane & 15, g = lane >> 4;
   const int row0 = blockIdx.x * NR_ROWS;
+  NrRow R;
   const int grow_raw = row0 + wave * 16 + r;
-  const int grow = min(grow_raw, A.rows - 1);
+  R.grow = min(grow_raw, A.rows - 1);
+  R.valid = grow_raw < A.rows;
+  R.q = 0.f; R.p = 0.f; R.l2 = 0.f;
+  R.nul = buf_rsrc(A.P0, 0u);
+  const int grow = R.grow;
   const uint64_t base = A.rng_base ? *A.rng_base : 0ull;
   NR_TR(kNrMaxUnits - 1, 0)
-  float* pix = nrs + NR_PIX_B / 4;                     // [2][NR_PIXLD] floats after the ring
+  float* pix = nrs + NR_PIX_B / 4;                     // [NR_PIXIMG][NR_PIXLD] floats after the ring
   const int img_a = row0 / A.kS;
   // ---- every global load of the prologue is issued (and consumed) before the
   // first DMA: a plain load in flight beside the ring would make hipcc drain it
-  // (1) the pixels of the workgroup's (at most two) images and the unit table
-  //     into LDS, the workgroup's "all pixels binary" flag
+  // (1) the pixels of the workgroup's images (kS >= 43: at most NR_PIXIMG)
+  //     and the unit table into LDS, the workgroup's "all pixels binary" flag
   bool allbin;
   {
     const int last = min(row0 + NR_ROWS, A.rows) - 1;
-    const int nimg = last / A.kS - img_a + 1;          // 1 or 2 (kS >= NR_ROWS)
-    constexpr int NPX = (2 * NR_PIXLD + NR_W * 64 - 1) / (NR_W * 64);
+    const int nimg = last / A.kS - img_a + 1;
+    constexpr int NPX = (NR_PIXIMG * NR_PIXLD + NR_W * 64 - 1) / (NR_W * 64);
     float pv[NPX];
 #pragma unroll
     for (int i = 0; i < NPX; ++i) {
       const int e = t + i * NR_W * 64;
       const int im = e / NR_PIXLD, c = e - im * NR_PIXLD;
-      pv[i] = (e < 2 * NR_PIXLD && im < nimg && c < A.xdim) ? A.x[(size_t)(img_a + im) * A.ldx + c] : 0.f;
+      pv[i] = (e < NR_PIXIMG * NR_PIXLD && im < nimg && c < A.xdim) ? A.x[(size_t)(img_a + im) * A.ldx + c] : 0.f;
     }
     unsigned* tab = reinterpret_cast<unsigned*>(nrs) + NR_TAB_B / 4;
     for (int e = t; e < kNrMaxUnits - 8; e += NR_W * 64) {
@@ -580,7 +692,7 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
 #pragma unroll
     for (int i = 0; i < NPX; ++i) {
       const int e = t + i * NR_W * 64;
-      if (e < 2 * NR_PIXLD) pix[e] = pv[i];
+      if (e < NR_PIXIMG * NR_PIXLD) pix[e] = pv[i];
       bin = bin && (pv[i] == 0.f || pv[i] == 1.f);
     }
     // workgroup AND of the waves' flags through the unit table's last entries
@@ -597,13 +709,12 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
   }
   // (2) the row's image (mu, zs) in the h1 pair layout (lane group g of tile
   //     t: columns 8t + 2g, + 1), materialized before the first DMA
-  constexpr int NTR0 = NT0;
-  float mu0[NTR0][2], zs0[NTR0][2];
+  float mu0[NT0][2], zs0[NT0][2];
   {
     const int d = A.d0;
     const float* Pp = A.P0 + (size_t)(grow / A.kS) * A.ldP0;
 #pragma unroll
-    for (int tt = 0; tt < NTR0; ++tt)
+    for (int tt = 0; tt < NT0; ++tt)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int j = min(8 * tt + 2 * g + c, d - 1);
@@ -611,10 +722,10 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
         zs0[tt][c] = Pp[d + j];
       }
 #pragma unroll
-    for (int tt = 0; tt < NTR0; ++tt)
+    for (int tt = 0; tt < NT0; ++tt)
       asm volatile("" : "+v"(mu0[tt][0]), "+v"(mu0[tt][1]), "+v"(zs0[tt][0]), "+v"(zs0[tt][1]));
   }
-  // (3) injected noise (parity runs) the same way; Philox noise is drawn below
+  // (3) the noise of h1 (and h2): injected (parity runs) or Philox
   float2 ep1[NT0];
   float2 ep2[L2 ? 4 * P.H2 : 1];
   if (INJ) {
@@ -626,6 +737,9 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
 #pragma unroll
       for (int tt = 0; tt < 4 * P.H2; ++tt) asm volatile("" : "+v"(ep2[tt].x), "+v"(ep2[tt].y));
     }
+  } else {
+    nr_noise_pairs(A, nullptr, 0, A.d0, base, grow, ep1);
+    if constexpr (L2) nr_noise_pairs(A, nullptr, 1, A.st[2].d, base, grow, ep2);
   }
   // pixel bits of this row's image in the Bernoulli epilogues' order: the
   // epilogue of tile t (columns 16 t + 4 g .. + 3) runs in phase t + 1
@@ -650,26 +764,8 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
       asm volatile("" : "+v"(pw[w]));            // built here, not sunk into the ring
     }
   }
-  NR_TR(kNrMaxUnits - 1, 1)
-  // ---- the ring: the first NR_D - NR_G units (whole groups); the Philox draws
-  // and the h1 sampling below overlap their flight
-  NrCtx C;
-  C.rh = buf_rsrc(A.fx_hi, A.fx_bytes);
-  C.rl = buf_rsrc(A.fx_lo, A.fx_bytes);
-  C.u = 0;
-  {
-    const unsigned* tab = reinterpret_cast<const unsigned*>(nrs) + NR_TAB_B / 4;
-#pragma unroll
-    for (int i = 0; i < NR_D - NR_G; ++i)
-      nr_issue(C, i, __builtin_amdgcn_readfirstlane(tab[2 * i]), (int)__builtin_amdgcn_readfirstlane(tab[2 * i + 1]));
-  }
-  if (!INJ) {
-    nr_noise_pairs(A, nullptr, 0, A.d0, base, grow, ep1);
-    if constexpr (L2) nr_noise_pairs(A, nullptr, 1, A.st[2].d, base, grow, ep2);
-  }
   // ---- h1 = eps * s0 + mu0 of the row's image in the pair layout, log q(h1 | x)
-  // (and log N(h1; 0, 1) for a one-layer model)
-  float lw = 0.f, l2 = 0.f;
+  // (and log N(h1; 0, 1) for a one-layer model); TR: h1, eps1 stored
   float2 hp1[NT0];
   {
     const int d = A.d0;
@@ -682,41 +778,91 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
         const int j = j0 + c;
         const float sc = fexp(zs0[tt][c]) + kScaleEps;
         const float h = (c == 0 ? ep1[tt].x : ep1[tt].y) * sc + mu0[tt][c];
-        float contrib = -nr_normal_logp(h, mu0[tt][c], sc);
-        if (!L2) contrib += -0.5f * (h * h) - kHalfLog2Pi;
-        lw += j < d ? contrib : 0.f;
+        R.q += j < d ? nr_normal_logp(h, mu0[tt][c], sc) : 0.f;
+        if (!L2) R.p += j < d ? -0.5f * (h * h) - kHalfLog2Pi : 0.f;
         hv[c] = j < d ? h : (j == d ? 1.f : 0.f);
       }
       hp1[tt] = make_float2(hv[0], hv[1]);
+      if (TR && 8 * tt < d) {
+        const bool ok = R.valid && j0 < d;
+        nr_st2(A.h1, ok ? (unsigned)(grow * A.ld_h1 + j0) * 4u : kOOB, hv[0], hv[1]);
+        nr_st2(A.e1, ok ? (unsigned)(grow * A.ld_e1 + j0) * 4u : kOOB, ep1[tt].x, ep1[tt].y);
+      }
     }
   }
-  nr_keep(lw);
-
+  nr_keep(R.q);
+  nr_keep(R.p);
+  NR_TR(kNrMaxUnits - 1, 1)
+  // ---- the ring: the first NR_D - NR_G units (whole groups).  TR: each group
+  // followed by the stores its phases would have issued (out of range), so
+  // the first waits count like every later one
+  NrCtx C;
+  C.rh = buf_rsrc(A.fx_hi, A.fx_bytes);
+  C.rl = buf_rsrc(A.fx_lo, A.fx_bytes);
+  C.u = 0;
+  {
+    const unsigned* tab = reinterpret_cast<const unsigned*>(nrs) + NR_TAB_B / 4;
+#pragma unroll
+    for (int i = 0; i < NR_D - NR_G; ++i) {
+      nr_issue(C, i, __builtin_amdgcn_readfirstlane(tab[2 * i]), (int)__builtin_amdgcn_readfirstlane(tab[2 * i + 1]));
+      if (TR && (i % NR_G) == NR_G - 1) {
+        asm volatile("" ::: "memory");
+        nr_st_pad<NR_G * NR_SEPI>(R);
+      }
+    }
+  }
   NrFrag X, Y;
   if constexpr (L2) {
     constexpr int EH = P.EH, H2 = P.H2, PH = P.PH;
-    nr_pairs_to_frag<NT0, H1>(hp1, X);
-    nr_dense_tanh<H1, EH, P.NTE>(C, A.st[0], X, Y);
-    nr_dense_tanh<EH, EH, P.NTE>(C, A.st[1], Y, X);
+    auto p0 = [&]() {
+      if (TR) nr_st_pad<NR_SEPI>(R);
+      nr_pairs_to_frag<NT0, H1>(hp1, X);
+    };
+    auto pe1 = nr_dense_tanh<H1, EH, P.NTE, TR>(C, A.st[0], X, Y, R, p0);
+    auto pe2 = nr_dense_tanh<EH, EH, P.NTE, TR>(C, A.st[1], Y, X, R, pe1);
     float2 hp2[4 * H2];
-    nr_head_sample<EH, P.NTEH, 4 * H2>(C, A.st[2], X, ep2, hp2, lw);
-    nr_pairs_to_frag<4 * H2, H2>(hp2, X);
-    nr_dense_tanh<H2, PH, P.NTP>(C, A.st[3], X, Y);
-    nr_dense_tanh<PH, PH, P.NTP>(C, A.st[4], Y, X);
-    nr_head_prior<PH, P.NTPH, NT0>(C, A.st[5], X, hp1, lw);
+    auto peh0 = nr_head_sample<EH, P.NTEH, 4 * H2, TR>(C, A.st[2], X, ep2, hp2, R, pe2);
+    auto peh = [&]() {
+      peh0();
+      nr_pairs_to_frag<4 * H2, H2>(hp2, X);
+    };
+    auto pp1 = nr_dense_tanh<H2, PH, P.NTP, TR>(C, A.st[3], X, Y, R, peh);
+    auto pp2 = nr_dense_tanh<PH, PH, P.NTP, TR>(C, A.st[4], Y, X, R, pp1);
+    auto pph0 = nr_head_prior<PH, P.NTPH, NT0, TR>(C, A.st[5], X, hp1, R, pp2);
+    auto pph = [&]() {
+      pph0();
+      nr_pairs_to_frag<NT0, H1>(hp1, X);
+    };
+    auto po1 = nr_dense_tanh<H1, P.OH, P.NTO, TR>(C, A.st[6], X, Y, R, pph);
+    auto po2 = nr_dense_tanh<P.OH, P.OH, P.NTO, TR>(C, A.st[7], Y, X, R, po1);
+    if (allbin) nr_dense_bern_bin<P.OH, P.NTB, TR>(C, A.st[8], X, pw, R, A.wa, po2);
+    else nr_dense_bern_frac<P.OH, TR>(C, A.st[8], X, pix + (grow / A.kS - img_a) * NR_PIXLD, R, A.wa, po2);
+  } else {
+    auto p0 = [&]() {
+      if (TR) nr_st_pad<NR_SEPI>(R);
+      nr_pairs_to_frag<NT0, H1>(hp1, X);
+    };
+    auto po1 = nr_dense_tanh<H1, P.OH, P.NTO, TR>(C, A.st[6], X, Y, R, p0);
+    auto po2 = nr_dense_tanh<P.OH, P.OH, P.NTO, TR>(C, A.st[7], Y, X, R, po1);
+    if (allbin) nr_dense_bern_bin<P.OH, P.NTB, TR>(C, A.st[8], X, pw, R, A.wa, po2);
+    else nr_dense_bern_frac<P.OH, TR>(C, A.st[8], X, pix + (grow / A.kS - img_a) * NR_PIXLD, R, A.wa, po2);
   }
-  nr_pairs_to_frag<NT0, H1>(hp1, X);
-  nr_dense_tanh<H1, P.OH, P.NTO>(C, A.st[6], X, Y);
-  nr_dense_tanh<P.OH, P.OH, P.NTO>(C, A.st[7], Y, X);
-  if (allbin) nr_dense_bern_bin<P.OH, P.NTB>(C, A.st[8], X, pw, l2);
-  else nr_dense_bern_frac<P.OH>(C, A.st[8], X, pix + (grow / A.kS - img_a) * NR_PIXLD, l2);
   // the trailing (out-of-range) DMA pieces land before the workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // ---- log w of the row: sum over the four lane groups
-  float v = lw + kLn2 * l2;
-  v += __shfl_xor(v, 16);
-  v += __shfl_xor(v, 32);
-  if (g == 0 && grow_raw < A.rows) A.lw[grow_raw] = v;
+  // ---- per row: sums over the four lane groups
+  float q = R.q, p = R.p, b = kLn2 * R.l2;
+  q += __shfl_xor(q, 16); q += __shfl_xor(q, 32);
+  p += __shfl_xor(p, 16); p += __shfl_xor(p, 32);
+  b += __shfl_xor(b, 16); b += __shfl_xor(b, 32);
+  if (g == 0 && R.valid) {
+    if (TR) {
+      A.logq[grow_raw] = q;
+      A.logp[grow_raw] = p;
+      A.bern[(size_t)grow_raw * A.ld_bern] = b;
+    } else {
+      A.lw[grow_raw] = (p + b) - q;          // log w = log p(h) + log p(x|h) - log q(h|x)
+    }
+  }
 }
 
 size_t nring_lds_bytes() { return (size_t)NR_TAB_B + 8 * kNrMaxUnits; }
@@ -726,50 +872,57 @@ static int nring_shape_id(const NrLaunch& L) {
   for (int i = 0; i < kNrNumShapes; ++i) {
     const NrShapeDef& P = kNrShapes[i];
     if (L.L != P.L) continue;
-    bool ok = L.st[8].N == 16 * P.NTB && L.st[8].ntile == P.NTB && L.st[6].ns == P.H1 && L.st[6].ntile == P.NTO && L.st[6].next_ns == P.OH && L.st[7].ns == P.OH &&
-              L.st[7].ntile == P.NTO && L.st[7].next_ns == P.OH && L.st[8].ns == P.OH && 4 * P.H1 * 8 >= L.d0 + 1;
+    bool ok = L.st[8].N == 16 * P.NTB && L.st[8].ntile == P.NTB && L.st[6].ns == P.H1 && L.st[6].ntile == P.NTO &&
+              L.st[6].next_ns == P.OH && L.st[7].ns == P.OH && L.st[7].ntile == P.NTO && L.st[7].next_ns == P.OH &&
+              L.st[8].ns == P.OH && 4 * P.H1 * 8 >= L.d0 + 1 && L.d0 % 2 == 0 && L.st[6].N % 4 == 0 &&
+              L.st[7].N % 4 == 0;
     if (P.L == 2)
       ok = ok && L.st[0].ns == P.H1 && L.st[0].ntile == P.NTE && L.st[0].next_ns == P.EH && L.st[1].ns == P.EH &&
            L.st[1].ntile == P.NTE && L.st[1].next_ns == P.EH && L.st[2].ns == P.EH && L.st[2].ntile == P.NTEH &&
-           4 * P.H2 * 8 >= L.st[2].d + 1 && L.st[3].ns == P.H2 && L.st[3].ntile == P.NTP && L.st[3].next_ns == P.PH &&
-           L.st[4].ns == P.PH && L.st[4].ntile == P.NTP && L.st[4].next_ns == P.PH && L.st[5].ns == P.PH &&
-           L.st[5].ntile == P.NTPH && L.st[5].d == L.d0 && P.NTPH <= 4 * P.H1;
+           4 * P.H2 * 8 >= L.st[2].d + 1 && L.st[2].d % 2 == 0 && L.st[3].ns == P.H2 && L.st[3].ntile == P.NTP &&
+           L.st[3].next_ns == P.PH && L.st[4].ns == P.PH && L.st[4].ntile == P.NTP && L.st[4].next_ns == P.PH &&
+           L.st[5].ns == P.PH && L.st[5].ntile == P.NTPH && L.st[5].d == L.d0 && P.NTPH <= 4 * P.H1 &&
+           L.st[0].N % 4 == 0 && L.st[1].N % 4 == 0 && L.st[3].N % 4 == 0 && L.st[4].N % 4 == 0;
     if (ok) return i;
   }
   return -1;
 }
 bool nring_shape_ok(const NrLaunch& L) { return nring_shape_id(L) >= 0; }
 
+#define NR_INSTANCES(X) X(0, false, false) X(0, true, false) X(0, false, true) X(0, true, true) \
+                        X(1, false, false) X(1, true, false) X(1, false, true) X(1, true, true)
+
 hipError_t launch_nring(hipStream_t st, const NrLaunch& L) {
   if (L.rows <= 0) return hipSuccess;
+  if (L.kS < 43) return hipErrorInvalidValue;          // the pixel cache holds NR_PIXIMG images
   const dim3 grid((L.rows + NR_ROWS - 1) / NR_ROWS), block(NR_W * 64);
   const size_t lds = nring_lds_bytes();
-  const bool inj = L.eps[0] != nullptr;
-  switch (nring_shape_id(L)) {
-    case 0:
-      if (inj) hipLaunchKernelGGL((nring_kernel<0, true>), grid, block, lds, st, L);
-      else hipLaunchKernelGGL((nring_kernel<0, false>), grid, block, lds, st, L);
-      break;
-    case 1:
-      if (inj) hipLaunchKernelGGL((nring_kernel<1, true>), grid, block, lds, st, L);
-      else hipLaunchKernelGGL((nring_kernel<1, false>), grid, block, lds, st, L);
-      break;
-    default: return hipErrorInvalidValue;
+  const bool inj = L.eps[0] != nullptr, tr = L.train != 0;
+  const int sh = nring_shape_id(L);
+#define NR_LAUNCH(s, i, t)                                                              \
+  if (sh == s && inj == i && tr == t) {                                                 \
+    hipLaunchKernelGGL((nring_kernel<s, i, t>), grid, block, lds, st, L);               \
+    return hipGetLastError();                                                           \
   }
-  return hipGetLastError();
+  NR_INSTANCES(NR_LAUNCH)
+#undef NR_LAUNCH
+  return hipErrorInvalidValue;
 }
 
 hipError_t nring_setup_attributes() {
-  const void* fns[] = {(const void*)nring_kernel<0, false>, (const void*)nring_kernel<0, true>,
-                       (const void*)nring_kernel<1, false>, (const void*)nring_kernel<1, true>};
-  for (const void* f : fns) {
-    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
+#define NR_ATTR(s, i, t)                                                                                     \
+  {                                                                                                          \
+    const hipError_t e = hipFuncSetAttribute((const void*)nring_kernel<s, i, t>,                             \
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);        \
+    if (e != hipSuccess) return e;                                                                           \
   }
+  NR_INSTANCES(NR_ATTR)
+#undef NR_ATTR
   return hipSuccess;
 }
 
 }  // namespace iwae
+
 
 #ifdef IWAE_NR_TRACE
 extern "C" int iwae_nr_trace_dump(unsigned long long* out, int cap) {

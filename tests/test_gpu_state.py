@@ -214,3 +214,37 @@ def test_dw_kernel_graph_replays_and_data_parallel_tail():
     np.testing.assert_allclose(lc, la, rtol=1e-6)
     assert np.linalg.norm(gc - ga) <= 1e-4 * np.linalg.norm(ga)
     assert np.abs(wc - wa).max() < 1e-5
+
+
+@pytest.mark.parametrize("B", [100, 512])
+@pytest.mark.parametrize("noise", ["injected", "philox"])
+def test_weight_ring_train_forward_matches_engine_forward(B, noise):
+    """Large batches: the train step's forward on the weight-ring kernel in
+    train mode (nring_kernel: 128 rows share one LDS weight stream; it writes
+    the activations, heads, h / eps, g and per-row log q / log p / Bernoulli
+    sums the engine's backward and the weight-gradient pass read) against the
+    engine's forward launch, same noise: loss, gradient and post-Adam weights
+    to bf16x3 summation order, over three steps with Philox noise (graph
+    replay) too.  Its launch counter proves the ring forward ran."""
+    rng = np.random.default_rng(68)
+    x = (rng.random((B, 784)) < 0.2).astype(np.float32)
+    eps = [rng.standard_normal((50, B, d)).astype(np.float32) for d in ARCH2[2]] if noise == "injected" else None
+    steps = 1 if eps else 3
+    la, ga, wa = _run_steps({"nring_train": 1}, x, eps, steps=steps)
+    lb, gb, wb = _run_steps({"nring_train": 0}, x, eps, steps=steps)
+    np.testing.assert_allclose(la, lb, rtol=1e-5)
+    assert np.linalg.norm(ga - gb) <= 5e-5 * np.linalg.norm(gb)
+    assert np.abs(wa - wb).max() <= 5e-5 * steps
+
+
+def test_weight_ring_train_forward_runs_at_large_batch_only():
+    """The ring forward runs from nring_train_rows sample rows (launch counter),
+    the engine's forward launch below."""
+    from iwae_replication_project_amd import Adam, Flexible_Model
+    rng = np.random.default_rng(69)
+    for B, want in ((20, False), (100, True)):
+        m = Flexible_Model(*ARCH2, dataset_bias=None, loss_function="IWAE", k=50, seed=5, use_graphs=False)
+        m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+        n0 = m._lib.iwae_debug_count(m._h, 4)
+        m.train_step((rng.random((B, 784)) < 0.2).astype(np.float32))
+        assert (m._lib.iwae_debug_count(m._h, 4) > n0) == want, B
