@@ -132,7 +132,11 @@ enum iwae_knob {
   IWAE_KNOB_LD_ALIGN = 20,     /* workspace row strides: multiples of 4, 8, 16 or 32 floats (4) */
   IWAE_KNOB_NRING = 21,        /* NLL: the weight-ring kernel where its model shapes apply (1) */
   IWAE_KNOB_NRING_TRAIN = 22,  /* train-step forward on the weight-ring kernel (1) ... */
-  IWAE_KNOB_NRING_TRAIN_ROWS = 23  /* ... from this many sample rows (4096) */
+  IWAE_KNOB_NRING_TRAIN_ROWS = 23, /* ... from this many sample rows (4096) */
+  IWAE_KNOB_NRING_BWD = 24,        /* ... and the output MLP's backward on the weight ring too: 0 off, 1 on the
+                                      step's stream, 2 on a side stream beside the engine's backward launch (2) */
+  IWAE_KNOB_WIDE_RT = 25           /* row tiles of 16 per workgroup of the engine's backward launches from
+                                      WIDE_ROWS: 1, 2 or 4 (2; the forward launch: 4) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --
@@ -270,7 +274,8 @@ double iwae_workspace_bytes(const iwae_handle* h);
  * launches, 1 those of them fed injected noise, 2 train-engine (tc_kernel)
  * launches issued (a captured step counts once, at capture), 3 NLL chunks run
  * by the weight-ring kernel (nring_kernel, a subset of 0), 4 train-step
- * forwards run by it in train mode; -1 for an unknown id. */
+ * forwards run by it in train mode, 5 train-step output-MLP backwards run by
+ * the weight-ring backward kernel (nrb_kernel); -1 for an unknown id. */
 long long iwae_debug_count(const iwae_handle* h, int what);
 /* Live kernel timing: bracket every launch of one kernel class with HIP events
  * on the handle's stream -- a GEMM class (kind: 0 forward, 1 backward-data,

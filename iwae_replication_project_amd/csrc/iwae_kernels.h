@@ -505,7 +505,7 @@ constexpr int NR_D = 8;
 constexpr int kNrMaxUnits = 512;
 struct NrUnit {
   unsigned off;              // FX byte offset of (column tile, k step 0), both planes
-  int ns;                    // k steps of 32 (<= 8)
+  int ns;                    // k steps of 32 (<= 8); nrb_kernel: pieces | piece stride KiB << 8
 };
 struct NrStage {
   int ntile, ns, N;          // column tiles, k steps of the input, output features (heads: 8 * ceil(d / 4))
@@ -538,6 +538,28 @@ bool nring_shape_ok(const NrLaunch& L);   // L, stage ns filled: an instantiated
 hipError_t launch_nring(hipStream_t st, const NrLaunch& L);
 hipError_t nring_setup_attributes();
 size_t nring_lds_bytes();
+
+// nrb_kernel (iwae_nring.hip): the output MLP's backward of a large-batch train
+// step (the train engine's job O': (dpx g) W3^T (1 - y2^2) -> W2^T (1 - y1^2)
+// -> W1^T) on 128-row workgroups sharing the GX weights through an LDS-DMA ring;
+// g is streamed by LDS-DMA beside the weights.  Units: NrUnit with
+// ns = pieces | piece stride in KiB << 8 (output-layer units: 8 column tiles
+// of one k step; the others: one column tile, its k steps).
+constexpr int kNrbMaxUnits = 128;
+struct NrbLaunch {
+  const __bf16* fx_hi; const __bf16* fx_lo; unsigned fx_bytes;
+  const NrUnit* units; int nunits;
+  int rows;
+  const float* g; int ld_g; int N;                // the Bernoulli layer's g (forward's store), width
+  const float* dpx;                               // dL/dlog p(x|h) per row (the bound's)
+  const float* y2; int ld_y2; const float* y1; int ld_y1;   // the output MLP's tanh outputs
+  float* dY2; int ld_dY2; float* dY1; int ld_dY1;           // their dZ (weight gradients); may be null
+  float* dh; int ld_dh;                           // dL/dh1 of the output MLP
+  int H, d1;                                      // hidden width, h1 width
+  int gx3_tiles, gx3_steps, gx2_tiles, gx2_steps, gx1_tiles, gx1_steps;   // shape check
+};
+bool nrb_shape_ok(const NrbLaunch& L);
+hipError_t launch_nrb(hipStream_t st, const NrbLaunch& L);
 
 // ---------------------------------------- row-chain train engine (bf16x3) ----
 // The small- and large-batch train step's per-sample-row work (everything

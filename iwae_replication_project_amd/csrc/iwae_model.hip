@@ -162,6 +162,12 @@ struct iwae_handle {
   int nr_nunits = 0;
   long long n_nring = 0;             // nring_kernel launches, iwae_debug_count
   long long n_nring_train = 0;       // ... of them train-step forwards
+  int nring_bwd = 2;                 // large-batch train step: the output MLP's backward on nrb_kernel
+                                     // (2: on the side stream beside the engine's backward launch)
+  int wide_rt = 2;                   // engine row tiles per workgroup of the backward launches from
+                                     // wide_rows (1, 2 or 4; the forward launch: 4)
+  NrUnit* nrb_units = nullptr;       // its unit table (device, built once)
+  long long n_nrb = 0;               // nrb_kernel launches, iwae_debug_count
   bool masked = false;               // active-unit masks in force (iwae_nll_masked only)
   long long n_mega = 0, n_mega_eps = 0;  // mega_fwd_kernel launches (all / injected noise), iwae_debug_count
   long long n_tc = 0;                    // train-engine launches (tc_kernel), iwae_debug_count(h, 2)
@@ -1740,7 +1746,7 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
   const int L = h->L, kS = P.kS;
   auto r32 = [](int x) { return (x + 31) & ~31; };
   // wide workgroups (32 / 64 sample rows, two-set weight pipeline) for large batches
-  const bool wide = (which <= 1 || which == 4) && (long long)P.Bimg * kS >= h->wide_rows;
+  const bool wide = (which <= 1 || which >= 4) && (long long)P.Bimg * kS >= h->wide_rows;
   std::vector<TcBuild> jobs;
   const bool fold0 = which == 0 && use_fold0(h, P);
   auto ldF = [&](int di) { return h->dense[di].ldF; };
@@ -1865,10 +1871,11 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
     // which 1: the backward launch.  which 4 (PIWAE's encoder pass): the same
     // chain run on the MIWAE weighting, storing only what the encoder's
     // backward reads (dL/dh, the encoder layers' dZ): the decoder layers' dZ
-    // of the IWAE pass stay for their weight gradients
-    const bool dec_out = which == 1;
+    // of the IWAE pass stay for their weight gradients.  which 5: which 1
+    // without job O' (nrb_kernel runs it)
+    const bool dec_out = which != 4;
     // job O': (dpx g) W3^T (1 - y2^2) -> W2^T (1 - y1^2) -> W1^T = dL/dh1 (output MLP part)
-    {
+    if (which != 5) {
       TcBuild B;
       TcOp& g = B.add(TC_LOADG);
       g.out_buf = 0; g.N = h->xdim; g.next_k = ldG(h->o3);
@@ -1940,7 +1947,7 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
   const int row_step = img ? (int)std::max<long long>(1, cdiv(P.Bimg, 256)) : 0;
   // rows per workgroup: 16 (four-set pipeline) below wide_rows, else the
   // widest the LDS allows (two-set pipeline)
-  const int want = wide ? 4 : h->tc_rt;
+  const int want = wide ? (which == 0 ? 4 : h->wide_rt) : h->tc_rt;
   iwae_handle::TcRec rec;
   for (int rt : {4, 2, 1}) {
     if (rt > want) continue;
@@ -2114,6 +2121,8 @@ static bool use_tc_bound(iwae_handle* h, const Plan& P) {
 
 static bool nring_train_forward(iwae_handle* h, const Plan& P, const EpsSet& E, bool& ran);
 static bool nring_plan(iwae_handle* h, NrLaunch& R);
+static bool nrb_plan(iwae_handle* h, NrbLaunch& R);
+static bool nring_train_backward(iwae_handle* h, const Plan& P, bool fwd_ring, bool& ran, hipStream_t st);
 
 static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
   // The first encoder layer's l2 / head: up to 32 images the few-row N-split
@@ -2141,7 +2150,24 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
     CHK(tc_run(h, P, E, 1, &b));
   } else {
     CHK(run_bound(h, P, true, -1.f, train_loss_ptr(h), adam, true));
-    CHK(tc_run(h, P, E, 1));
+    // the output MLP's backward on the weight ring where the forward ran on it,
+    // then the engine's launch without it (encoder and prior chains).  The two
+    // are independent (both read the bound's dL/dlw / dpx, the image-row job
+    // after them reads both): nring_bwd 2 runs the ring kernel on the side
+    // stream beside the engine's launch (each leaves CUs idle: 200 and 400
+    // workgroups), joined before the image-row job
+    const bool side = ring && h->nring_bwd == 2 && h->L >= 2;
+    if (side) {
+      HIPCHK(hipEventRecord(h->ev_fork, h->stream));
+      HIPCHK(hipStreamWaitEvent(h->side_stream, h->ev_fork, 0));
+    }
+    bool rb = false;
+    if (!nring_train_backward(h, P, ring, rb, side ? h->side_stream : h->stream))
+      return fail(h, IWAE_EHIP, "weight-ring backward launch failed");
+    if (side) HIPCHK(hipEventRecord(h->ev_join, h->side_stream));
+    if (!rb) CHK(tc_run(h, P, E, 1));
+    else if (h->L >= 2) CHK(tc_run(h, P, E, 5));
+    if (side) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
   }
   // PIWAE (PDF p7): the decoder's weight gradients come from IWAE_{k1 k2} (the
   // pass above stored their dZ), the encoder's from MIWAE(k1, k2): the
@@ -2272,8 +2298,9 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
     // fragment-major copies current before the step; the step itself refreshes them after its Adam
     CHK(ensure_fx(h));
     CHK(tc_prepare(h, P));
-    NrLaunch nr;                        // the ring kernel's unit table: allocated here, not inside a capture
-    (void)nring_plan(h, nr);
+    NrLaunch nr;                        // the ring kernels' unit tables: allocated here, not inside a capture
+    NrbLaunch nb;
+    if (nring_plan(h, nr) && nrb_plan(h, nb) && h->L >= 2) CHK(tc_prepare_one(h, P, 5));
   }
   const bool direct = P.Bimg == P.B && (engine || use_fused(h, P)) && smallm_ok(h, P.Bimg);
   if (!direct) CHK(copy_x(h, P, x));
@@ -2471,6 +2498,7 @@ void iwae_destroy(iwae_handle* h) {
   if (h->grad_own) (void)hipFree(h->grad_own);
   if (h->ds) (void)hipFree(h->ds);
   if (h->nr_units) (void)hipFree(h->nr_units);
+  if (h->nrb_units) (void)hipFree(h->nrb_units);
   if (h->wsplit_hi) (void)hipFree(h->wsplit_hi);
   if (h->fx_hi) (void)hipFree(h->fx_hi);
   if (h->prof_scratch) (void)hipFree(h->prof_scratch);
@@ -2604,6 +2632,8 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;
+    case IWAE_KNOB_NRING_BWD: h->nring_bwd = (int)std::min<long long>(std::max(0LL, value), 2); break;
+    case IWAE_KNOB_WIDE_RT: h->wide_rt = value >= 4 ? 4 : value <= 1 ? 1 : 2; break;
     case IWAE_KNOB_LD_ALIGN:
       if (value != 4 && value != 8 && value != 16 && value != 32)
         return fail(h, IWAE_EINVAL, "LD_ALIGN must be 4, 8, 16 or 32");
@@ -3067,6 +3097,66 @@ static bool nring_train_forward(iwae_handle* h, const Plan& P, const EpsSet& E, 
   return true;
 }
 
+// Plan of nrb_kernel (iwae_nring.hip): the GX units of the output MLP's
+// backward in consumption order -- per k step of GX(o3) its column tiles 0..7
+// and 8.. (one piece per tile, stride one tile's k steps), then GX(o2)'s and
+// GX(o1)'s column tiles (one unit each, their k steps).  False when the shape
+// is not instantiated (the engine's job O' runs instead).
+static bool nrb_plan(iwae_handle* h, NrbLaunch& R) {
+  std::memset(&R, 0, sizeof(R));
+  if (!h->nring_bwd || !h->x3) return false;
+  const DenseL& d3 = h->dense[h->o3];
+  const DenseL& d2 = h->dense[h->o2];
+  const DenseL& d1 = h->dense[h->o1];
+  R.gx3_tiles = d3.gx_tiles; R.gx3_steps = d3.gx_steps;
+  R.gx2_tiles = d2.gx_tiles; R.gx2_steps = d2.gx_steps;
+  R.gx1_tiles = d1.gx_tiles; R.gx1_steps = d1.gx_steps;
+  R.N = h->xdim; R.H = d2.fout; R.d1 = d1.fin;
+  if (d3.fin != R.H || d2.fin != R.H || d1.fout != R.H || d3.gx_tiles <= 8 || d3.gx_tiles > 16) return false;
+  std::vector<NrUnit> units;
+  auto piece = [](long long off_bf16) { return (unsigned)(off_bf16 * (long long)sizeof(__bf16)); };
+  for (int s = 0; s < d3.gx_steps; ++s) {
+    units.push_back(NrUnit{piece(d3.gx_off + (long long)s * 512), 8 | (d3.gx_steps << 8)});
+    units.push_back(NrUnit{piece(d3.gx_off + (8LL * d3.gx_steps + s) * 512), (d3.gx_tiles - 8) | (d3.gx_steps << 8)});
+  }
+  for (int t = 0; t < d2.gx_tiles; ++t)
+    units.push_back(NrUnit{piece(d2.gx_off + (long long)t * d2.gx_steps * 512), d2.gx_steps | (1 << 8)});
+  for (int t = 0; t < d1.gx_tiles; ++t)
+    units.push_back(NrUnit{piece(d1.gx_off + (long long)t * d1.gx_steps * 512), d1.gx_steps | (1 << 8)});
+  R.nunits = (int)units.size();
+  if (!nrb_shape_ok(R)) return false;
+  if (!h->nrb_units) {
+    if (hipMalloc(&h->nrb_units, kNrbMaxUnits * sizeof(NrUnit)) != hipSuccess) return false;
+    if (hipMemcpy(h->nrb_units, units.data(), units.size() * sizeof(NrUnit), hipMemcpyHostToDevice) != hipSuccess)
+      return false;
+  }
+  R.units = h->nrb_units;
+  R.fx_hi = h->fx_hi; R.fx_lo = h->fx_lo;
+  R.fx_bytes = (unsigned)(h->fx_elems * (long long)sizeof(__bf16));
+  return true;
+}
+
+// The output MLP's backward of a large-batch train step (the engine's job O')
+// on nrb_kernel, after the bound launch (dpx in HBM), when the forward ran on
+// the weight ring (its shapes; g, y1, y2 stored by it).  Writes what job O'
+// writes (ob.dY2, ob.dY1, dh_out[0]).  ran = false: the engine runs job O'.
+static bool nring_train_backward(iwae_handle* h, const Plan& P, bool fwd_ring, bool& ran, hipStream_t st) {
+  ran = false;
+  if (!fwd_ring || !h->nring_bwd) return true;
+  NrbLaunch NB;
+  if (!nrb_plan(h, NB)) return true;
+  NB.rows = P.Bimg * P.kS;
+  NB.g = h->ob.P.p; NB.ld_g = h->ob.P.ld;
+  NB.dpx = h->dpx;
+  NB.y2 = h->ob.y2.p; NB.ld_y2 = h->ob.y2.ld; NB.y1 = h->ob.y1.p; NB.ld_y1 = h->ob.y1.ld;
+  NB.dY2 = h->ob.dY2.p; NB.ld_dY2 = h->ob.dY2.ld; NB.dY1 = h->ob.dY1.p; NB.ld_dY1 = h->ob.dY1.ld;
+  NB.dh = h->dh_out[0].p; NB.ld_dh = h->dh_out[0].ld;
+  if (launch_nrb(st, NB) != hipSuccess) return false;
+  ++h->n_nrb;
+  ran = true;
+  return true;
+}
+
 // chunked k-sample NLL over N images; accumulates per-image (m, s)
 // eps (optional, parity): L buffers [k][N][d_i]; only the fused kernel takes
 // them chunk by chunk (the caller checks nll_mega_ok first)
@@ -3321,6 +3411,7 @@ long long iwae_debug_count(const iwae_handle* h, int what) {
     case 2: return h->n_tc;
     case 3: return h->n_nring;
     case 4: return h->n_nring_train;
+    case 5: return h->n_nrb;
     default: return -1;
   }
 }

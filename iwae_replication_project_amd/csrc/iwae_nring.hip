@@ -43,6 +43,8 @@
 // and one log weight per row, log p(h) + log p(x|h) - log q(h|x) (F:345-F:349).
 #include "iwae_kernels.h"
 
+#include <utility>
+
 namespace iwae {
 
 typedef float nr_f32x4 __attribute__((ext_vector_type(4)));
@@ -326,6 +328,15 @@ __device__ __forceinline__ void nr_st2(const float* base, unsigned off, float a,
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
   const u32x2 u = {__float_as_uint(a), __float_as_uint(b)};
   __builtin_amdgcn_raw_buffer_store_b64(u, buf_rsrc(base), off, 0, 0);
+}
+__device__ __forceinline__ void nr_st4r(__amdgpu_buffer_rsrc_t r, unsigned off, const float (&v)[4]) {
+  const nr_u32x4 u = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+  __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, 0);
+}
+__device__ __forceinline__ void nr_st2r(__amdgpu_buffer_rsrc_t r, unsigned off, float a, float b) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 u = {__float_as_uint(a), __float_as_uint(b)};
+  __builtin_amdgcn_raw_buffer_store_b64(u, r, off, 0, 0);
 }
 // n out-of-range stores: they count in vmcnt like the real ones
 template <int NPAD>
@@ -889,6 +900,388 @@ static int nring_shape_id(const NrLaunch& L) {
 }
 bool nring_shape_ok(const NrLaunch& L) { return nring_shape_id(L) >= 0; }
 
+// ===================================================================== backward
+// nrb_kernel: the output MLP's backward of a large-batch train step -- the
+// train engine's job O' (tc_kernel: LOADG -> TGRAD o3 -> TGRAD o2 -> LIN o1;
+// the tape through Decoder.call F:92-F:96 from the Bernoulli term
+// F:123-F:129) -- on nring_kernel's weight ring: 16 rows per wave, the 128
+// rows of a workgroup share the GX (backward) weight fragments through an
+// LDS-DMA ring.
+//   T3 (784 -> 200): the input dpx * g is 784 wide (25 k steps), too wide for
+//     registers, so it is streamed: one ring group per k step s = two units,
+//     the column tiles 0..7 and 8..12 of GX(o3) at step s (one piece per
+//     tile, stride one tile's k steps), and each wave's g of step s (its 16
+//     rows x 32 k = 2 KiB) by LDS-DMA into a 3-deep staging area.  The 13
+//     column tiles' accumulators stay in registers over the 25 steps.
+//   T3 epilogue: x (1 - y2^2) -> dY2 stored, packed as T2's B fragments.
+//   T2 (200 -> 200): one unit per column tile (7 k steps); epilogue x (1 - y1^2)
+//     -> dY1 stored, packed as T1's fragments.  T1 (200 -> d1): -> dL/dh1.
+// Per group every wave issues 2 g pieces and 2 pieces per unit (out of range
+// where there is nothing to fetch), so each group's counted vmcnt is a
+// compile-time constant: the operations younger than the group's pieces are
+// the next group's requests plus the stores / loads issued since (NrbCount).
+// y2 / y1 are plain loads issued in T3's group NS3 - 3 after its requests; they
+// have landed at the wait of group NS3 - 1, after which hipcc's own wait for
+// them (vmcnt(0)) only drains that group's requests.
+constexpr int NB_D = 6;                                   // ring slots (16 KiB)
+constexpr unsigned NB_G_B = NB_D * NR_SLOT_BF16 * 2;      // g staging: [3][8 waves][2 KiB]
+constexpr unsigned NB_TAB_B = NB_G_B + 3 * NR_W * 2048;   // unit table [kNrbMaxUnits] (off, ns)
+
+struct NrbShapeDef {
+  int NS3, NT3, NS2, NT2, NS1, NT1;   // k steps / column tiles of GX(o3), GX(o2), GX(o1)
+};
+constexpr NrbShapeDef kNrbShapes[] = {
+    {25, 13, 7, 13, 7, 7},    // 2L: 784 -> 200 -> 200 -> 100 (configs[1..4])
+    {25, 13, 7, 13, 7, 4},    // 1L: 784 -> 200 -> 200 -> 50 (configs[0])
+};
+constexpr int kNrbNumShapes = sizeof(kNrbShapes) / sizeof(kNrbShapes[0]);
+
+// vector memory operations per phase / group (units u = 0 .. UE - 1; unit U2
+// is T2's first, U1 T1's first).  A phase runs the epilogue of the unit
+// before it: phase U2 T3's (NT3 stores), phases U2 + 1 .. U1 T2's (one
+// each), the later ones T1's (two 8-byte stores each).  Group NS3 - 3 adds the
+// y2 / y1 loads.  nv(X): the count allowed at group X's wait -- everything
+// issued after group X's pieces were requested (at group X - 2): the rest of
+// group X - 2, group X - 1's 6 requests and its phases.
+template <int SH>
+struct NrbCount {
+  static constexpr NrbShapeDef P = kNrbShapes[SH];
+  static constexpr int U2 = 2 * P.NS3, U1 = U2 + P.NT2, UE = U1 + P.NT1;
+  static constexpr int stores(int u) { return u == U2 ? P.NT3 : (u > U2 && u <= U1) ? 1 : (u > U1 && u < UE) ? 2 : 0; }
+  static constexpr int post(int Y) {
+    return Y < 0 ? 0 : (Y == P.NS3 - 3 ? P.NT3 + P.NT2 : 0) + stores(2 * Y) + stores(2 * Y + 1);
+  }
+  static constexpr int nv(int X) { return post(X - 2) + 6 + post(X - 1); }
+};
+
+template <int B, class F, int... I>
+__device__ __forceinline__ void nrb_for_impl(F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, B + I>{}), ...);
+}
+// f(integral_constant<int, i>) for i = B .. E - 1, unrolled with i a constant expression
+template <int B, int E, class F>
+__device__ __forceinline__ void nrb_for(F&& f) {
+  nrb_for_impl<B>(f, std::make_integer_sequence<int, E - B>{});
+}
+
+// one unit's pieces: piece w = column tile / k step w of the unit, stride from the table
+__device__ __forceinline__ void nrb_issue(const NrCtx& C, int slot, unsigned off, unsigned nss) {
+  const int w = nr_wave(), lane = threadIdx.x & 63;
+  const int ns = (int)(nss & 255u);
+  const unsigned stride = (nss >> 8) * 1024u;
+  const unsigned voff = w < ns ? off + (unsigned)w * stride + (unsigned)lane * 16u : kOOB;
+  __bf16* dst = reinterpret_cast<__bf16*>(nrs) + slot * NR_SLOT_BF16 + w * 1024;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(C.rh, (nr_lds_void*)dst, 16, voff, 0, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(C.rl, (nr_lds_void*)(dst + 512), 16, voff, 0, 0, 0);
+}
+// this wave's g of k step s (lane l: row l & 15, k = 32 s + 8 (l >> 4) + 0..3
+// and + 4..7), lane-linear into staging (s % 3): two 1 KiB pieces
+__device__ __forceinline__ void nrb_issue_g(__amdgpu_buffer_rsrc_t rg, const NrbLaunch& A, int s, int grow,
+                                            bool valid) {
+  const int w = nr_wave(), lane = threadIdx.x & 63;
+  const int k0 = 32 * s + 8 * (lane >> 4);
+  const unsigned o = (unsigned)(grow * A.ld_g + k0) * 4u;
+  float* dst = nrs + NB_G_B / 4 + ((s % 3) * NR_W + w) * 512;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (nr_lds_void*)dst, 16, (valid && k0 + 4 <= A.N) ? o : kOOB, 0, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (nr_lds_void*)(dst + 256), 16, (valid && k0 + 8 <= A.N) ? o + 16u : kOOB,
+                                           0, 0, 0);
+}
+// group start at unit u (even): the counted wait + barrier (nr_next's); GR
+// (T3): then this wave's g of the group's k step from its staging slot --
+// read in the same asm statement (hipcc, which cannot tell the staging from
+// the DMA targets, would otherwise drain every DMA in flight before a plain
+// read); then the requests of group u / 2 + 2: its g, its two units
+template <int NV, bool GR>
+__device__ __forceinline__ void nrb_group(const NrCtx& C, int u, __amdgpu_buffer_rsrc_t rg, const NrbLaunch& A,
+                                          int grow, bool valid, nr_f32x4& ga, nr_f32x4& gb) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  static_assert(NV >= 0 && NV < 64, "vmcnt");
+  const int nu = u + NB_D - 2;
+  const unsigned ta = NB_TAB_B + 8u * (unsigned)nu;
+  u32x2 e0, e1;
+  if constexpr (GR) {
+    const unsigned gaddr = NB_G_B + (unsigned)((((u / 2) % 3) * NR_W + nr_wave()) * 2048 + (threadIdx.x & 63) * 16);
+    asm volatile("ds_read_b64 %0, %4\n\tds_read_b64 %1, %4 offset:8\n\ts_waitcnt vmcnt(%6)\n\t"
+                 "s_waitcnt lgkmcnt(0)\n\ts_barrier\n\tds_read_b128 %2, %5\n\tds_read_b128 %3, %5 offset:1024\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(e0), "=&v"(e1), "=&v"(ga), "=&v"(gb)
+                 : "v"(ta), "v"(gaddr), "n"(NV)
+                 : "memory");
+  } else {
+    asm volatile("ds_read_b64 %0, %2\n\tds_read_b64 %1, %2 offset:8\n\ts_waitcnt vmcnt(%3)\n\t"
+                 "s_waitcnt lgkmcnt(0)\n\ts_barrier"
+                 : "=&v"(e0), "=&v"(e1)
+                 : "v"(ta), "n"(NV)
+                 : "memory");
+  }
+  nrb_issue_g(rg, A, u / 2 + 2, grow, valid);
+  nrb_issue(C, nu % NB_D, __builtin_amdgcn_readfirstlane(e0[0]), __builtin_amdgcn_readfirstlane(e0[1]));
+  nrb_issue(C, (nu + 1) % NB_D, __builtin_amdgcn_readfirstlane(e1[0]), __builtin_amdgcn_readfirstlane(e1[1]));
+  asm volatile("" ::: "memory");               // the phase's stores / loads stay after the requests
+}
+__device__ __forceinline__ const __bf16* nrb_slot(int u) {
+  const __bf16* slot = reinterpret_cast<const __bf16*>(nrs) + (u % NB_D) * NR_SLOT_BF16;
+  __builtin_amdgcn_sched_barrier(0);
+  return slot;
+}
+// T3's B fragment of step s from the staged g (ga: k0 .. + 3, gb: k0 + 4 .. + 7):
+// dpx * g of this lane's row, split
+__device__ __forceinline__ void nrb_gfrag(const NrbLaunch& A, int s, float dp, bool valid, const nr_f32x4& ga,
+                                          const nr_f32x4& gb, nr_bf16x8& h, nr_bf16x8& l) {
+  const int k0 = 32 * s + 8 * ((threadIdx.x & 63) >> 4);
+  const bool oa = valid && k0 + 4 <= A.N, ob = valid && k0 + 8 <= A.N;   // (pieces not fetched hold stale data)
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = oa ? ga[i] * dp : 0.f;
+    v[4 + i] = ob ? gb[i] * dp : 0.f;
+  }
+  nr_split8(v, h, l);
+}
+constexpr int nrb_pair_tiles(int nj, int p) { return 2 * p + 2 <= nj ? 2 : (2 * p < nj ? 1 : 0); }
+// T3: acc[J0 + j] += GX(o3) tile (j of the unit) . B over one k step, NJ
+// tiles in pairs (two independent accumulators between dependent MFMAs),
+// the fragments of pair p + 2 read while pair p multiplies
+template <int NJ, int J0, int NA>
+__device__ __forceinline__ void nrb_mma_tiles(const __bf16* slot, const nr_bf16x8& bh, const nr_bf16x8& bl,
+                                              nr_f32x4 (&acc)[NA]) {
+  const int lane = threadIdx.x & 63;
+  constexpr int NPR = (NJ + 1) / 2;
+  nr_bf16x8 wh[NJ], wl[NJ];
+  auto rd = [&](int p) {
+#pragma unroll
+    for (int j = 2 * p; j < 2 * p + 2 && j < NJ; ++j) {
+      wh[j] = *reinterpret_cast<const nr_bf16x8*>(slot + j * 1024 + lane * 8);
+      wl[j] = *reinterpret_cast<const nr_bf16x8*>(slot + j * 1024 + 512 + lane * 8);
+    }
+  };
+  rd(0);
+  if (NPR > 1) rd(1);
+#pragma unroll
+  for (int p = 0; p < NPR; ++p) {
+    if (p + 2 < NPR) rd(p + 2);
+    const int ja = 2 * p, jb = 2 * p + 1;
+    acc[J0 + ja] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[ja], bh, acc[J0 + ja], 0, 0, 0);
+    if (jb < NJ) acc[J0 + jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[jb], bh, acc[J0 + jb], 0, 0, 0);
+    acc[J0 + ja] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[ja], bl, acc[J0 + ja], 0, 0, 0);
+    if (jb < NJ) acc[J0 + jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[jb], bl, acc[J0 + jb], 0, 0, 0);
+    acc[J0 + ja] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[ja], bh, acc[J0 + ja], 0, 0, 0);
+    if (jb < NJ) acc[J0 + jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[jb], bh, acc[J0 + jb], 0, 0, 0);
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, 2 * (nrb_pair_tiles(NJ, 0) + nrb_pair_tiles(NJ, 1)), 0);
+  nrb_for<0, NPR>([&](auto pc) {
+    constexpr int p = decltype(pc)::value;
+    __builtin_amdgcn_sched_group_barrier(0x008, 3 * nrb_pair_tiles(NJ, p), 0);
+    if constexpr (p + 2 < NPR) __builtin_amdgcn_sched_group_barrier(0x100, 2 * nrb_pair_tiles(NJ, p + 2), 0);
+  });
+}
+
+template <int SH>
+__global__ __launch_bounds__(NR_W * 64, 1) void nrb_kernel(NrbLaunch A) {
+  constexpr NrbShapeDef P = kNrbShapes[SH];
+  using CN = NrbCount<SH>;
+  constexpr int U2 = CN::U2, U1 = CN::U1;
+  static_assert(P.NT3 > 8 && P.NT3 <= 16 && P.NT3 <= 2 * P.NS2 && P.NT2 <= 2 * P.NS1 && P.NS2 <= 8 && P.NS1 <= 8,
+                "nrb shape");
+  static_assert(CN::UE + NB_D <= kNrbMaxUnits, "unit table");
+  const int t = threadIdx.x, lane = t & 63, wave = nr_wave();
+  const int g = lane >> 4;
+  const int grow_raw = blockIdx.x * NR_ROWS + wave * 16 + (lane & 15);
+  const bool valid = grow_raw < A.rows;
+  const int grow = min(grow_raw, A.rows - 1);
+  // ---- prologue: the unit table into LDS, the row's dpx and the first four
+  // units' entries -- plain loads, all consumed before the first DMA
+  unsigned* tab = reinterpret_cast<unsigned*>(nrs) + NB_TAB_B / 4;
+  for (int e = t; e < kNrbMaxUnits; e += NR_W * 64) {
+    const bool ok = e < A.nunits;
+    tab[2 * e] = ok ? A.units[e].off : 0u;
+    tab[2 * e + 1] = ok ? (unsigned)A.units[e].ns : 0u;
+  }
+  float dp = valid ? A.dpx[grow] : 0.f;
+  asm volatile("" : "+v"(dp));
+  unsigned u0[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bool ok = i < A.nunits;
+    u0[i][0] = __builtin_amdgcn_readfirstlane(ok ? A.units[i].off : 0u);
+    u0[i][1] = __builtin_amdgcn_readfirstlane(ok ? (unsigned)A.units[i].ns : 0u);
+    asm volatile("" : "+s"(u0[i][0]), "+s"(u0[i][1]));   // materialized before the first DMA
+  }
+  __syncthreads();                             // (the table; no DMA in flight yet)
+  NrCtx C;
+  C.rh = buf_rsrc(A.fx_hi, A.fx_bytes);
+  C.rl = buf_rsrc(A.fx_lo, A.fx_bytes);
+  C.u = 0;
+  const __amdgpu_buffer_rsrc_t rg = buf_rsrc(A.g);
+  // groups 0 and 1, in every group's order: g, then the two units
+  nrb_issue_g(rg, A, 0, grow, valid);
+  nrb_issue(C, 0, u0[0][0], u0[0][1]);
+  nrb_issue(C, 1, u0[1][0], u0[1][1]);
+  nrb_issue_g(rg, A, 1, grow, valid);
+  nrb_issue(C, 2, u0[2][0], u0[2][1]);
+  nrb_issue(C, 3, u0[3][0], u0[3][1]);
+  asm volatile("" ::: "memory");
+  const __amdgpu_buffer_rsrc_t nul = buf_rsrc(A.g, 0u);
+  const __amdgpu_buffer_rsrc_t rdy2 = A.dY2 ? buf_rsrc(A.dY2) : nul, rdy1 = A.dY1 ? buf_rsrc(A.dY1) : nul;
+  const __amdgpu_buffer_rsrc_t rdh = buf_rsrc(A.dh);
+  const int H = A.H;
+
+  // ---- T3
+  nr_f32x4 acc[P.NT3];
+#pragma unroll
+  for (int j = 0; j < P.NT3; ++j) acc[j] = (nr_f32x4){0.f, 0.f, 0.f, 0.f};
+  float4 y2v[P.NT3], y1v[P.NT2];
+  nrb_for<0, P.NS3>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    nr_f32x4 ga, gb;
+    nrb_group<CN::nv(s), true>(C, 2 * s, rg, A, grow, valid, ga, gb);
+    const __bf16* sa = nrb_slot(2 * s);
+    if constexpr (s == P.NS3 - 3) {
+      const __amdgpu_buffer_rsrc_t ry2 = buf_rsrc(A.y2), ry1 = buf_rsrc(A.y1);
+#pragma unroll
+      for (int j = 0; j < P.NT3; ++j) {
+        const int f0 = 16 * j + 4 * g;
+        y2v[j] = bld4(ry2, (valid && f0 < H) ? (unsigned)(grow * A.ld_y2 + f0) * 4u : kOOB);
+      }
+#pragma unroll
+      for (int j = 0; j < P.NT2; ++j) {
+        const int f0 = 16 * j + 4 * g;
+        y1v[j] = bld4(ry1, (valid && f0 < H) ? (unsigned)(grow * A.ld_y1 + f0) * 4u : kOOB);
+      }
+    }
+    nr_bf16x8 bh, bl;
+    nrb_gfrag(A, s, dp, valid, ga, gb, bh, bl);
+    nrb_mma_tiles<8, 0>(sa, bh, bl, acc);
+    const __bf16* sb = nrb_slot(2 * s + 1);
+    nrb_mma_tiles<P.NT3 - 8, 8>(sb, bh, bl, acc);
+  });
+
+  // ---- T2: epilogue of T3 first (its phase U2), then one unit per column tile
+  NrFrag X, Y;
+  auto pend3 = [&]() {
+#pragma unroll
+    for (int j = 0; j < P.NT3; j += 2) {
+      float v[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int jj = j + h;
+        const int f0 = 16 * jj + 4 * g;
+        if (jj < P.NT3) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float y = f4_at(y2v[jj], i);
+            v[h][i] = f0 + i < H ? acc[jj][i] * (1.f - y * y) : 0.f;
+          }
+          nr_st4r(rdy2, (valid && f0 < H) ? (unsigned)(grow * A.ld_dY2 + f0) * 4u : kOOB, v[h]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[h][i] = 0.f;
+        }
+      }
+      nr_pack(v[0], v[1], X.h[j >> 1], X.l[j >> 1]);
+    }
+  };
+  float va[4] = {0.f, 0.f, 0.f, 0.f};
+  auto epi2 = [&](int tt, const nr_f32x4& a) {
+    const int f0 = 16 * tt + 4 * g;
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float y = f4_at(y1v[tt], i);
+      v[i] = f0 + i < H ? a[i] * (1.f - y * y) : 0.f;
+    }
+    nr_st4r(rdy1, (valid && f0 < H) ? (unsigned)(grow * A.ld_dY1 + f0) * 4u : kOOB, v);
+    if (tt & 1) {
+      nr_pack(va, v, Y.h[tt >> 1], Y.l[tt >> 1]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) va[i] = v[i];
+    }
+  };
+  nr_f32x4 prev = {0.f, 0.f, 0.f, 0.f};
+  nrb_for<0, P.NT2>([&](auto tc) {
+    constexpr int tt = decltype(tc)::value;
+    constexpr int u = U2 + tt;
+    if constexpr (tt == 0) {
+      // y2 / y1 have landed (group U2 / 2 - 1's wait): hipcc's own wait for
+      // them (vmcnt(0), it does not see that one) here, before the next requests
+#pragma unroll
+      for (int j = 0; j < P.NT3; ++j) asm volatile("" ::"v"(y2v[j].x), "v"(y2v[j].y), "v"(y2v[j].z), "v"(y2v[j].w));
+#pragma unroll
+      for (int j = 0; j < P.NT2; ++j) asm volatile("" ::"v"(y1v[j].x), "v"(y1v[j].y), "v"(y1v[j].z), "v"(y1v[j].w));
+    }
+    nr_f32x4 ga, gb;
+    if constexpr ((u & 1) == 0) nrb_group<CN::nv(u / 2), false>(C, u, rg, A, grow, valid, ga, gb);
+    const __bf16* slot = nrb_slot(u);
+    if constexpr (tt == 0) pend3();
+    const nr_f32x4 a2 = nr_mma<P.NS2>(slot, X);
+    if constexpr (tt > 0) epi2(tt - 1, prev);
+    prev = a2;
+  });
+
+  // ---- T1 (LIN): dL/dh1, two 8-byte stores per tile (d1 even)
+  const int d1 = A.d1;
+  auto epi1 = [&](int tt, const nr_f32x4& a) {
+    const int f0 = 16 * tt + 4 * g;
+    const bool ok = valid && f0 < d1, ok2 = valid && f0 + 2 < d1;
+    nr_st2r(rdh, ok ? (unsigned)(grow * A.ld_dh + f0) * 4u : kOOB, a[0], a[1]);
+    nr_st2r(rdh, ok2 ? (unsigned)(grow * A.ld_dh + f0 + 2) * 4u : kOOB, a[2], a[3]);
+  };
+  nrb_for<0, P.NT1>([&](auto tc) {
+    constexpr int tt = decltype(tc)::value;
+    constexpr int u = U1 + tt;
+    nr_f32x4 ga, gb;
+    if constexpr ((u & 1) == 0) nrb_group<CN::nv(u / 2), false>(C, u, rg, A, grow, valid, ga, gb);
+    const __bf16* slot = nrb_slot(u);
+    if constexpr (tt == 0) {
+      epi2(P.NT2 - 1, prev);                   // T2's last tile, then the padding tile of its pair
+      if constexpr ((P.NT2 & 1) == 1) {
+        const float z[4] = {0.f, 0.f, 0.f, 0.f};
+        nr_pack(va, z, Y.h[P.NT2 >> 1], Y.l[P.NT2 >> 1]);
+      }
+    }
+    const nr_f32x4 a1 = nr_mma<P.NS1>(slot, Y);
+    if constexpr (tt > 0) epi1(tt - 1, prev);
+    prev = a1;
+  });
+  epi1(P.NT1 - 1, prev);
+  // the trailing (out-of-range) DMA pieces land before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+size_t nrb_lds_bytes() { return (size_t)NB_TAB_B + 8 * kNrbMaxUnits; }
+
+static int nrb_shape_id(const NrbLaunch& L) {
+  for (int i = 0; i < kNrbNumShapes; ++i) {
+    const NrbShapeDef& P = kNrbShapes[i];
+    if (L.gx3_steps == P.NS3 && L.gx3_tiles == P.NT3 && L.gx2_steps == P.NS2 && L.gx2_tiles == P.NT2 &&
+        L.gx1_steps == P.NS1 && L.gx1_tiles == P.NT1 && L.N % 4 == 0 && L.N <= 32 * P.NS3 && L.H % 4 == 0 &&
+        L.H <= 16 * P.NT3 && L.H <= 16 * P.NT2 && L.d1 % 2 == 0 && L.d1 <= 16 * P.NT1 && L.nunits <= kNrbMaxUnits)
+      return i;
+  }
+  return -1;
+}
+bool nrb_shape_ok(const NrbLaunch& L) { return nrb_shape_id(L) >= 0; }
+
+hipError_t launch_nrb(hipStream_t st, const NrbLaunch& L) {
+  if (L.rows <= 0) return hipSuccess;
+  const dim3 grid((L.rows + NR_ROWS - 1) / NR_ROWS), block(NR_W * 64);
+  switch (nrb_shape_id(L)) {
+    case 0: hipLaunchKernelGGL((nrb_kernel<0>), grid, block, nrb_lds_bytes(), st, L); break;
+    case 1: hipLaunchKernelGGL((nrb_kernel<1>), grid, block, nrb_lds_bytes(), st, L); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+static hipError_t nrb_setup_attributes() {
+  hipError_t e = hipFuncSetAttribute((const void*)nrb_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)nrb_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  return e;
+}
+
 #define NR_INSTANCES(X) X(0, false, false) X(0, true, false) X(0, false, true) X(0, true, true) \
                         X(1, false, false) X(1, true, false) X(1, false, true) X(1, true, true)
 
@@ -918,7 +1311,7 @@ hipError_t nring_setup_attributes() {
   }
   NR_INSTANCES(NR_ATTR)
 #undef NR_ATTR
-  return hipSuccess;
+  return nrb_setup_attributes();
 }
 
 }  // namespace iwae

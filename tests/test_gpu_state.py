@@ -237,6 +237,44 @@ def test_weight_ring_train_forward_matches_engine_forward(B, noise):
     assert np.abs(wa - wb).max() <= 5e-5 * steps
 
 
+@pytest.mark.parametrize("arch", ["2L", "1L"])
+@pytest.mark.parametrize("noise", ["injected", "philox"])
+def test_weight_ring_backward_matches_engine_backward(arch, noise):
+    """Large batches: the output MLP's backward (the engine's job O': dpx g
+    through W3^T, (1 - y2^2), W2^T, (1 - y1^2), W1^T) on the weight-ring
+    backward kernel (nrb_kernel: 128 rows share the GX weight stream, g
+    streamed by LDS-DMA beside it) against the engine's job O', both after the
+    ring forward, same noise: loss, gradient and post-Adam weights to bf16x3
+    summation order (three steps with Philox noise: graph replay).  The
+    launch counters prove both kernels ran; on the side stream beside the
+    engine's backward launch the results are the same bits; a 1-layer model
+    (no encoder / prior chain left for the engine's backward launch) too."""
+    from iwae_replication_project_amd import Adam, Flexible_Model
+    arch_def = ARCH2 if arch == "2L" else ([200], [200], [50], [784])
+    B = 100
+    rng = np.random.default_rng(70)
+    x = (rng.random((B, 784)) < 0.2).astype(np.float32)
+    eps = [rng.standard_normal((50, B, d)).astype(np.float32) for d in arch_def[2]] if noise == "injected" else None
+    steps = 1 if eps else 3
+
+    def run(tune):
+        m = Flexible_Model(*arch_def, dataset_bias=None, loss_function="IWAE", k=50, seed=13, tuning=tune)
+        m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+        c4, c5 = m._lib.iwae_debug_count(m._h, 4), m._lib.iwae_debug_count(m._h, 5)
+        losses = [m.train_step(x, eps=eps)["IWAE"] for _ in range(steps)]
+        ran = (m._lib.iwae_debug_count(m._h, 4) > c4, m._lib.iwae_debug_count(m._h, 5) > c5)
+        return losses, _flat(m.get_gradients()), _flat(m.get_weights()), ran
+
+    la, ga, wa, ra = run({"nring_bwd": 2})          # beside the engine's backward launch (side stream)
+    lc, gc, wc, rc = run({"nring_bwd": 1})          # before it, on the step's stream
+    lb, gb, wb, rb = run({"nring_bwd": 0})
+    assert ra == rc == (True, True) and rb == (True, False), (ra, rc, rb)
+    assert la == lc and np.array_equal(ga, gc) and np.array_equal(wa, wc)
+    np.testing.assert_allclose(la, lb, rtol=1e-5)
+    assert np.linalg.norm(ga - gb) <= 5e-5 * np.linalg.norm(gb)
+    assert np.abs(wa - wb).max() <= 5e-5 * steps
+
+
 def test_weight_ring_train_forward_runs_at_large_batch_only():
     """The ring forward runs from nring_train_rows sample rows (launch counter),
     the engine's forward launch below."""
