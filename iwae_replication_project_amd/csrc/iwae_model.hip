@@ -93,7 +93,7 @@ struct iwae_handle {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t side_stream = nullptr;   // second branch of a train step (the fused update's sample-row tiles)
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_mid = nullptr;   // side-stream fork / joins
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_mid = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
   iwae_config cfg{};
@@ -2144,7 +2144,6 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   }
   bool ring = false;
   if (!nring_train_forward(h, P, E, ring)) return fail(h, IWAE_EHIP, "weight-ring train forward launch failed");
-  bool side_grad = false;                      // the output MLP's weight-gradient pass on the side stream
   if (!ring) CHK(tc_run(h, P, E, 0));
   if (use_tc_bound(h, P)) {
     const BoundArgs b = make_bound_args(h, P, true, -1.f, train_loss_ptr(h), adam, true);
@@ -2166,14 +2165,10 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
     if (!nring_train_backward(h, P, ring, rb, side ? h->side_stream : h->stream))
       return fail(h, IWAE_EHIP, "weight-ring backward launch failed");
     if (side) HIPCHK(hipEventRecord(h->ev_join, h->side_stream));
-    // ... followed there by the output MLP's weight-gradient slab pass (its X and
-    // dZ are complete once the ring kernels ran), beside the engine's backward
-    // and image-row launches and the other layers' pass on the step's stream
-    side_grad = side && rb && use_update_slabs(h, P) && !h->dw_wide && !P.piwae;
-    if (side_grad) {
-      CHK(run_update(h, P, false, 1, h->side_stream, 1.f, nullptr, true));
-      HIPCHK(hipEventRecord(h->ev_mid, h->side_stream));
-    }
+    // (the output MLP's weight-gradient slab pass following it there, beside the
+    // other layers' pass on the step's stream, measured slower: 0.657-0.662 vs
+    // 0.613-0.621 ms at B = 512 -- the two passes, one workgroup per CU each,
+    // compete for the CUs)
     if (!rb) CHK(tc_run(h, P, E, 1));
     else if (h->L >= 2) CHK(tc_run(h, P, E, 5));
     if (side) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
@@ -2227,10 +2222,7 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
     return IWAE_OK;
   }
   if (use_update_slabs(h, P) && h->dw_wide) CHK(run_dw(h, P));
-  else if (side_grad) {
-    CHK(run_update(h, P, false, 2, nullptr, 1.f, nullptr, true));
-    HIPCHK(hipStreamWaitEvent(h->stream, h->ev_mid, 0));
-  } else if (use_update_slabs(h, P)) CHK(run_update(h, P, false, 0, nullptr, 1.f, nullptr, true));
+  else if (use_update_slabs(h, P)) CHK(run_update(h, P, false, 0, nullptr, 1.f, nullptr, true));
   else CHK(weight_grads(h, P, true, true, h->dpx));
   if (h->dp_weighted && adam && h->upd && upd_tiles_ok(h)) {
     // data parallel: the slabs summed into B_local * g (+ tail), the

