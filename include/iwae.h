@@ -134,7 +134,8 @@ enum iwae_knob {
   IWAE_KNOB_NRING_TRAIN = 22,  /* train-step forward on the weight-ring kernel (1) ... */
   IWAE_KNOB_NRING_TRAIN_ROWS = 23, /* ... from this many sample rows (4096) */
   IWAE_KNOB_NRING_BWD = 24,        /* ... and the output MLP's backward on the weight ring too: 0 off, 1 on the
-                                      step's stream, 2 on a side stream beside the engine's backward launch (2) */
+                                      step's stream, 2 on a side stream beside the engine's backward launch,
+                                      3 the encoder / prior backward on the ring as well (2-layer shape) (3) */
   IWAE_KNOB_WIDE_RT = 25           /* row tiles of 16 per workgroup of the engine's backward launches from
                                       WIDE_ROWS: 1, 2 or 4 (2; the forward launch: 4) */
 };
@@ -275,7 +276,8 @@ double iwae_workspace_bytes(const iwae_handle* h);
  * launches issued (a captured step counts once, at capture), 3 NLL chunks run
  * by the weight-ring kernel (nring_kernel, a subset of 0), 4 train-step
  * forwards run by it in train mode, 5 train-step output-MLP backwards run by
- * the weight-ring backward kernel (nrb_kernel); -1 for an unknown id. */
+ * the weight-ring backward kernel (nrb_kernel), 6 encoder / prior backwards
+ * run by nre_kernel; -1 for an unknown id. */
 long long iwae_debug_count(const iwae_handle* h, int what);
 /* Live kernel timing: bracket every launch of one kernel class with HIP events
  * on the handle's stream -- a GEMM class (kind: 0 forward, 1 backward-data,

@@ -561,6 +561,33 @@ struct NrbLaunch {
 bool nrb_shape_ok(const NrbLaunch& L);
 hipError_t launch_nrb(hipStream_t st, const NrbLaunch& L);
 
+// nre_kernel (iwae_nring.hip): the decoder prior's and the encoder's backward
+// of a large-batch 2-layer train step (the train engine's job E': prior
+// Gaussian backward -> ph^T (1 - y2^2) -> p2^T (1 - y1^2) -> p1^T = dL/dh2 of
+// the prior; encoder Gaussian backward of h2 -> eh^T -> e2^T -> e1^T = dL/dh1
+// of the encoder) on the weight ring, GX units of the six Dense layers (k steps
+// of one column tile each, nring_kernel's unit format) in that order.
+struct NreLaunch {
+  const __bf16* fx_hi; const __bf16* fx_lo; unsigned fx_bytes;
+  const NrUnit* units; int nunits;
+  int rows;
+  const float* dlw;                               // dL/dlog w per row (the bound's)
+  // prior of h1 given h2 (decoder layer 0): head (mu | zs), target h1, tanh outputs
+  const float* Pp; int ld_Pp; const float* h1; int ld_h1; int dp;
+  const float* py2; int ld_py2; const float* py1; int ld_py1; int Hp;
+  float* pdP; int ld_pdP; float* dh_prior; int ld_dh_prior;
+  float* pdY2; int ld_pdY2; float* pdY1; int ld_pdY1;
+  float* dh_dec; int ld_dh_dec;                   // dL/dh2 of the prior chain
+  // encoder layer 1 (h1 -> h2): head (mu | zs), h2, eps2, tanh outputs
+  const float* Pe; int ld_Pe; const float* h2; int ld_h2; const float* e2; int ld_e2; int de;
+  const float* ey2; int ld_ey2; const float* ey1; int ld_ey1; int He;
+  float* edP; int ld_edP; float* edY2; int ld_edY2; float* edY1; int ld_edY1;
+  float* dh_enc; int ld_dh_enc;                   // dL/dh1 of the encoder chain
+  int gx_tiles[6], gx_steps[6];                   // ph, p2, p1, eh, e2, e1 (shape check)
+};
+bool nre_shape_ok(const NreLaunch& L);
+hipError_t launch_nre(hipStream_t st, const NreLaunch& L);
+
 // ---------------------------------------- row-chain train engine (bf16x3) ----
 // The small- and large-batch train step's per-sample-row work (everything
 // after the first encoder layer, forward and backward) as chains of ops run by

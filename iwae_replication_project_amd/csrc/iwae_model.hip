@@ -162,11 +162,14 @@ struct iwae_handle {
   int nr_nunits = 0;
   long long n_nring = 0;             // nring_kernel launches, iwae_debug_count
   long long n_nring_train = 0;       // ... of them train-step forwards
-  int nring_bwd = 2;                 // large-batch train step: the output MLP's backward on nrb_kernel
-                                     // (2: on the side stream beside the engine's backward launch)
+  int nring_bwd = 3;                 // large-batch train step: the output MLP's backward on nrb_kernel
+                                     // (2: on the side stream beside the engine's backward launch;
+                                     // 3: then the encoder / prior backward on nre_kernel too)
   int wide_rt = 2;                   // engine row tiles per workgroup of the backward launches from
                                      // wide_rows (1, 2 or 4; the forward launch: 4)
   NrUnit* nrb_units = nullptr;       // its unit table (device, built once)
+  NrUnit* nre_units = nullptr;       // nre_kernel's (nring_bwd 3: the encoder / prior backward on the ring too)
+  long long n_nre = 0;
   long long n_nrb = 0;               // nrb_kernel launches, iwae_debug_count
   bool masked = false;               // active-unit masks in force (iwae_nll_masked only)
   long long n_mega = 0, n_mega_eps = 0;  // mega_fwd_kernel launches (all / injected noise), iwae_debug_count
@@ -2123,6 +2126,8 @@ static bool nring_train_forward(iwae_handle* h, const Plan& P, const EpsSet& E, 
 static bool nring_plan(iwae_handle* h, NrLaunch& R);
 static bool nrb_plan(iwae_handle* h, NrbLaunch& R);
 static bool nring_train_backward(iwae_handle* h, const Plan& P, bool fwd_ring, bool& ran, hipStream_t st);
+static bool nre_plan(iwae_handle* h, NreLaunch& R);
+static bool nring_train_backward_enc(iwae_handle* h, const Plan& P, bool& ran);
 
 static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
   // The first encoder layer's l2 / head: up to 32 images the few-row N-split
@@ -2169,8 +2174,14 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
     // other layers' pass on the step's stream, measured slower: 0.657-0.662 vs
     // 0.613-0.621 ms at B = 512 -- the two passes, one workgroup per CU each,
     // compete for the CUs)
-    if (!rb) CHK(tc_run(h, P, E, 1));
-    else if (h->L >= 2) CHK(tc_run(h, P, E, 5));
+    if (!rb) {
+      CHK(tc_run(h, P, E, 1));
+    } else if (h->L >= 2) {
+      // nring_bwd 3: the encoder / prior chains on the ring as well
+      bool re = false;
+      if (!nring_train_backward_enc(h, P, re)) return fail(h, IWAE_EHIP, "weight-ring encoder backward launch failed");
+      if (!re) CHK(tc_run(h, P, E, 5));
+    }
     if (side) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_join, 0));
   }
   // PIWAE (PDF p7): the decoder's weight gradients come from IWAE_{k1 k2} (the
@@ -2304,7 +2315,11 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
     CHK(tc_prepare(h, P));
     NrLaunch nr;                        // the ring kernels' unit tables: allocated here, not inside a capture
     NrbLaunch nb;
-    if (nring_plan(h, nr) && nrb_plan(h, nb) && h->L >= 2) CHK(tc_prepare_one(h, P, 5));
+    NreLaunch ne;
+    if (nring_plan(h, nr) && nrb_plan(h, nb) && h->L >= 2) {
+      CHK(tc_prepare_one(h, P, 5));
+      (void)nre_plan(h, ne);
+    }
   }
   const bool direct = P.Bimg == P.B && (engine || use_fused(h, P)) && smallm_ok(h, P.Bimg);
   if (!direct) CHK(copy_x(h, P, x));
@@ -2503,6 +2518,7 @@ void iwae_destroy(iwae_handle* h) {
   if (h->ds) (void)hipFree(h->ds);
   if (h->nr_units) (void)hipFree(h->nr_units);
   if (h->nrb_units) (void)hipFree(h->nrb_units);
+  if (h->nre_units) (void)hipFree(h->nre_units);
   if (h->wsplit_hi) (void)hipFree(h->wsplit_hi);
   if (h->fx_hi) (void)hipFree(h->fx_hi);
   if (h->prof_scratch) (void)hipFree(h->prof_scratch);
@@ -2636,7 +2652,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;
-    case IWAE_KNOB_NRING_BWD: h->nring_bwd = (int)std::min<long long>(std::max(0LL, value), 2); break;
+    case IWAE_KNOB_NRING_BWD: h->nring_bwd = (int)std::min<long long>(std::max(0LL, value), 3); break;
     case IWAE_KNOB_WIDE_RT: h->wide_rt = value >= 4 ? 4 : value <= 1 ? 1 : 2; break;
     case IWAE_KNOB_LD_ALIGN:
       if (value != 4 && value != 8 && value != 16 && value != 32)
@@ -3161,6 +3177,61 @@ static bool nring_train_backward(iwae_handle* h, const Plan& P, bool fwd_ring, b
   return true;
 }
 
+// Plan of nre_kernel (iwae_nring.hip): the GX units of the decoder prior's
+// head, l2, l1 and the encoder's second layer's head, l2, l1 (one column tile
+// each, its k steps).  2-layer paper shape only; false: the engine's job E'.
+static bool nre_plan(iwae_handle* h, NreLaunch& R) {
+  std::memset(&R, 0, sizeof(R));
+  if (h->nring_bwd != 3 || !h->x3 || h->L != 2) return false;
+  const int di[6] = {h->dec[0].head, h->dec[0].l2, h->dec[0].l1, h->enc[1].head, h->enc[1].l2, h->enc[1].l1};
+  std::vector<NrUnit> units;
+  for (int i = 0; i < 6; ++i) {
+    const DenseL& d = h->dense[di[i]];
+    R.gx_tiles[i] = d.gx_tiles; R.gx_steps[i] = d.gx_steps;
+    for (int t = 0; t < d.gx_tiles; ++t)
+      units.push_back(NrUnit{(unsigned)((d.gx_off + (long long)t * d.gx_steps * 512) * (long long)sizeof(__bf16)),
+                             d.gx_steps});
+  }
+  R.nunits = (int)units.size();
+  R.dp = h->dec[0].d; R.de = h->enc[1].d;
+  R.Hp = h->dense[h->dec[0].l2].fout; R.He = h->dense[h->enc[1].l2].fout;
+  if (!nre_shape_ok(R)) return false;
+  if (!h->nre_units) {
+    if (hipMalloc(&h->nre_units, kNrMaxUnits * sizeof(NrUnit)) != hipSuccess) return false;
+    if (hipMemcpy(h->nre_units, units.data(), units.size() * sizeof(NrUnit), hipMemcpyHostToDevice) != hipSuccess)
+      return false;
+  }
+  R.units = h->nre_units;
+  R.fx_hi = h->fx_hi; R.fx_lo = h->fx_lo;
+  R.fx_bytes = (unsigned)(h->fx_elems * (long long)sizeof(__bf16));
+  return true;
+}
+
+// The engine's job E' on nre_kernel (after nrb_kernel, which needs nothing of
+// it): writes what the engine's backward launch without job O' writes.
+static bool nring_train_backward_enc(iwae_handle* h, const Plan& P, bool& ran) {
+  ran = false;
+  NreLaunch R;
+  if (!nre_plan(h, R)) return true;
+  auto in = [](const Mat& m, const float*& p, int& ld) { p = m.p; ld = m.ld; };
+  auto out = [](const Mat& m, float*& p, int& ld) { p = m.p; ld = m.ld; };
+  R.rows = P.Bimg * P.kS;
+  R.dlw = h->dlw;
+  in(h->db[0].P, R.Pp, R.ld_Pp); in(h->h[0], R.h1, R.ld_h1);
+  in(h->db[0].y2, R.py2, R.ld_py2); in(h->db[0].y1, R.py1, R.ld_py1);
+  out(h->db[0].dP, R.pdP, R.ld_pdP); out(h->dh_prior[0], R.dh_prior, R.ld_dh_prior);
+  out(h->db[0].dY2, R.pdY2, R.ld_pdY2); out(h->db[0].dY1, R.pdY1, R.ld_pdY1);
+  out(h->dh_dec[1], R.dh_dec, R.ld_dh_dec);
+  in(h->eb[1].P, R.Pe, R.ld_Pe); in(h->h[1], R.h2, R.ld_h2); in(h->eps_st[1], R.e2, R.ld_e2);
+  in(h->eb[1].y2, R.ey2, R.ld_ey2); in(h->eb[1].y1, R.ey1, R.ld_ey1);
+  out(h->eb[1].dP, R.edP, R.ld_edP); out(h->eb[1].dY2, R.edY2, R.ld_edY2); out(h->eb[1].dY1, R.edY1, R.ld_edY1);
+  out(h->dh_enc[0], R.dh_enc, R.ld_dh_enc);
+  if (launch_nre(h->stream, R) != hipSuccess) return false;
+  ++h->n_nre;
+  ran = true;
+  return true;
+}
+
 // chunked k-sample NLL over N images; accumulates per-image (m, s)
 // eps (optional, parity): L buffers [k][N][d_i]; only the fused kernel takes
 // them chunk by chunk (the caller checks nll_mega_ok first)
@@ -3416,6 +3487,7 @@ long long iwae_debug_count(const iwae_handle* h, int what) {
     case 3: return h->n_nring;
     case 4: return h->n_nring_train;
     case 5: return h->n_nrb;
+    case 6: return h->n_nre;
     default: return -1;
   }
 }

@@ -1274,11 +1274,327 @@ hipError_t launch_nrb(hipStream_t st, const NrbLaunch& L) {
   return hipGetLastError();
 }
 
+
+
+// ========================================================= encoder / prior backward
+// nre_kernel: the rest of a large-batch 2-layer step's backward -- the train
+// engine's job E' (tc_kernel: GBWD_PRIOR -> TGRAD ph -> TGRAD p2 -> LIN p1,
+// GBWD_ENC -> TGRAD eh -> TGRAD e2 -> LIN e1; the tape through the decoder
+// prior F:138-F:141 and the encoder's second stochastic layer F:66-F:73,
+// reparameterised) -- on nring_kernel's weight ring (GX units, 16 rows per
+// wave, 128 rows per workgroup).
+//   P1 (prologue, before the ring starts): the prior head's Gaussian backward
+//     on dP's MFMA C layout (lane group g of tile t: features 16t + 4g .. + 3
+//     of (dmu | dzs)), dP and dL/dh1 stored, packed as ph^T's B fragments.
+//   ring phase A: ph^T (1 - y2^2), p2^T (1 - y1^2), p1^T -> dL/dh2 (kept in
+//     registers too).
+//   drain (every DMA and store), then E1: the encoder head's Gaussian backward
+//     of h2; its dL/dh2 source (p1^T's output) is re-laid out through LDS in
+//     phase A's last two slots, which the ring refills only at phase B's first
+//     group.
+//   ring phase B: eh^T, e2^T, e1^T -> dL/dh1.
+// Plain loads only where no DMA is in flight (P1, E1, the tanh outputs y of
+// each phase, read before its ring requests); every ring epilogue issues
+// NR_SEPI stores, so nr_next's counted waits hold unchanged.
+struct NreShapeDef {
+  int NSPH, NTPH, NSP2, NTP2, NSP1, NTP1, NSEH, NTEH, NSE2, NTE2, NSE1, NTE1;
+};
+constexpr NreShapeDef kNreShape = {7, 7, 4, 7, 4, 4, 4, 7, 4, 7, 4, 7};   // 2L 784-200-200-100-100-50
+
+// backward Dense stage (nr_dense_tanh's pipelining): v = acc (1 - y^2) (TG, y
+// of the lane's four features in registers) or acc; stored (N % 4 == 0, or
+// the padding columns get zeros), packed into OUT's NSO k steps, kept in C
+// layout (KEEP)
+template <int NSI, int NT, int NSO, bool TG, bool KEEP, int NY, class Pend>
+__device__ __forceinline__ auto nre_dense(NrCtx& C, const NrFrag& IN, NrFrag& OUT, const float4 (&yv)[NY], float* out,
+                                          int ld_out, int N, const NrRow& R, float (&kp)[NT][4], Pend pend) {
+  static_assert(!TG || NY >= NT, "y tiles");
+  static_assert(NSO == 0 || NT <= 2 * NSO, "tiles beyond the reader's k steps");
+  const int g = (threadIdx.x & 63) >> 4;
+  auto epi = [&OUT, &yv, &R, &kp, out, ld_out, N, g](int t, const nr_f32x4& a, float (&va)[4], bool real) {
+    const int f0 = 16 * t + 4 * g;
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float x = a[i];
+      if constexpr (TG) {
+        if (real) {
+          const float y = f4_at(yv[t < NY ? t : 0], i);
+          x = x * (1.f - y * y);
+        }
+      }
+      v[i] = (real && f0 + i < N) ? x : 0.f;
+    }
+    if (real) {
+      nr_st4(out, (R.valid && f0 < N) ? (unsigned)(R.grow * ld_out + f0) * 4u : kOOB, v);
+      nr_st_pad<NR_SEPI - 1>(R);
+      if constexpr (KEEP) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) kp[t < NT ? t : 0][i] = v[i];
+      }
+    }
+    if constexpr (NSO > 0) {
+      if (t & 1) {
+        nr_pack(va, v, OUT.h[t >> 1], OUT.l[t >> 1]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) va[i] = v[i];
+      }
+    }
+  };
+  float va[4] = {0.f, 0.f, 0.f, 0.f};
+  nr_f32x4 prev = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const __bf16* slot = nr_next<true>(C);
+    if (t == 0) pend();
+    const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
+    if (t > 0) epi(t - 1, prev, va, true);
+    prev = acc;
+  }
+  return [epi, prev, va]() mutable {
+    epi(NT - 1, prev, va, true);
+#pragma unroll
+    for (int t = NT; t < 2 * NSO; ++t) epi(t, prev, va, false);
+  };
+}
+
+// P1: the prior head's Gaussian backward (tc_gbwd<GBWD_PRIOR>'s arithmetic)
+// on dP's C layout, d % 4 == 0 (a lane's quad is all dmu or all dzs):
+// dmu = dl z / s, dzs = dl (z^2 - 1) / s e^zs, dL/dh1 = -dl z / s; NT tiles
+// of 2d features, packed into X's NSO k steps.  Loads in batches of NB tiles,
+// all issued before the batch's stores (hipcc keeps a load after a store it
+// cannot prove disjoint).
+template <int NT, int NSO, int NB>
+__device__ __forceinline__ void nre_gbwd_prior(const NreLaunch& A, const NrRow& R, float dl, NrFrag& X) {
+  const int g = (threadIdx.x & 63) >> 4, d = A.dp;
+  const __amdgpu_buffer_rsrc_t rp = buf_rsrc(A.Pp), rh = buf_rsrc(A.h1);
+  float va[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t0 = 0; t0 < 2 * NSO; t0 += NB) {
+    float4 mu[NB], zs[NB], hv[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int t = t0 + b, f0 = 16 * t + 4 * g;
+      const bool mu_part = f0 < d, ok = t < NT && R.valid && f0 < 2 * d;
+      const int c0 = mu_part ? f0 : f0 - d;
+      mu[b] = bld4(rp, ok ? (unsigned)(R.grow * A.ld_Pp + c0) * 4u : kOOB);
+      zs[b] = bld4(rp, ok ? (unsigned)(R.grow * A.ld_Pp + d + c0) * 4u : kOOB);
+      hv[b] = bld4(rh, ok ? (unsigned)(R.grow * A.ld_h1 + c0) * 4u : kOOB);
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int t = t0 + b, f0 = 16 * t + 4 * g;
+      if (t >= 2 * NSO) break;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (t < NT) {
+        const bool mu_part = f0 < d, ok = R.valid && f0 < 2 * d;
+        float dh[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float ez = fexp(f4_at(zs[b], i));
+          const float rs = frcp(ez + kScaleEps);
+          const float z = f4_at(hv[b], i) * rs - f4_at(mu[b], i) * rs;
+          dh[i] = dl * (-z * rs);
+          const float x = mu_part ? dl * (z * rs) : (dl * ((z * z - 1.f) * rs)) * ez;
+          v[i] = ok ? x : 0.f;
+        }
+        nr_st4(A.pdP, ok ? (unsigned)(R.grow * A.ld_pdP + f0) * 4u : kOOB, v);
+        nr_st4(A.dh_prior, (ok && mu_part) ? (unsigned)(R.grow * A.ld_dh_prior + f0) * 4u : kOOB, dh);
+      }
+      if (t & 1) {
+        nr_pack(va, v, X.h[t >> 1], X.l[t >> 1]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) va[i] = v[i];
+      }
+    }
+  }
+}
+
+// E1: the encoder head's Gaussian backward of h2 (tc_gbwd<GBWD_ENC>'s
+// arithmetic, the top layer: + dl d log N(h; 0, 1)/dh), per element (d = 50:
+// a quad may straddle dmu | dzs).  The dL/dh2 source comes from this wave's
+// LDS scratch [16 rows][64], read first (hipcc drains the VM counter before
+// an LDS read it cannot tell from the DMA targets); the global loads in
+// batches of NB tiles before their stores.
+template <int NT, int NSO, int NB, class Mid>
+__device__ __forceinline__ void nre_gbwd_enc(const NreLaunch& A, const NrRow& R, float dl, const float* scr,
+                                             NrFrag& X, Mid mid) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15, d = A.de;
+  const __amdgpu_buffer_rsrc_t rp = buf_rsrc(A.Pe), rh = buf_rsrc(A.h2), re = buf_rsrc(A.e2);
+  auto col = [d, g](int t, int i) {
+    const int f = 16 * t + 4 * g + i;
+    return f < d ? f : min(f - d, d - 1);
+  };
+  float G[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) G[t][i] = scr[r * 64 + col(t, i)];
+  mid();                                        // (the caller's loads, after the LDS reads)
+  float va[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t0 = 0; t0 < 2 * NSO; t0 += NB) {
+    float mu[NB][4], zs[NB][4], hv[NB][4], ev[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = t0 + b, f = 16 * t + 4 * g + i, c = col(t, i);
+        const bool ok = t < NT && R.valid && f < 2 * d;
+        mu[b][i] = bld1(rp, ok ? (unsigned)(R.grow * A.ld_Pe + c) * 4u : kOOB);
+        zs[b][i] = bld1(rp, ok ? (unsigned)(R.grow * A.ld_Pe + d + c) * 4u : kOOB);
+        hv[b][i] = bld1(rh, ok ? (unsigned)(R.grow * A.ld_h2 + c) * 4u : kOOB);
+        ev[b][i] = bld1(re, ok ? (unsigned)(R.grow * A.ld_e2 + c) * 4u : kOOB);
+      }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int t = t0 + b, f0 = 16 * t + 4 * g;
+      if (t >= 2 * NSO) break;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (t < NT) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int f = f0 + i;
+          const bool mu_part = f < d, ok = R.valid && f < 2 * d;
+          const float ez = fexp(zs[b][i]);
+          const float rs = frcp(ez + kScaleEps);
+          const float h = hv[b][i];
+          const float z = h * rs - mu[b][i] * rs;
+          const float dlq = -dl;
+          float Gq = G[t][i];
+          Gq += dl * (-h);
+          Gq += dlq * (-z * rs);
+          const float x = mu_part ? Gq + dlq * (z * rs) : (Gq * ev[b][i] + dlq * ((z * z - 1.f) * rs)) * ez;
+          v[i] = ok ? x : 0.f;
+        }
+        nr_st4(A.edP, (R.valid && f0 < 2 * d) ? (unsigned)(R.grow * A.ld_edP + f0) * 4u : kOOB, v);
+      }
+      if (t & 1) {
+        nr_pack(va, v, X.h[t >> 1], X.l[t >> 1]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) va[i] = v[i];
+      }
+    }
+  }
+}
+
+// y of a tanh layer's NT tiles (lane's four features) -- plain loads
+template <int NT>
+__device__ __forceinline__ void nre_load_y(const float* y, int ld, int H, const NrRow& R, float4 (&yv)[NT]) {
+  const int g = (threadIdx.x & 63) >> 4;
+  const __amdgpu_buffer_rsrc_t ry = buf_rsrc(y);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int f0 = 16 * t + 4 * g;
+    yv[t] = bld4(ry, (R.valid && f0 < H) ? (unsigned)(R.grow * ld + f0) * 4u : kOOB);
+  }
+}
+template <int NT>
+__device__ __forceinline__ void nre_touch(float4 (&yv)[NT]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) asm volatile("" : "+v"(yv[t].x), "+v"(yv[t].y), "+v"(yv[t].z), "+v"(yv[t].w));
+}
+
+__global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
+  constexpr NreShapeDef P = kNreShape;
+  constexpr int NA = P.NTPH + P.NTP2 + P.NTP1;          // phase A's units
+  static_assert(NA % NR_G == 0 && NA >= 2, "phase B starts a ring group");
+  static_assert(4 * 1024 * 2 <= NR_SLOT_BF16, "four waves' [16][64] float scratch per slot");
+  const int t = threadIdx.x, lane = t & 63, wave = nr_wave();
+  const int r = lane & 15, g = lane >> 4;
+  NrRow R;
+  const int grow_raw = blockIdx.x * NR_ROWS + wave * 16 + r;
+  R.grow = min(grow_raw, A.rows - 1);
+  R.valid = grow_raw < A.rows;
+  R.q = 0.f; R.p = 0.f; R.l2 = 0.f;
+  R.nul = buf_rsrc(A.dlw, 0u);
+  // ---- prologue (no DMA in flight): the unit table, dL/dlw, phase A's y, P1
+  unsigned* tab = reinterpret_cast<unsigned*>(nrs) + NR_TAB_B / 4;
+  for (int e = t; e < kNrMaxUnits - 8; e += NR_W * 64) {
+    const bool ok = e < A.nunits;
+    tab[2 * e] = ok ? A.units[e].off : 0u;
+    tab[2 * e + 1] = ok ? (unsigned)A.units[e].ns : 0u;
+  }
+  float dl = R.valid ? A.dlw[R.grow] : 0.f;
+  asm volatile("" : "+v"(dl));
+  NrFrag X, Y;
+  nre_gbwd_prior<(2 * 100 + 15) / 16, P.NSPH, 7>(A, R, dl, X);
+  float4 py2[P.NTPH], py1[P.NTP2];
+  nre_load_y(A.py2, A.ld_py2, A.Hp, R, py2);
+  nre_load_y(A.py1, A.ld_py1, A.Hp, R, py1);
+  nre_touch(py2);
+  nre_touch(py1);
+  __syncthreads();                                     // (the table; before the first DMA)
+  NrCtx C;
+  C.rh = buf_rsrc(A.fx_hi, A.fx_bytes);
+  C.rl = buf_rsrc(A.fx_lo, A.fx_bytes);
+  C.u = 0;
+  {
+#pragma unroll
+    for (int i = 0; i < NR_D - NR_G; ++i) {
+      nr_issue(C, i, __builtin_amdgcn_readfirstlane(tab[2 * i]), (int)__builtin_amdgcn_readfirstlane(tab[2 * i + 1]));
+      if ((i % NR_G) == NR_G - 1) {
+        asm volatile("" ::: "memory");
+        nr_st_pad<NR_G * NR_SEPI>(R);
+      }
+    }
+  }
+  auto p0 = [&]() { nr_st_pad<NR_SEPI>(R); };
+  float kp[P.NTP1][4], kx[P.NTE1][4];
+  // ---- phase A: ph^T, p2^T, p1^T
+  auto a1 = nre_dense<P.NSPH, P.NTPH, P.NSP2, true, false>(C, X, Y, py2, A.pdY2, A.ld_pdY2, A.Hp, R, kx, p0);
+  auto a2 = nre_dense<P.NSP2, P.NTP2, P.NSP1, true, false>(C, Y, X, py1, A.pdY1, A.ld_pdY1, A.Hp, R, kx, a1);
+  auto a3 = nre_dense<P.NSP1, P.NTP1, 0, false, true>(C, X, Y, py1, A.dh_dec, A.ld_dh_dec, A.de, R, kp, a2);
+  a3();
+  // ---- drain: phase B's first units and every store have landed; all waves
+  // are done with phase A's slots
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  float* scr = nrs + ((NA - 2 + wave / 4) % NR_D) * (NR_SLOT_BF16 / 2) + (wave % 4) * 1024;
+#pragma unroll
+  for (int tt = 0; tt < P.NTP1; ++tt)
+    *reinterpret_cast<float4*>(scr + r * 64 + 16 * tt + 4 * g) = make_float4(kp[tt][0], kp[tt][1], kp[tt][2], kp[tt][3]);
+  float4 ey2[P.NTEH], ey1[P.NTE2];
+  nre_gbwd_enc<(2 * 50 + 15) / 16, P.NSEH, 4>(A, R, dl, scr, X, [&]() {
+    nre_load_y(A.ey2, A.ld_ey2, A.He, R, ey2);
+    nre_load_y(A.ey1, A.ld_ey1, A.He, R, ey1);
+  });
+  nre_touch(ey2);
+  nre_touch(ey1);
+  // ---- phase B: eh^T, e2^T, e1^T
+  auto b1 = nre_dense<P.NSEH, P.NTEH, P.NSE2, true, false>(C, X, Y, ey2, A.edY2, A.ld_edY2, A.He, R, kx, p0);
+  auto b2 = nre_dense<P.NSE2, P.NTE2, P.NSE1, true, false>(C, Y, X, ey1, A.edY1, A.ld_edY1, A.He, R, kx, b1);
+  auto b3 = nre_dense<P.NSE1, P.NTE1, 0, false, false>(C, X, Y, ey1, A.dh_enc, A.ld_dh_enc, A.dp, R, kx, b2);
+  b3();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+bool nre_shape_ok(const NreLaunch& L) {
+  const NreShapeDef& P = kNreShape;
+  const int tiles[6] = {P.NTPH, P.NTP2, P.NTP1, P.NTEH, P.NTE2, P.NTE1};
+  const int steps[6] = {P.NSPH, P.NSP2, P.NSP1, P.NSEH, P.NSE2, P.NSE1};
+  for (int i = 0; i < 6; ++i)
+    if (L.gx_tiles[i] != tiles[i] || L.gx_steps[i] != steps[i]) return false;
+  return L.dp == 100 && L.de == 50 && L.Hp % 4 == 0 && L.He % 4 == 0 && L.Hp <= 16 * P.NTPH &&
+         L.He <= 16 * P.NTEH && L.nunits + NR_D <= kNrMaxUnits - 8;
+}
+
+hipError_t launch_nre(hipStream_t st, const NreLaunch& L) {
+  if (L.rows <= 0) return hipSuccess;
+  if (!nre_shape_ok(L)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(nre_kernel, dim3((L.rows + NR_ROWS - 1) / NR_ROWS), dim3(NR_W * 64), nring_lds_bytes(), st, L);
+  return hipGetLastError();
+}
+
 static hipError_t nrb_setup_attributes() {
   hipError_t e = hipFuncSetAttribute((const void*)nrb_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      160 * 1024);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)nrb_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)nre_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   return e;
 }
 
