@@ -2161,6 +2161,9 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
     // after them reads both): nring_bwd 2 runs the ring kernel on the side
     // stream beside the engine's launch (each leaves CUs idle: 200 and 400
     // workgroups), joined before the image-row job
+    // (nring_bwd 3, the encoder / prior backward on nre_kernel too: sequential,
+    // 0.574-0.577 vs 0.582-0.583 ms with nrb_kernel on the side stream -- the
+    // two ring kernels hold a CU's LDS each and cannot share one)
     const bool side = ring && h->nring_bwd == 2 && h->L >= 2;
     if (side) {
       HIPCHK(hipEventRecord(h->ev_fork, h->stream));
