@@ -361,6 +361,7 @@ struct UpdArgs {
   // gradient is read from grad, scaled by 1 / *scale_dev (or gscale), written
   // back, then Adam and the FX / GX copies as usual
   int apply; const float* scale_dev;
+  int waves;                                          // 4, or 8 (64-column tiles: two waves per SIMD)
 };
 hipError_t launch_update(hipStream_t st, const UpdArgs& a);
 hipError_t upd_setup_attributes();

@@ -283,6 +283,9 @@ __device__ __forceinline__ nr_f32x4 nr_mma(const __bf16* slot, const NrFrag& IN,
     wh[s % 3] = *reinterpret_cast<const nr_bf16x8*>(slot + s * 1024 + lane * 8);
     wl[s % 3] = *reinterpret_cast<const nr_bf16x8*>(slot + s * 1024 + 512 + lane * 8);
   };
+#ifdef IWAE_NR_PRIO     // experiment: the MFMA phase at raised wave priority
+  __builtin_amdgcn_s_setprio(IWAE_NR_PRIO);
+#endif
   rd(0);
   if (NS > 1) rd(1);
 #pragma unroll
@@ -298,6 +301,9 @@ __device__ __forceinline__ nr_f32x4 nr_mma(const __bf16* slot, const NrFrag& IN,
     __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);                // the MFMAs of step s
     if (s + 2 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0); // the reads of step s + 2
   }
+#ifdef IWAE_NR_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
 #ifdef IWAE_NR_TRACE
   asm volatile("s_nop 0" ::"v"(acc[0]), "v"(acc[3]));
   NR_TR(tu, 2)

@@ -73,15 +73,23 @@ __device__ __forceinline__ int up_cq(int t) { return t & 15; }
 typedef float up_f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 up_bf16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned up_u32x4 __attribute__((ext_vector_type(4)));
-// one iteration's loads of one thread: X rows 8 rg .. + 7 at columns 4 cq ..
-// + 3, dZ the same rows at TN / 16 columns (TN = 64: 4, TN = 32: 2), the row scale
+typedef unsigned up_u32x2 __attribute__((ext_vector_type(2)));
+// NW waves per workgroup (4, or 8 for 64-column tiles: two waves per SIMD);
+// each thread stages RPT rows of an iteration (16 threads per row group)
+template <int NW> struct UpCfg {
+  static constexpr int NT = NW * 64, RPT = 2048 / NT, NK = RPT / 4;
+};
+// one iteration's loads of one thread: X rows RPT rg .. + RPT - 1 at columns
+// 4 cq .. + 3, dZ the same rows at TN / 16 columns (TN = 64: 4, TN = 32: 2),
+// the row scale
 template <int TN> struct UpZ { typedef up_f32x4 type; };
 template <> struct UpZ<32> { typedef up_f32x2 type; };
-template <int TN>
+template <int TN, int NW>
 struct UpRegs {
-  up_f32x4 x[8];
-  typename UpZ<TN>::type z[8];
-  up_f32x4 k0, k1;
+  static constexpr int RPT = UpCfg<NW>::RPT;
+  up_f32x4 x[RPT];
+  typename UpZ<TN>::type z[RPT];
+  up_f32x4 k[UpCfg<NW>::NK];
 };
 __device__ __forceinline__ up_f32x4 up_ld4(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_bit_cast(up_f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
@@ -90,19 +98,20 @@ __device__ __forceinline__ up_f32x2 up_ld2(__amdgpu_buffer_rsrc_t r, unsigned of
   return __builtin_bit_cast(up_f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
 
-// Column C of 8 loaded rows -> bf16 hi / lo planes (hi = RNE(v), lo =
+// Column C of the RPT loaded rows -> bf16 hi / lo planes (hi = RNE(v), lo =
 // RNE(v - hi)), pairwise: one v_cvt_pk_bf16_f32 per pair and plane, the hi
 // pair widened back with a shift and a mask, the residual by one packed
 // subtract; SCALE multiplies row q by the row scale first.  (Pairs are built
 // straight from the vector components: an intermediate float[8] ends up in
 // scratch.)
-template <int C, bool SCALE, typename V, int TN>
-__device__ __forceinline__ void up_split_col(const V (&a)[8], const UpRegs<TN>& R, up_u32x4& h, up_u32x4& l) {
+template <int C, bool SCALE, typename V, int TN, int NW, int RPT>
+__device__ __forceinline__ void up_split_col(const V (&a)[RPT], const UpRegs<TN, NW>& R, unsigned (&h)[RPT / 2],
+                                             unsigned (&l)[RPT / 2]) {
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
+  for (int p = 0; p < RPT / 2; ++p) {
     up_f32x2 x = {a[2 * p][C], a[2 * p + 1][C]};
     if (SCALE) {
-      const up_f32x4& k = p < 2 ? R.k0 : R.k1;
+      const up_f32x4& k = R.k[p >> 1];
       x *= up_f32x2{k[(2 * p) & 3], k[(2 * p + 1) & 3]};
     }
     const unsigned hb = __builtin_bit_cast(unsigned, __builtin_convertvector(x, up_bf16x2));
@@ -112,24 +121,33 @@ __device__ __forceinline__ void up_split_col(const V (&a)[8], const UpRegs<TN>& 
     l[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, up_bf16x2));
   }
 }
-// stage column C of X (plane row 4 cq + C) and, for C < TN / 16, of dZ times
-// the row scale (plane row (TN / 16) cq + C)
-template <int C, int TN>
-__device__ __forceinline__ void up_stage_col(const UpRegs<TN>& R, float* wbuf, int cq, int rg) {
-  up_u32x4 h, l;
-  const int o = up_off(4 * cq + C, rg);
-  up_split_col<C, false>(R.x, R, h, l);
-  *reinterpret_cast<up_u32x4*>(wbuf + o) = h;
-  *reinterpret_cast<up_u32x4*>(wbuf + UP_PLANE + o) = l;
-  if (C < TN / 16) {
-    const int oz = up_off((TN / 16) * cq + C, rg);
-    up_split_col<C < TN / 16 ? C : 0, true>(R.z, R, h, l);
-    *reinterpret_cast<up_u32x4*>(wbuf + 2 * UP_PLANE + oz) = h;
-    *reinterpret_cast<up_u32x4*>(wbuf + 3 * UP_PLANE + oz) = l;
+// RPT k-values of plane row n at the thread's row group rg: 8 rows = one
+// ds_write_b128 at block rg; 4 rows = one ds_write_b64 at half (rg & 1) of block rg >> 1
+template <int NP>
+__device__ __forceinline__ void up_put(float* plane, int n, int rg, const unsigned (&v)[NP]) {
+  if constexpr (NP == 4) {
+    *reinterpret_cast<up_u32x4*>(plane + up_off(n, rg)) = up_u32x4{v[0], v[1], v[2], v[3]};
+  } else {
+    *reinterpret_cast<up_u32x2*>(plane + up_off(n, rg >> 1) + 2 * (rg & 1)) = up_u32x2{v[0], v[1]};
   }
 }
-template <int TN>
-__device__ __forceinline__ void up_stage_c(int c, const UpRegs<TN>& R, float* wbuf, int cq, int rg) {
+// stage column C of X (plane row 4 cq + C) and, for C < TN / 16, of dZ times
+// the row scale (plane row (TN / 16) cq + C)
+template <int C, int TN, int NW>
+__device__ __forceinline__ void up_stage_col(const UpRegs<TN, NW>& R, float* wbuf, int cq, int rg) {
+  constexpr int NP = UpCfg<NW>::RPT / 2;
+  unsigned h[NP], l[NP];
+  up_split_col<C, false>(R.x, R, h, l);
+  up_put(wbuf, 4 * cq + C, rg, h);
+  up_put(wbuf + UP_PLANE, 4 * cq + C, rg, l);
+  if (C < TN / 16) {
+    up_split_col<C < TN / 16 ? C : 0, true>(R.z, R, h, l);
+    up_put(wbuf + 2 * UP_PLANE, (TN / 16) * cq + C, rg, h);
+    up_put(wbuf + 3 * UP_PLANE, (TN / 16) * cq + C, rg, l);
+  }
+}
+template <int TN, int NW>
+__device__ __forceinline__ void up_stage_c(int c, const UpRegs<TN, NW>& R, float* wbuf, int cq, int rg) {
   if (c == 0) up_stage_col<0>(R, wbuf, cq, rg);
   else if (c == 1) up_stage_col<1>(R, wbuf, cq, rg);
   else if (c == 2) up_stage_col<2>(R, wbuf, cq, rg);
@@ -143,27 +161,28 @@ __device__ __forceinline__ void up_stage_c(int c, const UpRegs<TN>& R, float* wb
 struct UpOff {
   unsigned x, z, k;
 };
-template <int TN>
+template <int TN, int NW>
 __device__ __forceinline__ UpOff up_offsets(const UpdJob& J, int i0, int j0) {
+  constexpr int RPT = UpCfg<NW>::RPT;
   const int t = threadIdx.x, rg = up_rg(t), cq = up_cq(t);
   const int ci = i0 + 4 * cq, cj = j0 + (TN / 16) * cq;
   const bool okx = ci < J.lda && !(kUpdAblate & 4), okz = cj < J.ldb && !(kUpdAblate & 4);
   UpOff o;
-  o.x = okx ? (unsigned)(8 * rg * J.lda + ci) * 4u : kOOB;     // kOOB + 7 rows stays out of range
-  o.z = okz ? (unsigned)(8 * rg * J.ldb + cj) * 4u : kOOB;
-  o.k = (unsigned)(8 * rg) * 4u;
+  o.x = okx ? (unsigned)(RPT * rg * J.lda + ci) * 4u : kOOB;   // kOOB + RPT - 1 rows stays out of range
+  o.z = okz ? (unsigned)(RPT * rg * J.ldb + cj) * 4u : kOOB;
+  o.k = (unsigned)(RPT * rg) * 4u;
   return o;
 }
 
-template <int TN>
-__device__ __forceinline__ void up_load(const UpdJob& J, const UpOff& O, int it, UpRegs<TN>& R) {
+template <int TN, int NW>
+__device__ __forceinline__ void up_load(const UpdJob& J, const UpOff& O, int it, UpRegs<TN, NW>& R) {
   const int r0 = it * UP_RI;
   const unsigned left = J.rows > r0 ? (unsigned)(J.rows - r0) : 0u;
   const __amdgpu_buffer_rsrc_t ra = buf_rsrc(J.A + (size_t)r0 * J.lda, left * (unsigned)J.lda * 4u);
   const __amdgpu_buffer_rsrc_t rz = buf_rsrc(J.B + (size_t)r0 * J.ldb, left * (unsigned)J.ldb * 4u);
   const unsigned sx = (unsigned)J.lda * 4u, sz = (unsigned)J.ldb * 4u;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < UpCfg<NW>::RPT; ++q) {
     R.x[q] = up_ld4(ra, O.x + q * sx);
     if constexpr (TN == 64) R.z[q] = up_ld4(rz, O.z + q * sz);
     else R.z[q] = up_ld2(rz, O.z + q * sz);
@@ -171,13 +190,13 @@ __device__ __forceinline__ void up_load(const UpdJob& J, const UpOff& O, int it,
   // dZ row scale (dpx for the output layer, a ones vector otherwise); rows
   // past the last read 0, which also zeroes dZ's stale rows there
   const __amdgpu_buffer_rsrc_t rk = buf_rsrc(J.ks + r0, left * 4u);
-  R.k0 = up_ld4(rk, O.k);
-  R.k1 = up_ld4(rk, O.k + 16u);
+#pragma unroll
+  for (int q = 0; q < UpCfg<NW>::NK; ++q) R.k[q] = up_ld4(rk, O.k + 16u * q);
 }
 
 // registers -> LDS (transposed, split)
-template <int TN>
-__device__ __forceinline__ void up_stage(const UpRegs<TN>& R, float* buf) {
+template <int TN, int NW>
+__device__ __forceinline__ void up_stage(const UpRegs<TN, NW>& R, float* buf) {
   const int t = threadIdx.x, rg = up_rg(t), cq = up_cq(t);
 #pragma unroll
   for (int c = 0; c < 4; ++c) up_stage_c(c, R, buf, cq, rg);
@@ -187,14 +206,15 @@ __device__ __forceinline__ void up_stage(const UpRegs<TN>& R, float* buf) {
 // interleaved: the B fragments are read first, then per chunk c the A
 // fragments of row tile c + 1 are requested, column c of the staging is split
 // and written, and the MFMAs of accumulator row tile si = c run, so the matrix
-// core works while the VALU splits.
-template <int TN>
-__device__ __forceinline__ void up_mul_stage(const float* rbuf, float* wbuf, const UpRegs<TN>& R, bool stage,
-                                             up_f32x4 (&acc)[4][TN / 16]) {
-  constexpr int NJ = TN / 16;
+// core works while the VALU splits.  Wave w multiplies k step w & 3 of the
+// iteration into the column tiles of its part w >> 2 (NW = 8: two halves).
+template <int TN, int NW>
+__device__ __forceinline__ void up_mul_stage(const float* rbuf, float* wbuf, const UpRegs<TN, NW>& R, bool stage,
+                                             up_f32x4 (&acc)[4][TN / 16 / (NW / 4)]) {
+  constexpr int NJ = TN / 16 / (NW / 4);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int t = threadIdx.x, rg = up_rg(t), cq = up_cq(t);
-  const int blk = 4 * w + (lane >> 4);
+  const int blk = 4 * (w & 3) + (lane >> 4), s0 = NJ * (w >> 2);
   up_bf16x8 ah[2], al[2], bh[NJ], bl[NJ];
   auto read_a = [&](int c) __attribute__((always_inline)) {
     const int o = up_off(16 * c + (lane & 15), blk);
@@ -203,7 +223,7 @@ __device__ __forceinline__ void up_mul_stage(const float* rbuf, float* wbuf, con
   };
 #pragma unroll
   for (int s = 0; s < NJ; ++s) {
-    const int o = up_off(16 * s + (lane & 15), blk);
+    const int o = up_off(16 * (s0 + s) + (lane & 15), blk);
     bh[s] = *reinterpret_cast<const up_bf16x8*>(rbuf + 2 * UP_PLANE + o);
     bl[s] = *reinterpret_cast<const up_bf16x8*>(rbuf + 3 * UP_PLANE + o);
   }
@@ -231,9 +251,10 @@ __device__ __forceinline__ int up_fx_pos(int j, int head_d) {
 
 // One 64 x TN tile (TN = 64, or 32 for the sample-row layers: more
 // workgroups, half the MFMA and a quarter less staging per workgroup).
-template <int TN>
+template <int TN, int NW>
 __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, const AdamState& st, int b, int lt) {
-  constexpr int NJ = TN / 16, EJ = TN / 4, PS = TN + 4;
+  constexpr int NT = UpCfg<NW>::NT, TPR = NT / 64;   // threads per epilogue row
+  constexpr int NJ = TN / 16 / (NW / 4), EJ = TN / TPR, PS = TN + 4;
   const int tn = lt / J.tiles_m, tm = lt - tn * J.tiles_m;
   const int i0 = 64 * tm, j0 = TN * tn;
   const int t = threadIdx.x;
@@ -253,9 +274,9 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
   const int ngrp = ((kUpdAblate & 64) || a.apply) ? 0 : (J.rows + UP_G * UP_RI - 1) / (UP_G * UP_RI);
   float* buf0 = ups;
   float* buf1 = ups + UP_BUF;
-  const UpOff O = up_offsets<TN>(J, i0, j0);
+  const UpOff O = up_offsets<TN, NW>(J, i0, j0);
   // epilogue elements: row ei, columns ej .. ej + EJ - 1
-  const int ei = t >> 2, ej = EJ * (t & 3);
+  const int ei = t / TPR, ej = EJ * (t % TPR);
   const bool erow = i0 + ei < M;
   float4 pp[EJ / 4], mm[EJ / 4], vv[EJ / 4];
   // Adam operands of the epilogue's elements
@@ -279,45 +300,45 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
   // followed by another (stage / request across the boundary).
   // (the two sets are named explicitly per step: a reference chosen at run
   // time would put them in scratch memory)
-  auto step = [&](int u, const float* rbuf, float* wbuf, UpRegs<TN>& Rn, int it0, bool tail)
+  auto step = [&](int u, const float* rbuf, float* wbuf, UpRegs<TN, NW>& Rn, int it0, bool tail)
                   __attribute__((always_inline)) {
     const bool more = u + 1 < UP_G || tail;
-    up_mul_stage<TN>(rbuf, wbuf, Rn, more, acc);
+    up_mul_stage<TN, NW>(rbuf, wbuf, Rn, more, acc);
     __builtin_amdgcn_sched_barrier(0);
-    if (u + 3 < UP_G || tail) up_load<TN>(J, O, it0 + u + 3, Rn);
+    if (u + 3 < UP_G || tail) up_load<TN, NW>(J, O, it0 + u + 3, Rn);
     // the Adam operands once the last rows are requested (their registers
     // would otherwise crowd out the load sets for the whole reduction)
     if (!tail && u == UP_G - 3) adam_prefetch();
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   };
-  auto group = [&](UpRegs<TN>& R0, UpRegs<TN>& R1, int it0, bool tail) __attribute__((always_inline)) {
+  auto group = [&](UpRegs<TN, NW>& R0, UpRegs<TN, NW>& R1, int it0, bool tail) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < UP_G; u += 2) {
       step(u, buf0, buf1, R1, it0, tail);
       step(u + 1, buf1, buf0, R0, it0, tail);
     }
   };
-  auto start = [&](UpRegs<TN>& R0, UpRegs<TN>& R1) __attribute__((always_inline)) {
-    up_load<TN>(J, O, 0, R0);
+  auto start = [&](UpRegs<TN, NW>& R0, UpRegs<TN, NW>& R1) __attribute__((always_inline)) {
+    up_load<TN, NW>(J, O, 0, R0);
     __builtin_amdgcn_sched_barrier(0);
-    up_load<TN>(J, O, 1, R1);
+    up_load<TN, NW>(J, O, 1, R1);
     __builtin_amdgcn_sched_barrier(0);
-    up_stage<TN>(R0, buf0);
+    up_stage<TN, NW>(R0, buf0);
     __builtin_amdgcn_sched_barrier(0);
-    up_load<TN>(J, O, 2, R0);
+    up_load<TN, NW>(J, O, 2, R0);
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   };
   if (ngrp == 1) {
     // straight-line (up to 1024 rows): no loop-carried register set, so no
     // renaming copy drains the loads in flight
-    UpRegs<TN> R0, R1;
+    UpRegs<TN, NW> R0, R1;
     start(R0, R1);
     group(R0, R1, 0, false);
   } else if (ngrp > 1) {
     // the sets are carried into the next group: renamed once per 1024 rows
-    UpRegs<TN> R0, R1;
+    UpRegs<TN, NW> R0, R1;
     start(R0, R1);
     for (int gi = 0; gi < ngrp; ++gi) group(R0, R1, gi * UP_G, true);
     adam_prefetch();
@@ -342,23 +363,25 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
     }
     wsc = 1.f;
   } else {
-  // the four waves' tiles -> LDS, summed in wave order
+  // the four k steps' tiles -> LDS (NW = 8: each from two waves, column halves), summed in k order
   {
     const int lane = t & 63, w = t >> 6;
-    float* part = ups + w * 64 * PS;
+    float* part = ups + (w & 3) * 64 * PS;
+    const int s0 = NJ * (w >> 2);
 #pragma unroll
     for (int si = 0; si < 4; ++si)
 #pragma unroll
       for (int sj = 0; sj < NJ; ++sj)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) part[(16 * si + 4 * (lane >> 4) + q) * PS + 16 * sj + (lane & 15)] = acc[si][sj][q];
+        for (int q = 0; q < 4; ++q)
+          part[(16 * si + 4 * (lane >> 4) + q) * PS + 16 * (s0 + sj) + (lane & 15)] = acc[si][sj][q];
   }
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < EJ / 4; ++q) {
     float4 s = *reinterpret_cast<const float4*>(ups + ei * PS + ej + 4 * q);
 #pragma unroll
-    for (int w = 1; w < UP_NW; ++w) {
+    for (int w = 1; w < 4; ++w) {
       const float4 u = *reinterpret_cast<const float4*>(ups + w * 64 * PS + ei * PS + ej + 4 * q);
       s.x += u.x; s.y += u.y; s.z += u.z; s.w += u.w;
     }
@@ -408,8 +431,8 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
   __syncthreads();
   // FX chunks: (feature jj, 8 W_aug rows 8 ib ..) -> lane (pos & 15) + 16 ((k % 32) / 8) of step k / 32
 #pragma unroll
-  for (int e = 0; e < TN / 32; ++e) {
-    const int c = t + UP_NT * e, jj = c % TN, ib = c / TN;
+  for (int e = 0; e < TN * 8 / NT; ++e) {
+    const int c = t + NT * e, jj = c % TN, ib = c / TN;
     const int j = j0 + jj, k0 = i0 + 8 * ib;
     if (j < J.fout && k0 < M) {
       up_bf16x8 vh, vl;
@@ -429,8 +452,8 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
   }
   // GX chunks: (input feature ii < fin, 8 outputs 8 jb ..)
 #pragma unroll
-  for (int e = 0; e < TN / 32; ++e) {
-    const int c = t + UP_NT * e, jb = c % (TN / 8), ii = c / (TN / 8);
+  for (int e = 0; e < TN * 8 / NT; ++e) {
+    const int c = t + NT * e, jb = c % (TN / 8), ii = c / (TN / 8);
     const int n = i0 + ii, k0 = j0 + 8 * jb;
     if (n < J.fin && k0 < J.fout) {
       up_bf16x8 vh, vl;
@@ -449,7 +472,8 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
   }
 }
 
-__global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void upd_kernel(UpdArgs a) {
   // tile of this workgroup: consecutive tiles (sharing an operand slice) on one XCD
   // (the long reductions -- tiles [0, nheavy) -- are spread evenly over the
   // XCDs first, the short ones after, so no XCD gets more long tiles than CUs)
@@ -483,24 +507,34 @@ __global__ __launch_bounds__(UP_NT) void upd_kernel(UpdArgs a) {
     Js.ks = J.ks + r0;
     Js.rows = min(J.chunk, J.rows - (int)r0);
     Js.off = J.off + s * J.slab_stride;
-    upd_tile<64>(a, Js, st, b, lt - s * per);
-  } else if (J.tn == 32) {
-    upd_tile<32>(a, J, st, b, T - J.tile0);
+    upd_tile<64, NW>(a, Js, st, b, lt - s * per);
+  } else if (NW == 4 && J.tn == 32) {
+    upd_tile<32, 4>(a, J, st, b, T - J.tile0);
   } else {
-    upd_tile<64>(a, J, st, b, T - J.tile0);
+    upd_tile<64, NW>(a, J, st, b, T - J.tile0);
   }
 }
 
 hipError_t launch_update(hipStream_t st, const UpdArgs& a) {
   if (a.ntiles <= 0) return hipSuccess;
   const unsigned grid = 8u * (unsigned)(a.per_xcd + a.per_xcd2);
-  hipLaunchKernelGGL(upd_kernel, dim3(grid), dim3(UP_NT), (size_t)2 * UP_BUF * sizeof(float), st, a);
+  // 8 waves (two per SIMD, each half the tile's columns) unless a job uses 64 x 32 tiles
+  bool tn32 = false;
+  for (int j = 0; j < a.njobs; ++j) tn32 = tn32 || a.job[j].tn == 32;
+  if (a.waves == 8 && !tn32)
+    hipLaunchKernelGGL(upd_kernel<8>, dim3(grid), dim3(8 * 64), (size_t)2 * UP_BUF * sizeof(float), st, a);
+  else
+    hipLaunchKernelGGL(upd_kernel<4>, dim3(grid), dim3(4 * 64), (size_t)2 * UP_BUF * sizeof(float), st, a);
   return hipGetLastError();
 }
 
 hipError_t upd_setup_attributes() {
-  return hipFuncSetAttribute((const void*)upd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             2 * UP_BUF * (int)sizeof(float));
+  hipError_t e = hipFuncSetAttribute((const void*)upd_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     2 * UP_BUF * (int)sizeof(float));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)upd_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            2 * UP_BUF * (int)sizeof(float));
+  return e;
 }
 
 }  // namespace iwae
