@@ -138,7 +138,8 @@ enum iwae_knob {
                                       3 the encoder / prior backward on the ring as well (2-layer shape) (3) */
   IWAE_KNOB_WIDE_RT = 25           /* row tiles of 16 per workgroup of the engine's backward launches from
                                       WIDE_ROWS: 1, 2 or 4 (2; the forward launch: 4) */,
-  IWAE_KNOB_UPD_WAVES = 26         /* update kernel workgroup: 8 waves (two per SIMD, each half a tile's columns) or 4 (8) */
+  IWAE_KNOB_UPD_WAVES = 26         /* update kernel workgroup: 16 waves (four per SIMD, each a quarter of a tile's
+                                      columns for one k step), 8 or 4 (16) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --

@@ -165,7 +165,7 @@ struct iwae_handle {
   int nring_bwd = 3;                 // large-batch train step: the output MLP's backward on nrb_kernel
                                      // (2: on the side stream beside the engine's backward launch;
                                      // 3: then the encoder / prior backward on nre_kernel too)
-  int upd_waves = 8;                 // update kernel workgroups: 8 waves (two per SIMD) or 4
+  int upd_waves = 16;                // update kernel workgroups: 16 waves (four per SIMD), 8 or 4
   int wide_rt = 2;                   // engine row tiles per workgroup of the backward launches from
                                      // wide_rows (1, 2 or 4; the forward launch: 4)
   NrUnit* nrb_units = nullptr;       // its unit table (device, built once)
@@ -2658,7 +2658,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;
     case IWAE_KNOB_NRING_BWD: h->nring_bwd = (int)std::min<long long>(std::max(0LL, value), 3); break;
-    case IWAE_KNOB_UPD_WAVES: h->upd_waves = value == 4 ? 4 : 8; break;
+    case IWAE_KNOB_UPD_WAVES: h->upd_waves = value == 4 ? 4 : value >= 16 ? 16 : 8; break;
     case IWAE_KNOB_WIDE_RT: h->wide_rt = value >= 4 ? 4 : value <= 1 ? 1 : 2; break;
     case IWAE_KNOB_LD_ALIGN:
       if (value != 4 && value != 8 && value != 16 && value != 32)

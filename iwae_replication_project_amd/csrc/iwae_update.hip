@@ -77,7 +77,7 @@ typedef unsigned up_u32x2 __attribute__((ext_vector_type(2)));
 // NW waves per workgroup (4, or 8 for 64-column tiles: two waves per SIMD);
 // each thread stages RPT rows of an iteration (16 threads per row group)
 template <int NW> struct UpCfg {
-  static constexpr int NT = NW * 64, RPT = 2048 / NT, NK = RPT / 4;
+  static constexpr int NT = NW * 64, RPT = 2048 / NT, NK = RPT >= 4 ? RPT / 4 : 1;
 };
 // one iteration's loads of one thread: X rows RPT rg .. + RPT - 1 at columns
 // 4 cq .. + 3, dZ the same rows at TN / 16 columns (TN = 64: 4, TN = 32: 2),
@@ -127,8 +127,10 @@ template <int NP>
 __device__ __forceinline__ void up_put(float* plane, int n, int rg, const unsigned (&v)[NP]) {
   if constexpr (NP == 4) {
     *reinterpret_cast<up_u32x4*>(plane + up_off(n, rg)) = up_u32x4{v[0], v[1], v[2], v[3]};
-  } else {
+  } else if constexpr (NP == 2) {
     *reinterpret_cast<up_u32x2*>(plane + up_off(n, rg >> 1) + 2 * (rg & 1)) = up_u32x2{v[0], v[1]};
+  } else {
+    plane[up_off(n, rg >> 2) + (rg & 3)] = __uint_as_float(v[0]);
   }
 }
 // stage column C of X (plane row 4 cq + C) and, for C < TN / 16, of dZ times
@@ -431,10 +433,10 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
   __syncthreads();
   // FX chunks: (feature jj, 8 W_aug rows 8 ib ..) -> lane (pos & 15) + 16 ((k % 32) / 8) of step k / 32
 #pragma unroll
-  for (int e = 0; e < TN * 8 / NT; ++e) {
+  for (int e = 0; e < (TN * 8 + NT - 1) / NT; ++e) {
     const int c = t + NT * e, jj = c % TN, ib = c / TN;
     const int j = j0 + jj, k0 = i0 + 8 * ib;
-    if (j < J.fout && k0 < M) {
+    if (c < TN * 8 && j < J.fout && k0 < M) {
       up_bf16x8 vh, vl;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -452,10 +454,10 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
   }
   // GX chunks: (input feature ii < fin, 8 outputs 8 jb ..)
 #pragma unroll
-  for (int e = 0; e < TN * 8 / NT; ++e) {
+  for (int e = 0; e < (TN * 8 + NT - 1) / NT; ++e) {
     const int c = t + NT * e, jb = c % (TN / 8), ii = c / (TN / 8);
     const int n = i0 + ii, k0 = j0 + 8 * jb;
-    if (n < J.fin && k0 < J.fout) {
+    if (c < TN * 8 && n < J.fin && k0 < J.fout) {
       up_bf16x8 vh, vl;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -521,7 +523,9 @@ hipError_t launch_update(hipStream_t st, const UpdArgs& a) {
   // 8 waves (two per SIMD, each half the tile's columns) unless a job uses 64 x 32 tiles
   bool tn32 = false;
   for (int j = 0; j < a.njobs; ++j) tn32 = tn32 || a.job[j].tn == 32;
-  if (a.waves == 8 && !tn32)
+  if (a.waves == 16 && !tn32)
+    hipLaunchKernelGGL(upd_kernel<16>, dim3(grid), dim3(16 * 64), (size_t)2 * UP_BUF * sizeof(float), st, a);
+  else if (a.waves == 8 && !tn32)
     hipLaunchKernelGGL(upd_kernel<8>, dim3(grid), dim3(8 * 64), (size_t)2 * UP_BUF * sizeof(float), st, a);
   else
     hipLaunchKernelGGL(upd_kernel<4>, dim3(grid), dim3(4 * 64), (size_t)2 * UP_BUF * sizeof(float), st, a);
@@ -533,6 +537,9 @@ hipError_t upd_setup_attributes() {
                                      2 * UP_BUF * (int)sizeof(float));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)upd_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            2 * UP_BUF * (int)sizeof(float));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)upd_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             2 * UP_BUF * (int)sizeof(float));
   return e;
 }

@@ -8,5 +8,5 @@ mkdir -p $O
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
 tail -3 $O/pytest.log
 [ $rc -eq 0 ] || exit $rc
-EXTRA="--no-large-batch --no-c0 --no-stats" TUNES="default upd_waves=4 default upd_waves=4" bash tools/ab_tune.sh || exit $?
-TUNES="default upd_waves=4" bash tools/lb_ab.sh
+EXTRA="--no-large-batch --no-c0 --no-stats" TUNES="default upd_waves=8 default upd_waves=8" bash tools/ab_tune.sh || exit $?
+TUNES="default upd_waves=8" bash tools/lb_ab.sh
