@@ -1517,6 +1517,7 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
   R.valid = grow_raw < A.rows;
   R.q = 0.f; R.p = 0.f; R.l2 = 0.f;
   R.nul = buf_rsrc(A.dlw, 0u);
+  NR_TR(kNrMaxUnits - 1, 0)
   // ---- prologue (no DMA in flight): the unit table, dL/dlw, phase A's y, P1
   unsigned* tab = reinterpret_cast<unsigned*>(nrs) + NR_TAB_B / 4;
   for (int e = t; e < kNrMaxUnits - 8; e += NR_W * 64) {
@@ -1550,11 +1551,13 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
   }
   auto p0 = [&]() { nr_st_pad<NR_SEPI>(R); };
   float kp[P.NTP1][4], kx[P.NTE1][4];
+  NR_TR(kNrMaxUnits - 1, 1)
   // ---- phase A: ph^T, p2^T, p1^T
   auto a1 = nre_dense<P.NSPH, P.NTPH, P.NSP2, true, false>(C, X, Y, py2, A.pdY2, A.ld_pdY2, A.Hp, R, kx, p0);
   auto a2 = nre_dense<P.NSP2, P.NTP2, P.NSP1, true, false>(C, Y, X, py1, A.pdY1, A.ld_pdY1, A.Hp, R, kx, a1);
   auto a3 = nre_dense<P.NSP1, P.NTP1, 0, false, true>(C, X, Y, py1, A.dh_dec, A.ld_dh_dec, A.de, R, kp, a2);
   a3();
+  NR_TR(kNrMaxUnits - 2, 0)
   // ---- drain: phase B's first units and every store have landed; all waves
   // are done with phase A's slots
   asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -1569,6 +1572,7 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
   });
   nre_touch(ey2);
   nre_touch(ey1);
+  NR_TR(kNrMaxUnits - 2, 1)
   // ---- phase B: eh^T, e2^T, e1^T
   auto b1 = nre_dense<P.NSEH, P.NTEH, P.NSE2, true, false>(C, X, Y, ey2, A.edY2, A.ld_edY2, A.He, R, kx, p0);
   auto b2 = nre_dense<P.NSE2, P.NTE2, P.NSE1, true, false>(C, Y, X, ey1, A.edY1, A.ld_edY1, A.He, R, kx, b1);
