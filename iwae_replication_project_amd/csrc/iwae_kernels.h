@@ -586,6 +586,7 @@ struct NreLaunch {
   float* dh_enc; int ld_dh_enc;                   // dL/dh1 of the encoder chain
   int gx_tiles[6], gx_steps[6];                   // ph, p2, p1, eh, e2, e1 (shape check)
 };
+constexpr int kNreGap = 6;       // empty units in nre_kernel's table between its ring phases (NR_D - NR_G)
 bool nre_shape_ok(const NreLaunch& L);
 hipError_t launch_nre(hipStream_t st, const NreLaunch& L);
 

@@ -3197,6 +3197,10 @@ static bool nre_plan(iwae_handle* h, NreLaunch& R) {
     for (int t = 0; t < d.gx_tiles; ++t)
       units.push_back(NrUnit{(unsigned)((d.gx_off + (long long)t * d.gx_steps * 512) * (long long)sizeof(__bf16)),
                              d.gx_steps});
+    // (after the prior chain: empty units, so nothing of the encoder chain is
+    // in flight while the kernel stages the encoder's Gaussian backward in the ring's LDS)
+    if (i == 2)
+      for (int e = 0; e < kNreGap; ++e) units.push_back(NrUnit{0u, 0});
   }
   R.nunits = (int)units.size();
   R.dp = h->dec[0].d; R.de = h->enc[1].d;

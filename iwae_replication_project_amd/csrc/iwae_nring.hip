@@ -1365,28 +1365,60 @@ __device__ __forceinline__ auto nre_dense(NrCtx& C, const NrFrag& IN, NrFrag& OU
   };
 }
 
+// Row-contiguous copy of this wave's 16 rows (n floats each, global row
+// stride ld, n % V == 0) into LDS [16][n]: consecutive lanes take consecutive
+// V-float chunks of a row -- coalesced, where the C-layout lane map would read
+// 16 scattered 16-byte pieces per instruction.  Rows past the launch repeat
+// the last one.  Only where no DMA is in flight (hipcc waits vmcnt(0) before
+// an LDS access it cannot tell from the DMA targets).
+template <int V, int N>
+__device__ __forceinline__ void nre_stage_rows(const float* src, int ld, int rows, float* dst) {
+  static_assert(N % V == 0, "row width");
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  constexpr int PER = N / V, NI = (16 * PER + 63) / 64;
+  const int lane = threadIdx.x & 63, w = nr_wave();
+  const int row0 = blockIdx.x * NR_ROWS + w * 16;
+  const __amdgpu_buffer_rsrc_t r = buf_rsrc(src);
+  nr_u32x4 v4[V == 4 ? NI : 1];
+  u32x2 v2[V == 2 ? NI : 1];
+#pragma unroll
+  for (int k = 0; k < NI; ++k) {                 // every load first, then the LDS writes
+    const int e = lane + 64 * k, rr = e / PER, c = (e - rr * PER) * V;
+    const int gr = min(row0 + min(rr, 15), rows - 1);
+    const unsigned off = e < 16 * PER ? (unsigned)(gr * ld + c) * 4u : kOOB;
+    if constexpr (V == 4) v4[k] = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    else v2[k] = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  }
+#pragma unroll
+  for (int k = 0; k < NI; ++k) {
+    const int e = lane + 64 * k, rr = e / PER, c = (e - rr * PER) * V;
+    if (e < 16 * PER) {
+      if constexpr (V == 4) *reinterpret_cast<nr_u32x4*>(dst + rr * N + c) = v4[k];
+      else *reinterpret_cast<u32x2*>(dst + rr * N + c) = v2[k];
+    }
+  }
+}
+
 // P1: the prior head's Gaussian backward (tc_gbwd<GBWD_PRIOR>'s arithmetic)
 // on dP's C layout, d % 4 == 0 (a lane's quad is all dmu or all dzs):
 // dmu = dl z / s, dzs = dl (z^2 - 1) / s e^zs, dL/dh1 = -dl z / s; NT tiles
-// of 2d features, packed into X's NSO k steps.  Loads in batches of NB tiles,
-// all issued before the batch's stores (hipcc keeps a load after a store it
-// cannot prove disjoint).
+// of 2d features, packed into X's NSO k steps.  (mu | zs) of the wave's rows
+// staged in LDS (stg, [16][2d]: each column is read by a dmu and a dzs quad);
+// h read directly, in batches of NB tiles issued before their stores.
 template <int NT, int NSO, int NB>
-__device__ __forceinline__ void nre_gbwd_prior(const NreLaunch& A, const NrRow& R, float dl, NrFrag& X) {
-  const int g = (threadIdx.x & 63) >> 4, d = A.dp;
-  const __amdgpu_buffer_rsrc_t rp = buf_rsrc(A.Pp), rh = buf_rsrc(A.h1);
+__device__ __forceinline__ void nre_gbwd_prior(const NreLaunch& A, const NrRow& R, float dl, float* stg, NrFrag& X) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15, d = A.dp;
+  nre_stage_rows<4, 200>(A.Pp, A.ld_Pp, A.rows, stg);             // (dp == 100: nre_shape_ok)
+  const __amdgpu_buffer_rsrc_t rh = buf_rsrc(A.h1);
   float va[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t0 = 0; t0 < 2 * NSO; t0 += NB) {
-    float4 mu[NB], zs[NB], hv[NB];
+    float4 hv[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int t = t0 + b, f0 = 16 * t + 4 * g;
       const bool mu_part = f0 < d, ok = t < NT && R.valid && f0 < 2 * d;
-      const int c0 = mu_part ? f0 : f0 - d;
-      mu[b] = bld4(rp, ok ? (unsigned)(R.grow * A.ld_Pp + c0) * 4u : kOOB);
-      zs[b] = bld4(rp, ok ? (unsigned)(R.grow * A.ld_Pp + d + c0) * 4u : kOOB);
-      hv[b] = bld4(rh, ok ? (unsigned)(R.grow * A.ld_h1 + c0) * 4u : kOOB);
+      hv[b] = bld4(rh, ok ? (unsigned)(R.grow * A.ld_h1 + (mu_part ? f0 : f0 - d)) * 4u : kOOB);
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -1395,12 +1427,15 @@ __device__ __forceinline__ void nre_gbwd_prior(const NreLaunch& A, const NrRow& 
       float v[4] = {0.f, 0.f, 0.f, 0.f};
       if (t < NT) {
         const bool mu_part = f0 < d, ok = R.valid && f0 < 2 * d;
+        const int c0 = min(mu_part ? f0 : f0 - d, d - 4);
+        const float4 mu = *reinterpret_cast<const float4*>(stg + r * 2 * d + c0);
+        const float4 zs = *reinterpret_cast<const float4*>(stg + r * 2 * d + d + c0);
         float dh[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float ez = fexp(f4_at(zs[b], i));
+          const float ez = fexp(f4_at(zs, i));
           const float rs = frcp(ez + kScaleEps);
-          const float z = f4_at(hv[b], i) * rs - f4_at(mu[b], i) * rs;
+          const float z = f4_at(hv[b], i) * rs - f4_at(mu, i) * rs;
           dh[i] = dl * (-z * rs);
           const float x = mu_part ? dl * (z * rs) : (dl * ((z * z - 1.f) * rs)) * ez;
           v[i] = ok ? x : 0.f;
@@ -1420,69 +1455,47 @@ __device__ __forceinline__ void nre_gbwd_prior(const NreLaunch& A, const NrRow& 
 
 // E1: the encoder head's Gaussian backward of h2 (tc_gbwd<GBWD_ENC>'s
 // arithmetic, the top layer: + dl d log N(h; 0, 1)/dh), per element (d = 50:
-// a quad may straddle dmu | dzs).  The dL/dh2 source comes from this wave's
-// LDS scratch [16 rows][64], read first (hipcc drains the VM counter before
-// an LDS read it cannot tell from the DMA targets); the global loads in
-// batches of NB tiles before their stores.
-template <int NT, int NSO, int NB, class Mid>
-__device__ __forceinline__ void nre_gbwd_enc(const NreLaunch& A, const NrRow& R, float dl, const float* scr,
-                                             NrFrag& X, Mid mid) {
+// a quad may straddle dmu | dzs), every operand from this wave's LDS region
+// stg: (mu | zs) [16][2d], h [16][d], eps [16][d] (row-contiguous copies) and
+// the dL/dh2 source [16][52] (p1^T's output, written by the caller)
+template <int NT, int NSO>
+__device__ __forceinline__ void nre_gbwd_enc(const NreLaunch& A, const NrRow& R, float dl, const float* stg,
+                                             NrFrag& X) {
   const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15, d = A.de;
-  const __amdgpu_buffer_rsrc_t rp = buf_rsrc(A.Pe), rh = buf_rsrc(A.h2), re = buf_rsrc(A.e2);
-  auto col = [d, g](int t, int i) {
-    const int f = 16 * t + 4 * g + i;
-    return f < d ? f : min(f - d, d - 1);
-  };
-  float G[NT][4];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) G[t][i] = scr[r * 64 + col(t, i)];
-  mid();                                        // (the caller's loads, after the LDS reads)
+  const float* sP = stg;
+  const float* sH = stg + 16 * 2 * d;
+  const float* sE = sH + 16 * d;
+  const float* sG = sE + 16 * d;
   float va[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int t0 = 0; t0 < 2 * NSO; t0 += NB) {
-    float mu[NB][4], zs[NB][4], hv[NB][4], ev[NB][4];
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
+  for (int t = 0; t < 2 * NSO; ++t) {
+    const int f0 = 16 * t + 4 * g;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (t < NT) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int t = t0 + b, f = 16 * t + 4 * g + i, c = col(t, i);
-        const bool ok = t < NT && R.valid && f < 2 * d;
-        mu[b][i] = bld1(rp, ok ? (unsigned)(R.grow * A.ld_Pe + c) * 4u : kOOB);
-        zs[b][i] = bld1(rp, ok ? (unsigned)(R.grow * A.ld_Pe + d + c) * 4u : kOOB);
-        hv[b][i] = bld1(rh, ok ? (unsigned)(R.grow * A.ld_h2 + c) * 4u : kOOB);
-        ev[b][i] = bld1(re, ok ? (unsigned)(R.grow * A.ld_e2 + c) * 4u : kOOB);
+        const int f = f0 + i;
+        const bool mu_part = f < d, ok = R.valid && f < 2 * d;
+        const int c = mu_part ? f : min(f - d, d - 1);
+        const float mu = sP[r * 2 * d + c], zs = sP[r * 2 * d + d + c];
+        const float h = sH[r * d + c], e = sE[r * d + c], G0 = sG[r * 52 + c];
+        const float ez = fexp(zs);
+        const float rs = frcp(ez + kScaleEps);
+        const float z = h * rs - mu * rs;
+        const float dlq = -dl;
+        float Gq = G0;
+        Gq += dl * (-h);
+        Gq += dlq * (-z * rs);
+        const float x = mu_part ? Gq + dlq * (z * rs) : (Gq * e + dlq * ((z * z - 1.f) * rs)) * ez;
+        v[i] = ok ? x : 0.f;
       }
+      nr_st4(A.edP, (R.valid && f0 < 2 * d) ? (unsigned)(R.grow * A.ld_edP + f0) * 4u : kOOB, v);
+    }
+    if (t & 1) {
+      nr_pack(va, v, X.h[t >> 1], X.l[t >> 1]);
+    } else {
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const int t = t0 + b, f0 = 16 * t + 4 * g;
-      if (t >= 2 * NSO) break;
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (t < NT) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int f = f0 + i;
-          const bool mu_part = f < d, ok = R.valid && f < 2 * d;
-          const float ez = fexp(zs[b][i]);
-          const float rs = frcp(ez + kScaleEps);
-          const float h = hv[b][i];
-          const float z = h * rs - mu[b][i] * rs;
-          const float dlq = -dl;
-          float Gq = G[t][i];
-          Gq += dl * (-h);
-          Gq += dlq * (-z * rs);
-          const float x = mu_part ? Gq + dlq * (z * rs) : (Gq * ev[b][i] + dlq * ((z * z - 1.f) * rs)) * ez;
-          v[i] = ok ? x : 0.f;
-        }
-        nr_st4(A.edP, (R.valid && f0 < 2 * d) ? (unsigned)(R.grow * A.ld_edP + f0) * 4u : kOOB, v);
-      }
-      if (t & 1) {
-        nr_pack(va, v, X.h[t >> 1], X.l[t >> 1]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) va[i] = v[i];
-      }
+      for (int i = 0; i < 4; ++i) va[i] = v[i];
     }
   }
 }
@@ -1508,7 +1521,8 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
   constexpr NreShapeDef P = kNreShape;
   constexpr int NA = P.NTPH + P.NTP2 + P.NTP1;          // phase A's units
   static_assert(NA % NR_G == 0 && NA >= 2, "phase B starts a ring group");
-  static_assert(4 * 1024 * 2 <= NR_SLOT_BF16, "four waves' [16][64] float scratch per slot");
+  static_assert(16 * 200 <= NR_SLOT_BF16 / 2 && 16 * (4 * 50 + 52) <= NR_SLOT_BF16 / 2, "staging in a wave's slot");
+  static_assert(kNreGap == NR_D - NR_G, "empty units between the ring phases");
   const int t = threadIdx.x, lane = t & 63, wave = nr_wave();
   const int r = lane & 15, g = lane >> 4;
   NrRow R;
@@ -1528,7 +1542,8 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
   float dl = R.valid ? A.dlw[R.grow] : 0.f;
   asm volatile("" : "+v"(dl));
   NrFrag X, Y;
-  nre_gbwd_prior<(2 * 100 + 15) / 16, P.NSPH, 7>(A, R, dl, X);
+  // (the ring is idle: each wave stages in its 16 KiB of it)
+  nre_gbwd_prior<(2 * 100 + 15) / 16, P.NSPH, 7>(A, R, dl, nrs + wave * (NR_SLOT_BF16 / 2), X);
   float4 py2[P.NTPH], py1[P.NTP2];
   nre_load_y(A.py2, A.ld_py2, A.Hp, R, py2);
   nre_load_y(A.py1, A.ld_py1, A.Hp, R, py1);
@@ -1558,20 +1573,44 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
   auto a3 = nre_dense<P.NSP1, P.NTP1, 0, false, true>(C, X, Y, py1, A.dh_dec, A.ld_dh_dec, A.de, R, kp, a2);
   a3();
   NR_TR(kNrMaxUnits - 2, 0)
-  // ---- drain: phase B's first units and every store have landed; all waves
-  // are done with phase A's slots
+  // ---- drain: every store and request has landed (the table's NR_D - NR_G
+  // empty units after phase A: nothing of phase B was requested), every
+  // wave is done with the ring -- each stages E1's operands in its 16 KiB
   asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  float* scr = nrs + ((NA - 2 + wave / 4) % NR_D) * (NR_SLOT_BF16 / 2) + (wave % 4) * 1024;
+  {
+    const int de = A.de;
+    float* stg = nrs + wave * (NR_SLOT_BF16 / 2);
+    nre_stage_rows<4, 100>(A.Pe, A.ld_Pe, A.rows, stg);            // (de == 50: nre_shape_ok)
+    nre_stage_rows<2, 50>(A.h2, A.ld_h2, A.rows, stg + 16 * 2 * de);
+    nre_stage_rows<2, 50>(A.e2, A.ld_e2, A.rows, stg + 16 * 3 * de);
+    float* sG = stg + 16 * 4 * de;                     // [16][52]: p1^T's output, features < 52
 #pragma unroll
-  for (int tt = 0; tt < P.NTP1; ++tt)
-    *reinterpret_cast<float4*>(scr + r * 64 + 16 * tt + 4 * g) = make_float4(kp[tt][0], kp[tt][1], kp[tt][2], kp[tt][3]);
+    for (int tt = 0; tt < P.NTP1; ++tt)
+      if (16 * tt + 4 * g < 52)
+        *reinterpret_cast<float4*>(sG + r * 52 + 16 * tt + 4 * g) = make_float4(kp[tt][0], kp[tt][1], kp[tt][2], kp[tt][3]);
+    nre_gbwd_enc<(2 * 50 + 15) / 16, P.NSEH>(A, R, dl, stg, X);
+  }
   float4 ey2[P.NTEH], ey1[P.NTE2];
-  nre_gbwd_enc<(2 * 50 + 15) / 16, P.NSEH, 4>(A, R, dl, scr, X, [&]() {
-    nre_load_y(A.ey2, A.ld_ey2, A.He, R, ey2);
-    nre_load_y(A.ey1, A.ld_ey1, A.He, R, ey1);
-  });
+  nre_load_y(A.ey2, A.ld_ey2, A.He, R, ey2);
+  nre_load_y(A.ey1, A.ld_ey1, A.He, R, ey1);
   nre_touch(ey2);
   nre_touch(ey1);
+  // ---- restart the ring at phase B (unit NA + NR_D - NR_G, a group start):
+  // every wave is done with its staging, then the first NR_D - NR_G units as
+  // in the prologue
+  __builtin_amdgcn_s_barrier();
+  C.u = NA + NR_D - NR_G;
+  {
+#pragma unroll
+    for (int i = 0; i < NR_D - NR_G; ++i) {
+      const int u = NA + NR_D - NR_G + i;
+      nr_issue(C, u % NR_D, __builtin_amdgcn_readfirstlane(tab[2 * u]), (int)__builtin_amdgcn_readfirstlane(tab[2 * u + 1]));
+      if ((i % NR_G) == NR_G - 1) {
+        asm volatile("" ::: "memory");
+        nr_st_pad<NR_G * NR_SEPI>(R);
+      }
+    }
+  }
   NR_TR(kNrMaxUnits - 2, 1)
   // ---- phase B: eh^T, e2^T, e1^T
   auto b1 = nre_dense<P.NSEH, P.NTEH, P.NSE2, true, false>(C, X, Y, ey2, A.edY2, A.ld_edY2, A.He, R, kx, p0);
