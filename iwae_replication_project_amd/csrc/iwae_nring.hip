@@ -1372,32 +1372,38 @@ __device__ __forceinline__ auto nre_dense(NrCtx& C, const NrFrag& IN, NrFrag& OU
 // the last one.  Only where no DMA is in flight (hipcc waits vmcnt(0) before
 // an LDS access it cannot tell from the DMA targets).
 template <int V, int N>
-__device__ __forceinline__ void nre_stage_rows(const float* src, int ld, int rows, float* dst) {
+struct NreRows {
   static_assert(N % V == 0, "row width");
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-  constexpr int PER = N / V, NI = (16 * PER + 63) / 64;
-  const int lane = threadIdx.x & 63, w = nr_wave();
-  const int row0 = blockIdx.x * NR_ROWS + w * 16;
-  const __amdgpu_buffer_rsrc_t r = buf_rsrc(src);
+  static constexpr int PER = N / V, NI = (16 * PER + 63) / 64;
   nr_u32x4 v4[V == 4 ? NI : 1];
   u32x2 v2[V == 2 ? NI : 1];
+  // the loads (all issued before any of the LDS writes)
+  __device__ __forceinline__ void load(const float* src, int ld, int rows) {
+    const int lane = threadIdx.x & 63, w = nr_wave();
+    const int row0 = blockIdx.x * NR_ROWS + w * 16;
+    const __amdgpu_buffer_rsrc_t r = buf_rsrc(src);
 #pragma unroll
-  for (int k = 0; k < NI; ++k) {                 // every load first, then the LDS writes
-    const int e = lane + 64 * k, rr = e / PER, c = (e - rr * PER) * V;
-    const int gr = min(row0 + min(rr, 15), rows - 1);
-    const unsigned off = e < 16 * PER ? (unsigned)(gr * ld + c) * 4u : kOOB;
-    if constexpr (V == 4) v4[k] = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-    else v2[k] = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
-  }
-#pragma unroll
-  for (int k = 0; k < NI; ++k) {
-    const int e = lane + 64 * k, rr = e / PER, c = (e - rr * PER) * V;
-    if (e < 16 * PER) {
-      if constexpr (V == 4) *reinterpret_cast<nr_u32x4*>(dst + rr * N + c) = v4[k];
-      else *reinterpret_cast<u32x2*>(dst + rr * N + c) = v2[k];
+    for (int k = 0; k < NI; ++k) {
+      const int e = lane + 64 * k, rr = e / PER, c = (e - rr * PER) * V;
+      const int gr = min(row0 + min(rr, 15), rows - 1);
+      const unsigned off = e < 16 * PER ? (unsigned)(gr * ld + c) * 4u : kOOB;
+      if constexpr (V == 4) v4[k] = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+      else v2[k] = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
     }
   }
-}
+  __device__ __forceinline__ void store(float* dst) const {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      const int e = lane + 64 * k, rr = e / PER, c = (e - rr * PER) * V;
+      if (e < 16 * PER) {
+        if constexpr (V == 4) *reinterpret_cast<nr_u32x4*>(dst + rr * N + c) = v4[k];
+        else *reinterpret_cast<u32x2*>(dst + rr * N + c) = v2[k];
+      }
+    }
+  }
+};
 
 // P1: the prior head's Gaussian backward (tc_gbwd<GBWD_PRIOR>'s arithmetic)
 // on dP's C layout, d % 4 == 0 (a lane's quad is all dmu or all dzs):
@@ -1405,25 +1411,26 @@ __device__ __forceinline__ void nre_stage_rows(const float* src, int ld, int row
 // of 2d features, packed into X's NSO k steps.  (mu | zs) of the wave's rows
 // staged in LDS (stg, [16][2d]: each column is read by a dmu and a dzs quad);
 // h read directly, in batches of NB tiles issued before their stores.
-template <int NT, int NSO, int NB>
-__device__ __forceinline__ void nre_gbwd_prior(const NreLaunch& A, const NrRow& R, float dl, float* stg, NrFrag& X) {
-  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15, d = A.dp;
-  nre_stage_rows<4, 200>(A.Pp, A.ld_Pp, A.rows, stg);             // (dp == 100: nre_shape_ok)
+template <int NT>
+__device__ __forceinline__ void nre_load_h(const NreLaunch& A, const NrRow& R, float4 (&hv)[NT]) {
+  const int g = (threadIdx.x & 63) >> 4, d = A.dp;
   const __amdgpu_buffer_rsrc_t rh = buf_rsrc(A.h1);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int f0 = 16 * t + 4 * g;
+    const bool mu_part = f0 < d, ok = R.valid && f0 < 2 * d;
+    hv[t] = bld4(rh, ok ? (unsigned)(R.grow * A.ld_h1 + (mu_part ? f0 : f0 - d)) * 4u : kOOB);
+  }
+}
+template <int NT, int NSO>
+__device__ __forceinline__ void nre_gbwd_prior(const NreLaunch& A, const NrRow& R, float dl, const float* stg,
+                                               const float4 (&hv)[NT], NrFrag& X) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15, d = A.dp;
   float va[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int t0 = 0; t0 < 2 * NSO; t0 += NB) {
-    float4 hv[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const int t = t0 + b, f0 = 16 * t + 4 * g;
-      const bool mu_part = f0 < d, ok = t < NT && R.valid && f0 < 2 * d;
-      hv[b] = bld4(rh, ok ? (unsigned)(R.grow * A.ld_h1 + (mu_part ? f0 : f0 - d)) * 4u : kOOB);
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const int t = t0 + b, f0 = 16 * t + 4 * g;
-      if (t >= 2 * NSO) break;
+  for (int t = 0; t < 2 * NSO; ++t) {
+    const int f0 = 16 * t + 4 * g;
+    {
       float v[4] = {0.f, 0.f, 0.f, 0.f};
       if (t < NT) {
         const bool mu_part = f0 < d, ok = R.valid && f0 < 2 * d;
@@ -1435,7 +1442,7 @@ __device__ __forceinline__ void nre_gbwd_prior(const NreLaunch& A, const NrRow& 
         for (int i = 0; i < 4; ++i) {
           const float ez = fexp(f4_at(zs, i));
           const float rs = frcp(ez + kScaleEps);
-          const float z = f4_at(hv[b], i) * rs - f4_at(mu, i) * rs;
+          const float z = f4_at(hv[t < NT ? t : 0], i) * rs - f4_at(mu, i) * rs;
           dh[i] = dl * (-z * rs);
           const float x = mu_part ? dl * (z * rs) : (dl * ((z * z - 1.f) * rs)) * ez;
           v[i] = ok ? x : 0.f;
@@ -1542,11 +1549,22 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
   float dl = R.valid ? A.dlw[R.grow] : 0.f;
   asm volatile("" : "+v"(dl));
   NrFrag X, Y;
-  // (the ring is idle: each wave stages in its 16 KiB of it)
-  nre_gbwd_prior<(2 * 100 + 15) / 16, P.NSPH, 7>(A, R, dl, nrs + wave * (NR_SLOT_BF16 / 2), X);
+  // every load of the prologue in one batch (one memory round trip): the prior
+  // head's (mu | zs) rows, h1, phase A's y; then (the ring is idle: each wave
+  // stages in its 16 KiB of it) the LDS copy and P1
+  constexpr int NT1 = (2 * 100 + 15) / 16;
+  float4 hv1[NT1];
   float4 py2[P.NTPH], py1[P.NTP2];
-  nre_load_y(A.py2, A.ld_py2, A.Hp, R, py2);
-  nre_load_y(A.py1, A.ld_py1, A.Hp, R, py1);
+  {
+    NreRows<4, 200> pr;                                   // (dp == 100: nre_shape_ok)
+    pr.load(A.Pp, A.ld_Pp, A.rows);
+    nre_load_h(A, R, hv1);
+    nre_load_y(A.py2, A.ld_py2, A.Hp, R, py2);
+    nre_load_y(A.py1, A.ld_py1, A.Hp, R, py1);
+    float* stg = nrs + wave * (NR_SLOT_BF16 / 2);
+    pr.store(stg);
+    nre_gbwd_prior<NT1, P.NSPH>(A, R, dl, stg, hv1, X);
+  }
   nre_touch(py2);
   nre_touch(py1);
   __syncthreads();                                     // (the table; before the first DMA)
@@ -1577,12 +1595,21 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
   // empty units after phase A: nothing of phase B was requested), every
   // wave is done with the ring -- each stages E1's operands in its 16 KiB
   asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  float4 ey2[P.NTEH], ey1[P.NTE2];
   {
     const int de = A.de;
     float* stg = nrs + wave * (NR_SLOT_BF16 / 2);
-    nre_stage_rows<4, 100>(A.Pe, A.ld_Pe, A.rows, stg);            // (de == 50: nre_shape_ok)
-    nre_stage_rows<2, 50>(A.h2, A.ld_h2, A.rows, stg + 16 * 2 * de);
-    nre_stage_rows<2, 50>(A.e2, A.ld_e2, A.rows, stg + 16 * 3 * de);
+    // one batch of loads: the encoder head's rows, h2, eps2, and phase B's y
+    NreRows<4, 100> pe;                                   // (de == 50: nre_shape_ok)
+    NreRows<2, 50> ph, pe2;
+    pe.load(A.Pe, A.ld_Pe, A.rows);
+    ph.load(A.h2, A.ld_h2, A.rows);
+    pe2.load(A.e2, A.ld_e2, A.rows);
+    nre_load_y(A.ey2, A.ld_ey2, A.He, R, ey2);
+    nre_load_y(A.ey1, A.ld_ey1, A.He, R, ey1);
+    pe.store(stg);
+    ph.store(stg + 16 * 2 * de);
+    pe2.store(stg + 16 * 3 * de);
     float* sG = stg + 16 * 4 * de;                     // [16][52]: p1^T's output, features < 52
 #pragma unroll
     for (int tt = 0; tt < P.NTP1; ++tt)
@@ -1590,9 +1617,6 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
         *reinterpret_cast<float4*>(sG + r * 52 + 16 * tt + 4 * g) = make_float4(kp[tt][0], kp[tt][1], kp[tt][2], kp[tt][3]);
     nre_gbwd_enc<(2 * 50 + 15) / 16, P.NSEH>(A, R, dl, stg, X);
   }
-  float4 ey2[P.NTEH], ey1[P.NTE2];
-  nre_load_y(A.ey2, A.ld_ey2, A.He, R, ey2);
-  nre_load_y(A.ey1, A.ld_ey1, A.He, R, ey1);
   nre_touch(ey2);
   nre_touch(ey1);
   // ---- restart the ring at phase B (unit NA + NR_D - NR_G, a group start):
