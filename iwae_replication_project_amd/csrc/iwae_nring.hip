@@ -1,7 +1,11 @@
-// Weight-ring k-sample forward for the NLL estimator (get_NLL F:463-F:464
-// through get_log_weights F:327-F:351), gfx950: the same per-row work as
-// mega_fwd_kernel (iwae_mega.hip) with the roles of the operands' storage
-// swapped.
+// Weight-ring kernels (gfx950).  This file holds three:
+//   nring_kernel -- the k-sample forward for the NLL estimator (get_NLL
+//     F:463-F:464 through get_log_weights F:327-F:351) and, in train mode, the
+//     forward of a large-batch train step (below);
+//   nrb_kernel   -- that step's output-MLP backward (further down);
+//   nre_kernel   -- its decoder-prior / encoder backward (at the end).
+// nring_kernel does the same per-row work as mega_fwd_kernel (iwae_mega.hip)
+// with the roles of the operands' storage swapped.
 //
 // mega_fwd_kernel keeps a 64-row tile's activations in LDS and streams every
 // weight fragment from L2 into registers, so each CU re-reads the whole model
