@@ -289,6 +289,24 @@ def test_weight_ring_backward_matches_engine_backward(arch, noise):
     assert np.abs(wa - wb).max() <= 5e-5 * steps
 
 
+@pytest.mark.parametrize("B", [20, 100])
+def test_update_kernel_wave_counts_agree(B):
+    """The update kernel in 16-wave (default), 8-wave and 4-wave workgroups:
+    the same tiles, k-step copies summed in the same order, so the same
+    gradient and post-Adam weights up to the staging's rounding-free
+    relayout -- B = 20 (fused update: gradient + Adam + FX / GX copies) and
+    B = 100 (the large-batch slab pass), injected noise."""
+    rng = np.random.default_rng(71)
+    x = (rng.random((B, 784)) < 0.2).astype(np.float32)
+    eps = [rng.standard_normal((50, B, d)).astype(np.float32) for d in ARCH2[2]]
+    ref = _run_steps({"upd_waves": 16}, x, eps)
+    for w in (8, 4):
+        l, gr, wt = _run_steps({"upd_waves": w}, x, eps)
+        assert l == ref[0]
+        np.testing.assert_array_equal(gr, ref[1])
+        np.testing.assert_array_equal(wt, ref[2])
+
+
 def test_weight_ring_train_forward_runs_at_large_batch_only():
     """The ring forward runs from nring_train_rows sample rows (launch counter),
     the engine's forward launch below."""
