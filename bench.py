@@ -14,6 +14,12 @@ k=50) under "large_batch" -- weak scaling at that per-GPU share.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...    (one process per GPU)
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, this process starts
+the N ranks itself (torch.distributed.run as a child process, before any GPU
+call here), relays rank 0's JSON line and exits with the workers' status.
+Under the default backend (nccl = RCCL) N must not exceed the visible GPUs;
+IWAE_DIST_BACKEND=gloo rehearses N ranks on one GPU.
 """
 from __future__ import annotations
 
@@ -21,6 +27,8 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -167,6 +175,67 @@ def cpu_baseline_nll(seconds=8.0, k=5000):
                        f"{el:.1f} s; extrapolates linearly to 10k images")
 
 
+def dist_backend():
+    """nccl (= RCCL over xGMI) unless IWAE_DIST_BACKEND names another one (gloo:
+    the one-GPU rehearsal of N ranks)."""
+    return os.environ.get("IWAE_DIST_BACKEND", "nccl")
+
+
+def visible_gpus():
+    """GPUs this process may use.  torch.cuda.device_count() does not initialise
+    the GPU on this image, so the launcher may call it before spawning ranks."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_command(n, argv, port, script=None):
+    """The child command that runs n ranks of this script on one node."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(n, backend, ngpus):
+    """A world of n ranks needs n GPUs under nccl (one process per GPU); gloo
+    may place every rank on one GPU (rehearsal)."""
+    if n < 1:
+        raise SystemExit(f"--gpus must be >= 1, got {n}")
+    if backend == "nccl" and n > ngpus:
+        raise SystemExit(f"--gpus {n} needs {n} visible GPUs under nccl (RCCL, one process per GPU); "
+                         f"{ngpus} visible. Set IWAE_DIST_BACKEND=gloo to rehearse {n} ranks on fewer GPUs.")
+
+
+def launch_ranks(n, argv, script=None):
+    """Run n ranks as a torch.distributed.run child (never an exec: this
+    process has not touched the GPU and stays the parent); relay rank 0's
+    JSON line to stdout, everything else to stderr; return the exit code."""
+    check_world(n, dist_backend(), visible_gpus())
+    cmd = launcher_command(n, argv, free_port(), script)
+    print("[bench] launching: " + " ".join(cmd), file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    line = None
+    for ln in proc.stdout:
+        if ln.startswith("{") and '"metric"' in ln:
+            line = ln.strip()
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if rc != 0:
+        print(f"[bench] a rank failed (exit {rc})", file=sys.stderr, flush=True)
+        return rc
+    if line is None:
+        print("[bench] rank 0 printed no result line", file=sys.stderr, flush=True)
+        return 1
+    print(line, flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -186,17 +255,28 @@ def main():
     ap.add_argument("--tune", action="append", default=[],
                     help="library tuning knob name=value (include/iwae.h enum iwae_knob), repeatable; A/B runs only")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    dev = local % max(1, torch.cuda.device_count())   # = local on a full node; wraps only in a 1-GPU rehearsal
+    backend = dist_backend()
+    if world != args.gpus:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the {world} ranks that run",
+              file=sys.stderr, flush=True)
+    ngpu = visible_gpus()
+    if world > 1:
+        check_world(world, backend, ngpu)
+    # one process per GPU; only the gloo rehearsal shares a GPU between ranks
+    dev = local if backend == "nccl" or world == 1 else local % max(1, ngpu)
+    if dev >= ngpu:
+        raise SystemExit(f"LOCAL_RANK {local} has no GPU ({ngpu} visible)")
     torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = os.environ.get("IWAE_DIST_BACKEND", "nccl")   # nccl = RCCL; gloo only to rehearse N>1 on one GPU
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
@@ -210,6 +290,12 @@ def main():
     model.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
     if world > 1:
         distributed.enable_data_parallel(model)
+    import ctypes
+    dpw, dpc = ctypes.c_int(0), ctypes.c_int(0)
+    model._call(model._lib.iwae_dp_world(model._h, ctypes.byref(dpw), ctypes.byref(dpc)))
+    rccl_world = dict(torch_world=dist.get_world_size() if world > 1 else 1, backend=backend if world > 1 else None,
+                      library_dp_world=dpw.value, library_rccl_comm_ranks=dpc.value,
+                      train_reduce=(model._dp.comm if model._dp is not None else None))
     xd = model._x(x_all)
     nb = xd.shape[0] // B_PER_GPU
     batches = [xd[i * B_PER_GPU:(i + 1) * B_PER_GPU] for i in range(nb)]
@@ -250,7 +336,6 @@ def main():
     # re-launched K times back to back between two HIP events on the library's
     # stream (the stream it runs on); avg = elapsed / K.  The dominant one (the
     # longest) is priced against its matrix-core peak.
-    import ctypes
 
     def live(kind, epi):
         model._call(model._lib.iwae_profile_gemm(model._h, kind, epi))
@@ -375,8 +460,28 @@ def main():
             dist.all_reduce(tot)
         nll = dict(value=round(args.nll_images / el2, 2), unit="images/s", images=args.nll_images, k=args.nll_k,
                    seconds=round(el2, 4), nll=round(float(-(tot[0] / tot[1]).item()), 4), shard="image",
+                   n_gpus=world, images_per_rank=[distributed.shard_range(args.nll_images, r, world)[1] -
+                                                  distributed.shard_range(args.nll_images, r, world)[0]
+                                                  for r in range(world)],
                    tflops=round(NLL_FLOP_PER_IMAGE * (args.nll_k / 5000) * args.nll_images / el2 / 1e12, 3),
                    precision="bf16x3")
+        if world > 1:
+            # the 1-GPU rate on this node: rank 0 alone over every image (the others wait),
+            # so the sharded rate reads as a fraction of N x the 1-GPU rate
+            barrier()
+            single = None
+            if rank == 0:
+                xa = model._x(xt)
+                torch.cuda.synchronize()
+                t5 = time.perf_counter()
+                model.log_px(xa, args.nll_k)
+                torch.cuda.synchronize()
+                single = args.nll_images / (time.perf_counter() - t5)
+                del xa
+            barrier()
+            if rank == 0:
+                nll.update(one_gpu_value=round(single, 2), frac_of_linear=round(nll["value"] / (world * single), 4),
+                           one_gpu_note="rank 0 alone over all images, same run, after the sharded leg")
 
     # ---- get_training_statistics (F:496-F:526) over the 10k synthetic test images
     # at the model's k: VAE, IWAE, E_q log p(x|h), both KLs, reconstruction loss
@@ -453,6 +558,7 @@ def main():
                        "global_batch": B_PER_GPU * world, "k": K, "parallelism": f"dp{world}",
                        "noise": "device Philox", "graphs": not args.no_graphs},
             "loss": round(loss, 4),
+            "rccl_world": rccl_world,
             "nll": nll,
             "large_batch": large,
             "training_statistics": stats,

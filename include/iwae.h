@@ -138,8 +138,10 @@ enum iwae_knob {
                                       3 the encoder / prior backward on the ring as well (2-layer shape) (3) */
   IWAE_KNOB_WIDE_RT = 25           /* row tiles of 16 per workgroup of the engine's backward launches from
                                       WIDE_ROWS: 1, 2 or 4 (2; the forward launch: 4) */,
-  IWAE_KNOB_UPD_WAVES = 26         /* update kernel workgroup: 16 waves (four per SIMD, each a quarter of a tile's
+  IWAE_KNOB_UPD_WAVES = 26,        /* update kernel workgroup: 16 waves (four per SIMD, each a quarter of a tile's
                                       columns for one k step), 8 or 4 (16) */
+  IWAE_KNOB_NLL_IMGS = 27          /* images per NLL chunk where the call passes chunk 0 (iwae_nll_eps too);
+                                      with NLL_ROWS < imgs * k the chunk's samples split into sample chunks (0: auto) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --
@@ -221,6 +223,10 @@ int iwae_dp_init(iwae_handle* h, int rank, int world, const void* rccl_unique_id
 /* Broadcast parameters, Adam moments and the Adam step from rank 0 over the
  * library communicator (needs iwae_dp_init with an RCCL id); synchronous. */
 int iwae_dp_broadcast_state(iwae_handle* h);
+/* The data-parallel world of the handle: *world = iwae_dp_init's world (1 when
+ * never called), *comm_ranks = the rank count of the library's RCCL
+ * communicator (ncclCommCount), 0 without one.  bench.py reports both. */
+int iwae_dp_world(const iwae_handle* h, int* world, int* comm_ranks);
 
 /* --- evaluation ----------------------------------------------------------- */
 /* get_log_weights (F:327-F:351): lw [dev] [B][k] (image-major). */

@@ -20,6 +20,7 @@ KNOBS = {
     "upd": 8, "upd_rows": 9, "upd_tn32": 10, "upd_slabs": 11, "upd_slab_wg": 12, "dw_target": 13,
     "smallm_rows": 14, "out_x3_rows": 15, "mg_waves": 16, "nll_rows": 17, "wide_rows": 18, "dw_wide": 19, "ld_align": 20,
     "nring": 21, "nring_train": 22, "nring_train_rows": 23, "nring_bwd": 24, "wide_rt": 25, "upd_waves": 26,
+    "nll_imgs": 27,
 }
 LOSS_IDS = {
     "VAE": 0, "IWAE": 1, "VAE_V1": 2, "L_alpha": 3, "L_power_p": 4,
@@ -78,6 +79,7 @@ SIGNATURES = {
     "iwae_dp_unique_id": (c_int, [c_void_p]),
     "iwae_dp_init": (c_int, [H, c_int, c_int, c_void_p]),
     "iwae_dp_broadcast_state": (c_int, [H]),
+    "iwae_dp_world": (c_int, [H, POINTER(c_int), POINTER(c_int)]),
     "iwae_grad_moments": (c_int, [H, FP, FP]),
     "iwae_export_internal": (c_int, [H, FP, FP, c_longlong]),
     "iwae_log_weights": (c_int, [H, FP, c_int, c_int, FPP, c_int, FP]),

@@ -643,6 +643,7 @@ struct TcJob {
   TcOp op[kTcMaxOps]; int nop;
   int buf_off[kTcMaxBufs], buf_ld[kTcMaxBufs];   // bf16 offset of the hi plane / row stride
   float* logq; float* logp; float* bern; int ld_bern, bern_col;   // per-row sums this job writes (null: none)
+  int bern_ncol;              // jobs that split the Bernoulli columns (1: this job alone also zeroes column 1)
   float* bce;                 // L_alpha: per-row Keras-BCE sums (same layout as bern)
 };
 struct TcPlan {              // device resident (built once per shape)

@@ -203,6 +203,7 @@ struct iwae_handle {
   long long dw_target = 768;         // split-K target workgroups per layer of the grouped weight-gradient GEMMs
   int smallm_rows = 32;              // first encoder layer on the few-row launches up to this many images (0: never)
   long long nll_rows = 1LL << 20;    // sample rows per NLL chunk (measured fastest: 2^17-2^20 within 10 %)
+  int nll_imgs = 0;                  // images per NLL chunk when the caller passes chunk 0 (0: nll_rows / k)
   int tc_rt = 1;                     // row tiles of 16 per engine workgroup below wide_rows
   int ld_align = 4;                  // workspace row strides: multiples of this many floats (4 or 32)
   long long wide_rows = 4097;        // sample rows from which the engine runs 32 / 64-row workgroups
@@ -1649,7 +1650,15 @@ static bool use_engine(const iwae_handle* h, const Plan& P) {
   if (!h->engine || !h->x3 || h->path == 1 || h->path == 2 || h->masked) return false;
   if (P.kl) return false;       // VAE_V1's analytic KL: fused row-block path
   if (h->L > kTcMaxLayers || h->enc[0].d > 2048) return false;   // (image-row backward: d / 4 column quads)
-  return (long long)P.Bimg * P.kS <= (1LL << 18);
+  const long long rows = (long long)P.Bimg * P.kS;
+  if (rows > (1LL << 18)) return false;
+  // the engine and the ring kernels address each activation / gradient matrix
+  // through one buffer resource (32-bit byte offsets, range < 2^31): every
+  // matrix they write must stay below 2 GiB, else the row-block path runs
+  long long w = h->xdim;
+  for (const DenseL& d : h->dense) w = std::max<long long>(w, std::max(d.fout, d.fin + 1));
+  w = (w + 31) / 32 * 32;
+  return rows * w * (long long)sizeof(float) < (1LL << 31);
 }
 
 struct TcBuild {
@@ -1826,7 +1835,7 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
       const int t0 = part * (ntile / nsplit), t1 = part + 1 == nsplit ? ntile : (part + 1) * (ntile / nsplit);
       c.t0 = t0;
       if (t1 < ntile) c.N = 16 * t1;
-      B.J.bern = h->ebern; B.J.ld_bern = 4; B.J.bern_col = part;
+      B.J.bern = h->ebern; B.J.ld_bern = 4; B.J.bern_col = part; B.J.bern_ncol = nsplit;
       B.J.bce = P.need_bce ? h->ebce : nullptr;
       if (L == 1 && first) { B.J.logq = h->logq; B.J.logp = h->logp; }
       jobs.push_back(B);
@@ -2625,6 +2634,9 @@ int iwae_set_graphs(iwae_handle* h, int enable) {
 int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
   if (!h) return IWAE_EINVAL;
   const bool on = value != 0;
+  // kernels already queued on the handle's stream may still read the arena and
+  // the plan tables that some knobs free below
+  HIPCHK(hipStreamSynchronize(h->stream));
   switch (knob) {
     case IWAE_KNOB_ENGINE: h->engine = on; break;
     case IWAE_KNOB_TC_IMG: h->engine_img = on; break;
@@ -2652,6 +2664,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
       h->mg_waves = (int)value;
       break;
     case IWAE_KNOB_NLL_ROWS: h->nll_rows = std::max(1LL, value); break;
+    case IWAE_KNOB_NLL_IMGS: h->nll_imgs = (int)std::max(0LL, std::min(value, 1LL << 20)); break;
     case IWAE_KNOB_WIDE_ROWS: h->wide_rows = std::max(0LL, value); break;
     case IWAE_KNOB_DW_WIDE: h->dw_wide = on; break;
     case IWAE_KNOB_NRING: h->nring = on; break;
@@ -2669,7 +2682,6 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     default: return fail(h, IWAE_EINVAL, "unknown tuning knob " + std::to_string(knob));
   }
   // captured steps and engine plans were built for the previous setting
-  HIPCHK(hipStreamSynchronize(h->stream));
   for (auto& kv : h->graphs) destroy_graph(kv.second);
   h->graphs.clear();
   for (auto& kv : h->tc_plans) (void)hipFree(kv.second.dev);
@@ -2883,6 +2895,15 @@ int iwae_dp_broadcast_state(iwae_handle* h) {
     return fail(h, IWAE_EHIP, std::string("ncclBroadcast: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
   HIPCHK(hipStreamSynchronize(h->stream));
   h->params_version++;
+  return IWAE_OK;
+}
+
+int iwae_dp_world(const iwae_handle* h, int* world, int* comm_ranks) {
+  if (!h || !world || !comm_ranks) return IWAE_EINVAL;
+  *world = h->dp_world;
+  int n = 0;
+  if (h->comm && ncclCommCount(h->comm, &n) != ncclSuccess) n = -1;
+  *comm_ranks = n;
   return IWAE_OK;
 }
 
@@ -3260,6 +3281,7 @@ static int nll_core(iwae_handle* h, const float* x, int N, int k, int chunk, flo
   // 2^20 sample rows per chunk (measured fastest: 2^17-2^20 within 10 %, smaller slower)
   const long long nll_rows = h->nll_rows;
   const long long target_rows = std::max<long long>(nll_rows, k);
+  if (chunk <= 0) chunk = h->nll_imgs;
   int imgs = chunk > 0 ? chunk : (int)std::max<long long>(1, target_rows / k);
   imgs = std::min(imgs, N);
   const int kS = (int)std::min<long long>(k, std::max<long long>(1, target_rows / imgs));

@@ -879,7 +879,8 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
     if (TR) {
       A.logq[grow_raw] = q;
       A.logp[grow_raw] = p;
-      A.bern[(size_t)grow_raw * A.ld_bern] = b;
+      // columns 0-1 (the bound sums both): column 1 cleared, a split engine launch may have written it
+      *reinterpret_cast<float2*>(A.bern + (size_t)grow_raw * A.ld_bern) = make_float2(b, 0.f);
     } else {
       A.lw[grow_raw] = (p + b) - q;          // log w = log p(h) + log p(x|h) - log q(h|x)
     }

@@ -1244,8 +1244,15 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
     const int rg = row0 + t;
     if (J.logq) J.logq[rg] = rq[t] + s4[0];
     if (J.logp) J.logp[rg] = rp[t] + s4[1];
-    if (J.bern) J.bern[(size_t)rg * J.ld_bern + J.bern_col] = kLn2 * s4[2];
-    if (J.bce) J.bce[(size_t)rg * J.ld_bern + J.bern_col] = kLn2 * s4[3];
+    // the bound sums columns 0-1 of a row: a single-split job clears column 1,
+    // which a split launch of another (smaller) shape may have written earlier
+    if (J.bern_ncol == 1) {
+      if (J.bern) *reinterpret_cast<float2*>(J.bern + (size_t)rg * J.ld_bern) = make_float2(kLn2 * s4[2], 0.f);
+      if (J.bce) *reinterpret_cast<float2*>(J.bce + (size_t)rg * J.ld_bern) = make_float2(kLn2 * s4[3], 0.f);
+    } else {
+      if (J.bern) J.bern[(size_t)rg * J.ld_bern + J.bern_col] = kLn2 * s4[2];
+      if (J.bce) J.bce[(size_t)rg * J.ld_bern + J.bern_col] = kLn2 * s4[3];
+    }
   }
 }
 
