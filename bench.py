@@ -305,6 +305,17 @@ def main():
             dist.barrier()
 
     def run(n, off=0):
+        # fit's batch loop (E:82): consecutive batches of the resident set, one
+        # library call per contiguous run (iwae_train_steps: up to 32 steps per graph)
+        while n > 0:
+            o = off % nb
+            m = min(n, nb - o)
+            model.train_steps(xd[o * B_PER_GPU:(o + m) * B_PER_GPU], B_PER_GPU, sync=False)
+            n -= m
+            off += m
+
+    def run_calls(n, off=0):
+        # the same steps as one train_step call each (F:221 per call)
         for i in range(n):
             model.train_step(batches[(off + i) % nb], sync=False)
 
@@ -325,10 +336,27 @@ def main():
         t = torch.tensor([el], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    loss = float(model._loss_buf.item())
     rows = world * B_PER_GPU * K * args.steps
     value = rows / el
     ms_per_step = 1e3 * el / args.steps
+    # the same number of steps as one train_step call each (host issue + one graph per step)
+    run_calls(min(args.warmup, 10), args.warmup + args.steps)
+    model._stream.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    tc0 = time.perf_counter()
+    run_calls(args.steps, 2 * args.warmup + args.steps)
+    model._stream.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    elc = time.perf_counter() - tc0
+    if world > 1:
+        t = torch.tensor([elc], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elc = float(t.item())
+    loss = float(model._loss_buf.item())
+    per_call = dict(ms_per_step=round(1e3 * elc / args.steps, 5), value=round(rows / elc, 1),
+                    note="the same steps issued as one train_step (F:221) call each: one graph launch per step")
 
     # ---- dominant kernel live timing.  Candidates: the train engine's forward and
     # backward launches (iwae_train.hip) and, where the step still uses it, the
@@ -556,8 +584,11 @@ def main():
             "config": {"workload": "IWAE train step (fwd+bound+bwd+Adam), k=50, 2 stochastic layers "
                                    "784-200-200-100-100-50, batch 20 per GPU (BASELINE configs[1])",
                        "global_batch": B_PER_GPU * world, "k": K, "parallelism": f"dp{world}",
-                       "noise": "device Philox", "graphs": not args.no_graphs},
+                       "noise": "device Philox", "graphs": not args.no_graphs,
+                       "loop": "fit's batch loop (E:82): consecutive batches through Flexible_Model.train_steps "
+                               "(iwae_train_steps, up to 32 captured steps per graph launch)"},
             "loss": round(loss, 4),
+            "train_step_calls": per_call,
             "rccl_world": rccl_world,
             "nll": nll,
             "large_batch": large,

@@ -179,6 +179,14 @@ int iwae_set_adam_state(iwae_handle* h, const float* m_host, const float* v_host
  * scalar loss (= -bound, the value train_step returns in {loss: ...}). */
 int iwae_train_step(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,
                     const float* const* eps, int n_eps, float* loss_dev);
+/* fit's batch loop (E:82 -> F:221-F:247 per batch): nsteps consecutive train
+ * steps with device Philox noise on the batches x + i*B*x_dim, i < nsteps
+ * (x [dev] holds nsteps*B images); loss_dev [dev, may be NULL] receives
+ * nsteps losses.  Same arithmetic as nsteps iwae_train_step calls; with graphs
+ * on, consecutive steps replay from one captured graph of up to 32 steps (no
+ * launch gap between them). */
+int iwae_train_steps(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B, int nsteps,
+                     float* loss_dev);
 /* The same without the Adam update (gradient kept on device).  For data
  * parallelism: forward_backward -> all-reduce(grad buffer) -> apply_adam. */
 int iwae_forward_backward(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,

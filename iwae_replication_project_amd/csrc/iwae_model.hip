@@ -217,6 +217,10 @@ struct iwae_handle {
     hipGraphNode_t x_node = nullptr;
     SmArgs x_args{};
     const float* x_cap = nullptr;
+    // multi-step graphs (iwae_train_steps): one input-layer launch per captured step
+    std::vector<hipGraphNode_t> xs_node;
+    std::vector<SmArgs> xs_args;
+    std::vector<const float*> xs_cap;
   };
   std::map<std::vector<long long>, GraphRec> graphs;
   const float* x_user = nullptr;       // train step: caller's x read directly by the first kernel
@@ -225,6 +229,7 @@ struct iwae_handle {
   SmArgs cap_x_args{};
   // live kernel timing (HIP events around every launch of one GEMM class)
   float* loss_out = nullptr;           // train-step loss destination (part of the graph key)
+  float* loss_slots = nullptr;         // multi-step graphs: step j's loss (kGraphSteps floats)
   int prof_kind = -1, prof_epi = -1;
   std::vector<hipEvent_t> prof_ev;
   size_t prof_used = 0;
@@ -2405,6 +2410,123 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
   return IWAE_OK;
 }
 
+// consecutive Philox train steps on the batches x + i * B * x_dim (fit's loop,
+// E:82): graphs of up to kGraphSteps captured steps, so consecutive steps run
+// without the per-graph launch gap; step j of a graph reads its own batch (its
+// input-layer launch re-pointed when the batch moves) and writes its loss to
+// loss_slots[j], copied to loss_dev + i after the graph.  Anything the
+// multi-step graph does not cover (no graphs, staged x, data parallel, live
+// profiling) runs as nsteps single steps.
+static constexpr int kGraphSteps = 32;
+
+static int do_train_steps(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B, int nsteps,
+                          float* loss_dev) {
+  if (!x) return fail(h, IWAE_EINVAL, "x is NULL");
+  if (nsteps < 0) return fail(h, IWAE_EINVAL, "nsteps must be >= 0");
+  if (nsteps == 0) return IWAE_OK;
+  const long long xstride = (long long)B * h->xdim;
+  // (single steps write the loss to the handle's scalar, then copy it: one
+  // captured graph per shape, not one per loss address)
+  auto single = [&]() -> int {
+    for (int i = 0; i < nsteps; ++i) {
+      CHK(do_train(h, lc, x + i * xstride, B, nullptr, 0, nullptr, true));
+      if (loss_dev)
+        HIPCHK(hipMemcpyAsync(loss_dev + i, &h->ds->scalars[0], sizeof(float), hipMemcpyDeviceToDevice, h->stream));
+    }
+    return IWAE_OK;
+  };
+  if (nsteps == 1 || !h->use_graphs || h->prof_kind >= 0 || h->dp_weighted) return single();
+  Plan P;
+  CHK(make_plan(h, lc, B, P));
+  EpsSet E;
+  CHK(parse_eps(h, P, nullptr, 0, E));
+  CHK(ensure_capacity(h, P.Bimg, P.Bimg * P.kS, true));
+  const bool engine = use_engine(h, P);
+  // (the engine step refreshes every copy it reads inside the step; other
+  // paths decide their split-copy refreshes on the host at capture time)
+  const bool direct = P.Bimg == P.B && engine && smallm_ok(h, P.Bimg);
+  if (!direct) return single();
+  {
+    CHK(ensure_fx(h));
+    CHK(tc_prepare(h, P));
+    NrLaunch nr;
+    NrbLaunch nb;
+    NreLaunch ne;
+    if (nring_plan(h, nr) && nrb_plan(h, nb) && h->L >= 2) {
+      CHK(tc_prepare_one(h, P, 5));
+      (void)nre_plan(h, ne);
+    }
+  }
+  if (!h->loss_slots) HIPCHK(hipMalloc(&h->loss_slots, kGraphSteps * sizeof(float)));
+  h->in_train_step = true;
+  struct Reset {
+    iwae_handle* h;
+    ~Reset() {
+      h->in_train_step = false; h->out_x3 = false; h->x_user = nullptr; h->capturing = false; h->loss_out = nullptr;
+    }
+  } reset_flag{h};
+  for (int i0 = 0; i0 < nsteps; i0 += kGraphSteps) {
+    const int S = std::min(kGraphSteps, nsteps - i0);
+    const float* xi = x + i0 * xstride;
+    std::vector<long long> key = {2, lc->loss, B, lc->k, lc->k1, lc->k2, S, 1};
+    float fk[3] = {lc->p, lc->alpha, lc->beta};
+    for (float f : fk) {
+      int bits;
+      std::memcpy(&bits, &f, 4);
+      key.push_back(bits);
+    }
+    auto it = h->graphs.find(key);
+    if (it == h->graphs.end()) {
+      iwae_handle::GraphRec g;
+      hipGraph_t graph;
+      h->capturing = true;
+      HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
+      int rc = IWAE_OK;
+      for (int j = 0; j < S && rc == IWAE_OK; ++j) {
+        h->x_user = xi + j * xstride;
+        h->loss_out = h->loss_slots + j;
+        h->cap_x_node = nullptr;
+        rc = train_body(h, P, E, true);
+        g.xs_node.push_back(h->cap_x_node);
+        g.xs_args.push_back(h->cap_x_args);
+        g.xs_cap.push_back(h->x_user);
+      }
+      hipError_t ec = hipStreamEndCapture(h->stream, &graph);
+      h->capturing = false;
+      if (rc != IWAE_OK) return rc;
+      HIPCHK(ec);
+      g.graph = graph;
+      HIPCHK(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
+      for (hipGraphNode_t n : g.xs_node)
+        if (!n) {
+          destroy_graph(g);
+          return fail(h, IWAE_EHIP, "multi-step capture: input-layer launch not found");
+        }
+      it = h->graphs.emplace(key, g).first;
+    }
+    iwae_handle::GraphRec& g = it->second;
+    for (int j = 0; j < S; ++j) {
+      const float* xj = xi + j * xstride;
+      if (g.xs_cap[j] == xj) continue;
+      hipKernelNodeParams kp;
+      HIPCHK(hipGraphKernelNodeGetParams(g.xs_node[j], &kp));
+      SmArgs na = g.xs_args[j];
+      na.A = xj;
+      void* args[] = {&na};
+      kp.kernelParams = args;
+      kp.extra = nullptr;
+      HIPCHK(hipGraphExecKernelNodeSetParams(g.exec, g.xs_node[j], &kp));
+      g.xs_cap[j] = xj;
+    }
+    HIPCHK(hipGraphLaunch(g.exec, h->stream));
+    if (loss_dev)
+      HIPCHK(hipMemcpyAsync(loss_dev + i0, h->loss_slots, S * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
+    h->params_version++;
+    h->fx_version = h->params_version;   // every replayed step refreshed the fragment-major copies
+  }
+  return IWAE_OK;
+}
+
 // ---------------------------------------------------------------- ABI
 extern "C" {
 
@@ -2530,6 +2652,7 @@ void iwae_destroy(iwae_handle* h) {
   if (h->adam_v) (void)hipFree(h->adam_v);
   if (h->grad_own) (void)hipFree(h->grad_own);
   if (h->ds) (void)hipFree(h->ds);
+  if (h->loss_slots) (void)hipFree(h->loss_slots);
   if (h->nr_units) (void)hipFree(h->nr_units);
   if (h->nrb_units) (void)hipFree(h->nrb_units);
   if (h->nre_units) (void)hipFree(h->nre_units);
@@ -2791,6 +2914,13 @@ int iwae_train_step(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
                     const float* const* eps, int n_eps, float* loss_dev) {
   if (!h) return IWAE_EINVAL;
   return do_train(h, lc, x, B, eps, n_eps, loss_dev, true);
+}
+
+int iwae_train_steps(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B, int nsteps,
+                     float* loss_dev) {
+  if (!h) return IWAE_EINVAL;
+  if (!lc) return fail(h, IWAE_EINVAL, "loss config is NULL");
+  return do_train_steps(h, lc, x, B, nsteps, loss_dev);
 }
 
 int iwae_forward_backward(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,

@@ -370,9 +370,40 @@ class Flexible_Model:
         self._stream.synchronize()
         return {self.loss_function: float(self._loss_buf.item())}
 
+    def train_steps(self, x, batch_size, sync=True):
+        """len(x) // batch_size consecutive train steps (F:221-F:247 each) on the
+        batches x[i*batch_size:(i+1)*batch_size] with device noise: fit's inner
+        loop (E:82) as one library call (iwae_train_steps: up to 32 steps per
+        captured graph).  Returns the per-step losses (device tensor if
+        sync=False)."""
+        if self.optimizer is None:
+            self.compile()
+        xd = self._x(x)
+        B = int(batch_size)
+        if B <= 0:
+            raise ValueError("batch_size must be positive")
+        n = xd.shape[0] // B
+        with torch.cuda.stream(self._stream):
+            losses = torch.empty(n, device=self.device)
+        if n == 0:
+            return losses if not sync else losses.cpu().numpy()
+        if self._dp is not None and self._dp.comm != "library":
+            for i in range(n):
+                self._dp.step(self, self._lc(), xd[i * B:(i + 1) * B], B, None, 0)
+                with torch.cuda.stream(self._stream):
+                    losses[i] = self._loss_buf[0]
+        else:
+            self._call(self._lib.iwae_train_steps(self._h, self._lc(), _lib.fptr(xd), B, n, _lib.fptr(losses)))
+        self.epoch += n                                                   # F:245, per step
+        if not sync:
+            return losses
+        self._stream.synchronize()
+        return losses.cpu().numpy()
+
     def fit(self, x, epochs=1, batch_size=100, shuffle=True, verbose=0, seed=None):
         """Keras-style loop (E:82): per epoch shuffle, batches of batch_size
-        (last partial batch included), one train_step each."""
+        (last partial batch included), one train step each (the whole batches
+        through train_steps, the partial one through train_step)."""
         xd = self._x(x)
         N = xd.shape[0]
         g = torch.Generator(device="cpu")
@@ -384,10 +415,15 @@ class Flexible_Model:
             with torch.cuda.stream(self._stream):
                 xs = xd[perm.to(self.device)] if shuffle else xd
                 losses = torch.zeros((N + batch_size - 1) // batch_size, device=self.device)
-            for i, s in enumerate(range(0, N, batch_size)):
-                out = self.train_step(xs[s:s + batch_size], sync=False)[self.loss_function]
+            nfull = N // batch_size
+            if nfull:
+                full = self.train_steps(xs[:nfull * batch_size], batch_size, sync=False)
                 with torch.cuda.stream(self._stream):
-                    losses[i] = out[0]
+                    losses[:nfull] = full
+            if N % batch_size:
+                out = self.train_step(xs[nfull * batch_size:], sync=False)[self.loss_function]
+                with torch.cuda.stream(self._stream):
+                    losses[nfull] = out[0]
             self._stream.synchronize()
             hist.append(float(losses.mean().item()))
             if verbose:

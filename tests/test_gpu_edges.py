@@ -227,3 +227,35 @@ def test_alternating_split_and_single_split_output_jobs_leave_no_stale_rows(big)
     torch.cuda.synchronize()
     assert la == lb, (la, lb)
     assert np.array_equal(ga, gb)
+
+
+@pytest.mark.parametrize("B,n", [(20, 11), (20, 40), (7, 3), (64, 9)])
+def test_train_steps_equal_single_step_calls(B, n):
+    """fit's batch loop as one call (iwae_train_steps: graphs of up to 8
+    captured steps, each re-pointed at its own batch) equals n train_step
+    calls -- captured one step per graph, and eager -- bit for bit: per-step
+    losses, the final weights and Adam state (same seed, same Philox stream).
+    Shapes: the bench's B=20 (11 steps: one graph; 40 = 32 + 8: two graphs of
+    different length), a ragged 7, and 64 images (image-row jobs, single steps)."""
+    import torch
+    rng = np.random.default_rng(11 + B + n)
+    xs = (rng.random((n * B + 5, 784)) < 0.25).astype(np.float32)
+    runs = []
+    for mode in ("steps", "calls", "eager"):
+        m = _model(ARCH2, "IWAE", 50, use_graphs=mode != "eager")
+        X = torch.from_numpy(xs).to(m.device)
+        if mode == "steps":
+            # twice over the same batches: the second call replays the graphs it captured
+            l1 = m.train_steps(X[:n * B], B)
+            l2 = m.train_steps(X[5:5 + n * B], B)          # shifted batches: every input launch re-pointed
+            losses = list(l1) + list(l2)
+        else:
+            losses = [m.train_step(X[i * B:(i + 1) * B])["IWAE"] for i in range(n)]
+            losses += [m.train_step(X[5 + i * B:5 + (i + 1) * B])["IWAE"] for i in range(n)]
+        mm, vv, st = m.get_optimizer_state()
+        runs.append((np.asarray(losses, np.float32), _flat(m.get_weights()), mm, st))
+    for r in runs[1:]:
+        np.testing.assert_array_equal(runs[0][0], r[0])
+        np.testing.assert_array_equal(runs[0][1], r[1])
+        np.testing.assert_array_equal(runs[0][2], r[2])
+        assert runs[0][3] == r[3] == 2 * n
