@@ -128,7 +128,7 @@ enum iwae_knob {
   IWAE_KNOB_MG_WAVES = 16,     /* NLL kernel workgroup: 8 waves / 64 rows or 4 waves / 32 rows (8) */
   IWAE_KNOB_NLL_ROWS = 17,     /* sample rows per NLL chunk (2^20) */
   IWAE_KNOB_WIDE_ROWS = 18,    /* engine: 32 / 64-row workgroups from this many sample rows (4097) */
-  IWAE_KNOB_DW_WIDE = 19,      /* beyond UPD_ROWS: weight gradients on the 112 x 256-block kernel (0) */
+  IWAE_KNOB_DW_WIDE = 19,      /* beyond UPD_ROWS: weight gradients on the 208 x 128-block kernel (0) */
   IWAE_KNOB_LD_ALIGN = 20,     /* workspace row strides: multiples of 4, 8, 16 or 32 floats (4) */
   IWAE_KNOB_NRING = 21,        /* NLL: the weight-ring kernel where its model shapes apply (1) */
   IWAE_KNOB_NRING_TRAIN = 22,  /* train-step forward on the weight-ring kernel (1) ... */
@@ -140,8 +140,9 @@ enum iwae_knob {
                                       WIDE_ROWS: 1, 2 or 4 (2; the forward launch: 4) */,
   IWAE_KNOB_UPD_WAVES = 26,        /* update kernel workgroup: 16 waves (four per SIMD, each a quarter of a tile's
                                       columns for one k step), 8 or 4 (16) */
-  IWAE_KNOB_NLL_IMGS = 27          /* images per NLL chunk where the call passes chunk 0 (iwae_nll_eps too);
+  IWAE_KNOB_NLL_IMGS = 27,         /* images per NLL chunk where the call passes chunk 0 (iwae_nll_eps too);
                                       with NLL_ROWS < imgs * k the chunk's samples split into sample chunks (0: auto) */
+  IWAE_KNOB_DW_WG = 28             /* workgroups the DW_WIDE weight-gradient pass balances its row chunks over (256) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --

@@ -368,19 +368,18 @@ hipError_t upd_setup_attributes();
 
 // Large-batch weight gradients into split-K slabs (iwae_dwgrad.hip): per layer,
 // workgroup blocks of 7 x 16 W_aug rows by 8 * nb x 16 columns over a row chunk.
-constexpr int kDwMT = 7;                              // 16-row tiles of W_aug rows per block
 struct DwJob {
   const float* A; const float* B; const float* ks;   // X_aug [rows][lda] (ones column at fin), dZ [rows][ldb], dZ row scale
   int lda, ldb, rows;
   float* out; int ldo; long long slab_stride;        // slab s at out + s * slab_stride: [M][ldo]
-  int M, mt, nt;                                     // M = fin + 1; 16-tiles along M and along fout
-  int nb, mblocks, nblocks;                          // n-tiles per wave (1 or 2); blocks along M / N
+  int M, N, mt, nt;                                  // M = fin + 1, N = fout; 16-tiles along M / N
+  int mtb, ntb, nib, njb;                            // tiles per block (<= 13 / <= 8), blocks along M / N
   int nsplit, chunk;                                 // row chunks (chunk % 32 == 0)
-  int tile0;                                         // first workgroup of the job (split-major)
+  int item0;                                         // first work item of the job (chunk-major, then N, then M block)
 };
 constexpr int kDwMaxJobs = 20;
 struct DwArgs {
-  DwJob job[kDwMaxJobs]; int njobs, ntiles;
+  DwJob job[kDwMaxJobs]; int njobs, nitems, per_xcd;
 };
 hipError_t launch_dw(hipStream_t st, const DwArgs& a);
 hipError_t dw_setup_attributes();

@@ -37,6 +37,7 @@ struct DenseL {
   int ldF = 0, ldG = 0;
   long long size() const { return (long long)(fin + 1) * ldw; }
   int max_splits = 1, splits = 1;
+  int cap_splits = 1;                  // slabs allocated (>= max_splits: the large-batch weight-gradient pass may use more)
   long long slab_off = 0;
   int rows_kind = 1;           // 0: image rows (encoder layer 0), 1: sample rows
   int head_d = 0;              // a stochastic layer's (mu | zs) head: its latent width
@@ -198,12 +199,12 @@ struct iwae_handle {
   int upd_tn32 = 0;                  // ... sample-row layers in 64 x 32 tiles
   int upd_slabs = 1;                 // ... and beyond upd_rows its split-K gradient pass into the slabs
   long long upd_slab_wg = 512;       // sample-row workgroups of that pass
-  int dw_wide = 0;                   // ... run by the 112 x 256-block weight-gradient kernel (iwae_dwgrad.hip;
-                                     // measured slower than the update kernel's pass: 223 vs 190 us at B = 512)
+  int dw_wide = 0;                   // ... run by the 208 x 128-block weight-gradient kernel (iwae_dwgrad.hip)
   long long dw_target = 768;         // split-K target workgroups per layer of the grouped weight-gradient GEMMs
   int smallm_rows = 32;              // first encoder layer on the few-row launches up to this many images (0: never)
   long long nll_rows = 1LL << 20;    // sample rows per NLL chunk (measured fastest: 2^17-2^20 within 10 %)
   int nll_imgs = 0;                  // images per NLL chunk when the caller passes chunk 0 (0: nll_rows / k)
+  int dw_wg = 256;                   // large-batch weight-gradient pass: workgroups its row chunks aim at
   int tc_rt = 1;                     // row tiles of 16 per engine workgroup below wide_rows
   int ld_align = 4;                  // workspace row strides: multiples of this many floats (4 or 32)
   long long wide_rows = 4097;        // sample rows from which the engine runs 32 / 64-row workgroups
@@ -421,8 +422,10 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
       // more slabs only add write + read traffic at large batch)
       S = std::min(S, std::min(16LL, std::max(1LL, cdiv(R, 64))));
       d.max_splits = (int)S;
+      // the large-batch weight-gradient pass (run_dw) balances its workgroups with up to 32 row chunks
+      d.cap_splits = (int)std::max<long long>(S, std::min(32LL, std::max(1LL, cdiv(R, 32))));
       d.slab_off = (long long)slab_total;
-      slab_total += (size_t)((d.size() * S + 63) & ~63LL);
+      slab_total += (size_t)((d.size() * d.cap_splits + 63) & ~63LL);
     }
   }
   size_t slab_base = take(slab_total);
@@ -1575,9 +1578,12 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int bucket = 0, 
 }
 
 // Large-batch weight gradients (iwae_dwgrad.hip): every layer's X_aug^T dZ in
-// 112 x (128 | 256) blocks split over row chunks into the slabs adam_kernel
-// sums; the chunks are sized so every workgroup has about the same MFMA work
-// (one round of the chip, one workgroup per CU), the heaviest layers first.
+// blocks of up to 208 x 128 (13 x 8 MFMA tiles) split over row chunks into the
+// slabs adam_kernel sums.  Blocks of one layer are as even as the tile counts
+// allow; row chunks are sized so every workgroup has about the same MFMA work
+// (about one workgroup per CU: 96 KiB of LDS each), at most cap_splits slabs per
+// layer; work items are ordered chunk-major so one row chunk's blocks share an
+// XCD (and its L2).
 static int run_dw(iwae_handle* h, const Plan& P) {
   const int L = h->L, M = P.Bimg * P.kS;
   struct WJ { int di; const Mat* A; const Mat* dZ; int rows; const float* ks; };
@@ -1601,26 +1607,20 @@ static int run_dw(iwae_handle* h, const Plan& P) {
   if ((int)js.size() > kDwMaxJobs) return fail(h, IWAE_EINVAL, "weight-gradient pass: too many layers");
   DwArgs a;
   std::memset(&a, 0, sizeof(a));
-  // MFMA work of a block per row: its m-tiles x the busiest wave's n-tiles
-  auto block_cost = [](int mt_blk, int nt_blk, int nb) {
-    const int per_wave = nb == 2 ? (nt_blk > 8 ? 2 : 1) : 1;
-    return (double)std::min(mt_blk, kDwMT) * per_wave;
-  };
-  std::vector<double> cost(js.size(), 0.0);
   double W = 0.0;
+  std::vector<double> cost(js.size(), 0.0);        // MFMA tiles of one block per k step
   for (size_t q = 0; q < js.size(); ++q) {
     const DenseL& d = h->dense[js[q].di];
     DwJob& J = a.job[q];
-    J.M = d.fin + 1; J.mt = (int)cdiv(J.M, 16); J.nt = (int)cdiv(d.fout, 16);
-    J.nb = J.nt > 8 ? 2 : 1;
-    J.mblocks = (int)cdiv(J.mt, kDwMT); J.nblocks = (int)cdiv(J.nt, 8 * J.nb);
-    for (int mb = 0; mb < J.mblocks; ++mb)
-      for (int nbk = 0; nbk < J.nblocks; ++nbk)
-        cost[q] += block_cost(J.mt - kDwMT * mb, std::min(8 * J.nb, J.nt - 8 * J.nb * nbk), J.nb);
-    W += cost[q] * js[q].rows;
+    J.M = d.fin + 1; J.N = d.fout;
+    J.mt = (int)cdiv(J.M, 16); J.nt = (int)cdiv(J.N, 16);
+    J.nib = (int)cdiv(J.mt, 13); J.mtb = (int)cdiv(J.mt, J.nib);
+    J.njb = (int)cdiv(J.nt, 8); J.ntb = (int)cdiv(J.nt, J.njb);
+    cost[q] = (double)J.mtb * J.ntb;
+    W += cost[q] * J.nib * J.njb * (double)cdiv(js[q].rows, 32);
   }
-  const double target = W / 256.0;                 // per-workgroup work: one round of the chip
-  int tiles = 0;
+  const double target = W / (double)h->dw_wg;      // block-k-steps of tiles per workgroup
+  int items = 0;
   for (size_t q = 0; q < js.size(); ++q) {
     const WJ& w = js[q];
     DenseL& d = h->dense[w.di];
@@ -1628,18 +1628,19 @@ static int run_dw(iwae_handle* h, const Plan& P) {
     J.A = w.A->p; J.lda = w.A->ld; J.B = w.dZ->p; J.ldb = w.dZ->ld; J.ks = w.ks ? w.ks : h->ones;
     J.rows = w.rows;
     J.out = h->slabs + d.slab_off; J.ldo = d.ldw; J.slab_stride = d.size();
-    const double per_block = cost[q] / (J.mblocks * J.nblocks);
-    long long S = std::llround(w.rows * per_block / std::max(target, 1.0));
-    S = std::max(1LL, std::min<long long>(S, d.max_splits));
+    const double ksteps = (double)cdiv(w.rows, 32);
+    long long S = std::llround(ksteps * cost[q] / std::max(target, 1.0));
+    S = std::max(1LL, std::min<long long>(S, d.cap_splits));
     const long long chunk = cdiv(cdiv(w.rows, S), 32) * 32;
     S = cdiv(w.rows, chunk);
     J.nsplit = (int)S; J.chunk = (int)chunk;
     d.splits = (int)S;
-    J.tile0 = tiles;
-    tiles += J.mblocks * J.nblocks * J.nsplit;
+    J.item0 = items;
+    items += J.nib * J.njb * J.nsplit;
   }
   a.njobs = (int)js.size();
-  a.ntiles = tiles;
+  a.nitems = items;
+  a.per_xcd = (int)cdiv(items, 8);
   HIPCHK(launch_dw(h->stream, a));
   return IWAE_OK;
 }
@@ -2790,6 +2791,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_NLL_IMGS: h->nll_imgs = (int)std::max(0LL, std::min(value, 1LL << 20)); break;
     case IWAE_KNOB_WIDE_ROWS: h->wide_rows = std::max(0LL, value); break;
     case IWAE_KNOB_DW_WIDE: h->dw_wide = on; break;
+    case IWAE_KNOB_DW_WG: h->dw_wg = (int)std::max(8LL, std::min(value, 4096LL)); break;
     case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;

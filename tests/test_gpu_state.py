@@ -182,7 +182,7 @@ def _run_steps(tuning, x, eps=None, steps=1, dp=False, seed=13, use_graphs=True)
 @pytest.mark.parametrize("B", [100, 512])
 def test_wide_engine_and_dw_kernel_match_the_16_row_engine(B):
     """Large batches: the 32 / 64-row engine workgroups (two-set weight
-    pipeline) and the 112 x 256-block weight-gradient kernel against the
+    pipeline) and the 208 x 128-block weight-gradient kernel against the
     16-row engine and the update kernel's slab pass, same injected noise:
     loss to bf16x3 rounding order, gradient and post-Adam weights."""
     rng = np.random.default_rng(66)
