@@ -142,7 +142,9 @@ enum iwae_knob {
                                       columns for one k step), 8 or 4 (16) */
   IWAE_KNOB_NLL_IMGS = 27,         /* images per NLL chunk where the call passes chunk 0 (iwae_nll_eps too);
                                       with NLL_ROWS < imgs * k the chunk's samples split into sample chunks (0: auto) */
-  IWAE_KNOB_DW_WG = 28             /* workgroups the DW_WIDE weight-gradient pass balances its row chunks over (256) */
+  IWAE_KNOB_DW_WG = 28,            /* workgroups the DW_WIDE weight-gradient pass balances its row chunks over (256) */
+  IWAE_KNOB_PIWAE_ONE = 29         /* PIWAE on the engine: one unit-weight backward chain for both weightings (1);
+                                      0: the chain twice (IWAE_{k1 k2}, then MIWAE for the encoder) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --

@@ -663,6 +663,11 @@ struct TcArgs {
   const float* eps_a[8]; const float* eps_b[8]; int Bsplit, Bimg;   // injected noise ([k][B][d]) or null
   const float* dlw; const float* dpx; float wa;
   float wb; int need_bce;                   // L_alpha: Keras-BCE term of the output epilogue (weight wb)
+  // unit row weights (PIWAE): the backward chain runs with dL/dlw = dpx = 1 per
+  // row (every output of the chain is linear in a row's weight), the weight
+  // gradients scale each layer's dZ rows by its own weighting afterwards, and
+  // the image-row Gaussian backward scales its dL/dh sources by dlw per sample
+  int unit_w;
   // the bound inside the backward launch (bnd_rows): every workgroup computes
   // its rows' dL/dlw and dpx into LDS at float offset bnd_lds (dpx at + 16 RT)
   // from its images' log weights, staging an image per wave at wave * bnd_ld;

@@ -205,6 +205,8 @@ struct iwae_handle {
   long long nll_rows = 1LL << 20;    // sample rows per NLL chunk (measured fastest: 2^17-2^20 within 10 %)
   int nll_imgs = 0;                  // images per NLL chunk when the caller passes chunk 0 (0: nll_rows / k)
   int dw_wg = 256;                   // large-batch weight-gradient pass: workgroups its row chunks aim at
+  int piwae_one = 1;                 // PIWAE: one unit-weight backward chain serves both weightings (knob)
+  bool piwae_ks = false;             // (during a step) the weight gradients apply the per-layer PIWAE weighting
   int tc_rt = 1;                     // row tiles of 16 per engine workgroup below wide_rows
   int ld_align = 4;                  // workspace row strides: multiples of this many floats (4 or 32)
   long long wide_rows = 4097;        // sample rows from which the engine runs 32 / 64-row workgroups
@@ -1432,6 +1434,18 @@ static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const
 // bf16x3 products, and up to upd_rows sample rows (one workgroup reduces a
 // tile over all rows: beyond that the split-K GEMM + Adam launches parallelise
 // better).
+// the row scale of layer di's dZ in the weight gradients: ks as given, or under
+// piwae_unit the layer's weighting
+static const float* dz_scale(const iwae_handle* h, int di, const float* ks) {
+  if (!h->piwae_ks) return ks;
+  if (di == h->o1 || di == h->o2 || di == h->o3) return h->dpx;
+  for (int i = 0; i < h->L - 1; ++i)
+    if (di == h->dec[i].l1 || di == h->dec[i].l2 || di == h->dec[i].head) return h->dlw;
+  for (int i = 1; i < h->L; ++i)
+    if (di == h->enc[i].l1 || di == h->enc[i].l2 || di == h->enc[i].head) return h->dlw2;
+  return ks;                          // the first encoder layer: its image-row dZ are weighted already
+}
+
 static bool upd_tiles_ok(const iwae_handle* h) {
   long long tiles = 0;
   for (const DenseL& d : h->dense) tiles += cdiv(d.fin + 1, 64) * cdiv(d.fout, h->upd_tn32 ? 32 : 64);
@@ -1510,7 +1524,8 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int bucket = 0, 
   for (const WJ& w : js) {
     DenseL& d = h->dense[w.di];
     UpdJob& J = a.job[a.njobs++];
-    J.A = w.A->p; J.lda = w.A->ld; J.B = w.dZ->p; J.ldb = w.dZ->ld; J.ks = w.ks ? w.ks : h->ones; J.rows = w.rows;
+    const float* ks = dz_scale(h, w.di, w.ks);
+    J.A = w.A->p; J.lda = w.A->ld; J.B = w.dZ->p; J.ldb = w.dZ->ld; J.ks = ks ? ks : h->ones; J.rows = w.rows;
     J.off = d.off; J.fin = d.fin; J.fout = d.fout; J.ldw = d.ldw;
     const bool fx = w.di != h->enc[0].l1;       // the input layer has no fragment-major copies
     J.fx_off = fx ? d.fx_off : -1; J.fx_steps = d.fx_steps; J.head_d = d.head_d;
@@ -1625,7 +1640,8 @@ static int run_dw(iwae_handle* h, const Plan& P) {
     const WJ& w = js[q];
     DenseL& d = h->dense[w.di];
     DwJob& J = a.job[q];
-    J.A = w.A->p; J.lda = w.A->ld; J.B = w.dZ->p; J.ldb = w.dZ->ld; J.ks = w.ks ? w.ks : h->ones;
+    const float* ks = dz_scale(h, w.di, w.ks);
+    J.A = w.A->p; J.lda = w.A->ld; J.B = w.dZ->p; J.ldb = w.dZ->ld; J.ks = ks ? ks : h->ones;
     J.rows = w.rows;
     J.out = h->slabs + d.slab_off; J.ldo = d.ldw; J.slab_stride = d.size();
     const double ksteps = (double)cdiv(w.rows, 32);
@@ -2024,7 +2040,7 @@ static int tc_prepare(iwae_handle* h, const Plan& P) {
 // dlw / dpx: the bound's weighting the launch reads (default: the bound's
 // first one; PIWAE's encoder pass: the MIWAE one, dlw2 / dpx2)
 static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which, const BoundArgs* bnd = nullptr,
-                  const float* dlw = nullptr, const float* dpx = nullptr) {
+                  const float* dlw = nullptr, const float* dpx = nullptr, bool unit = false) {
   auto it = h->tc_plans.find(tc_key(P, which));
   if (it == h->tc_plans.end()) return fail(h, IWAE_EINVAL, "engine plan missing");
   const iwae_handle::TcRec& rec = it->second;
@@ -2067,6 +2083,7 @@ static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which, con
   a.Bsplit = P.Bsplit; a.Bimg = P.Bimg;
   a.dlw = dlw ? dlw : h->dlw; a.dpx = dpx ? dpx : h->dpx; a.wa = P.wa;
   a.wb = P.wb; a.need_bce = P.need_bce;
+  a.unit_w = unit ? 1 : 0;
   a.bnd_block = -1;
   if (bnd) {
     // the bound in this (backward) launch: its rows' dL/dlw per workgroup, the
@@ -2146,6 +2163,16 @@ static bool nring_train_backward(iwae_handle* h, const Plan& P, bool fwd_ring, b
 static bool nre_plan(iwae_handle* h, NreLaunch& R);
 static bool nring_train_backward_enc(iwae_handle* h, const Plan& P, bool& ran);
 
+// PIWAE (PDF p7) on the engine with ONE backward chain: every quantity of the
+// backward is linear in a row's weight (dL/dlw for the log q / prior terms, dpx
+// for the Bernoulli term), so the chain runs once with unit weights and each
+// consumer applies the weighting it needs -- IWAE_{k1 k2} (dlw, dpx) for the
+// decoder's weight gradients, MIWAE(k1, k2) (dlw2) for the encoder's.  Where
+// the row-chain engine runs the backward (not the ring kernels) and the image-
+// row job takes the first encoder layer's backward.
+static bool piwae_unit(const iwae_handle* h, const Plan& P, bool ring) {
+  return P.piwae && !ring && (h->engine_img_bwd || (h->engine_img && !smallm_ok(h, P.Bimg))) && h->piwae_one;
+}
 static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
   // The first encoder layer's l2 / head: up to 32 images the few-row N-split
   // launches (one 16-column tile per workgroup; at B = 20 the image-row jobs,
@@ -2195,7 +2222,7 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
     // 0.613-0.621 ms at B = 512 -- the two passes, one workgroup per CU each,
     // compete for the CUs)
     if (!rb) {
-      CHK(tc_run(h, P, E, 1));
+      CHK(tc_run(h, P, E, 1, nullptr, nullptr, nullptr, piwae_unit(h, P, ring)));
     } else if (h->L >= 2) {
       // nring_bwd 3: the encoder / prior chains on the ring as well
       bool re = false;
@@ -2207,14 +2234,24 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   // PIWAE (PDF p7): the decoder's weight gradients come from IWAE_{k1 k2} (the
   // pass above stored their dZ), the encoder's from MIWAE(k1, k2): the
   // backward chain again on dlw2 / dpx2, storing only the encoder path
+  // With unit row weights (piwae_unit) the one chain above serves both
+  // weightings: the weight gradients scale each layer's dZ rows by its own
+  // (run_update / run_dw: dpx or dlw for the decoder, dlw2 for the encoder),
+  // and the image-row job scales its dL/dh sources by dlw2 per sample.
+  const bool unit = piwae_unit(h, P, ring);
   const float* enc_dlw = P.piwae ? h->dlw2 : nullptr;
-  if (P.piwae) CHK(tc_run(h, P, E, 4, nullptr, h->dlw2, h->dpx2));
+  if (P.piwae && !unit) CHK(tc_run(h, P, E, 4, nullptr, h->dlw2, h->dpx2));
+  h->piwae_ks = unit;
+  struct KsReset {
+    iwae_handle* h;
+    ~KsReset() { h->piwae_ks = false; }
+  } ks_reset{h};
   // (a second stream for the first encoder layer's backward beside the other
   // weight gradients measured slower inside the captured graph: sequential).
   // Its image-row job also at small batches (B = 20: step 128.1 -> 126.4 us
   // against the row-block Gaussian backward + two few-row launches)
   const bool img_bwd = img || h->engine_img_bwd;
-  if (img_bwd) CHK(tc_run(h, P, E, 3, nullptr, enc_dlw));
+  if (img_bwd) CHK(tc_run(h, P, E, 3, nullptr, enc_dlw, nullptr, unit));
   else CHK(fused_encoder_bwd(h, P, P.piwae ? h->dlw2 : h->dlw, 0));
   if (use_update(h, P) && h->dp_weighted) {
     // data parallel: the fused gradient pass (B_local * g, B_local in the
@@ -2792,6 +2829,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_WIDE_ROWS: h->wide_rows = std::max(0LL, value); break;
     case IWAE_KNOB_DW_WIDE: h->dw_wide = on; break;
     case IWAE_KNOB_DW_WG: h->dw_wg = (int)std::max(8LL, std::min(value, 4096LL)); break;
+    case IWAE_KNOB_PIWAE_ONE: h->piwae_one = on; break;
     case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;

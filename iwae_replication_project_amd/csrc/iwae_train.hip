@@ -869,7 +869,7 @@ __device__ __forceinline__ void tc_loadg(const TcArgs& A, CJob& J, COp& S, int r
   const int t = threadIdx.x, rr = t / TPR, sub = t - rr * TPR;
   const TcBuf B = tc_buf<RT>(J, S.out_buf);
   const int rg = row0 + min(rr, nrows - 1);
-  const float dp = A.bnd_rows ? tcs[A.bnd_lds + R + min(rr, nrows - 1)] : A.dpx[rg];
+  const float dp = A.unit_w ? 1.f : A.bnd_rows ? tcs[A.bnd_lds + R + min(rr, nrows - 1)] : A.dpx[rg];
   const __amdgpu_buffer_rsrc_t rs = buf_rsrc(S.y);
   for (int c4 = sub; 4 * c4 < S.next_k; c4 += TPR) {
     const int k = 4 * c4;
@@ -901,7 +901,7 @@ __device__ __forceinline__ void tc_gbwd(const TcArgs& A, CJob& J, COp& S, int ro
   }
   const int rg = row0 + min(rr, nrows - 1);
   const bool st = rr < nrows;
-  const float dl = A.bnd_rows ? tcs[A.bnd_lds + min(rr, nrows - 1)] : A.dlw[rg];
+  const float dl = A.unit_w ? 1.f : A.bnd_rows ? tcs[A.bnd_lds + min(rr, nrows - 1)] : A.dlw[rg];
   const float* Pr = S.P + (size_t)rg * S.ld_P;
   const float* Hr = S.h + (size_t)rg * S.ld_h;
   __amdgpu_buffer_rsrc_t rsrc[4];
@@ -1055,6 +1055,7 @@ __device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int r
         for (int q = 0; q < 4; ++q) {
           const float h = f4_at(hv[i], q), e = f4_at(ev[i], q);
           float G = (f4_at(gs[i][0], q) + f4_at(gs[i][1], q)) + f4_at(gs[i][2], q);
+          if (A.unit_w) G *= dl[i];            // sources from a unit-weight chain: this sample's weight
           const float z = h * rs4[q] - mu[q] * rs4[q];
           const float dlq = -dl[i];
           if (S.stdnormal) G += dl[i] * (-h);

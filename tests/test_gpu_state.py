@@ -318,3 +318,30 @@ def test_weight_ring_train_forward_runs_at_large_batch_only():
         n0 = m._lib.iwae_debug_count(m._h, 4)
         m.train_step((rng.random((B, 784)) < 0.2).astype(np.float32))
         assert (m._lib.iwae_debug_count(m._h, 4) > n0) == want, B
+
+
+@pytest.mark.parametrize("B,k1,k2", [(20, 8, 8), (7, 4, 3)])
+def test_piwae_one_unit_chain_matches_two_chains(B, k1, k2):
+    """PIWAE (PDF p7) with ONE backward chain at unit row weights, the decoder's
+    weight gradients scaled by the IWAE_{k1 k2} weighting and the encoder's by
+    the MIWAE(k1, k2) one (knob piwae_one, default), against the chain run twice
+    (piwae_one 0): same loss bits, gradient and post-Adam weights to rounding."""
+    from iwae_replication_project_amd import Adam, Flexible_Model
+    rng = np.random.default_rng(68 + B)
+    k = k1 * k2
+    x = (rng.random((B, 784)) < 0.2).astype(np.float32)
+    eps = [rng.standard_normal((k, B, d)).astype(np.float32) for d in ARCH2[2]]
+
+    def step(flag):
+        m = Flexible_Model(*ARCH2, dataset_bias=None, loss_function="PIWAE", k=k, k1=k1, k2=k2, seed=14,
+                           tuning={"piwae_one": flag})
+        m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+        n0 = m._lib.iwae_debug_count(m._h, 2)
+        loss = m.train_step(x, eps=eps)["PIWAE"]
+        return loss, _flat(m.get_gradients()), _flat(m.get_weights()), m._lib.iwae_debug_count(m._h, 2) - n0
+    la, ga, wa, na = step(1)
+    lb, gb, wb, nb = step(0)
+    assert la == lb
+    assert na == nb - 1                       # one engine backward launch fewer
+    assert np.linalg.norm(ga - gb) <= 1e-5 * np.linalg.norm(gb)
+    assert np.abs(wa - wb).max() <= 1e-5
