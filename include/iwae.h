@@ -144,7 +144,8 @@ enum iwae_knob {
                                       with NLL_ROWS < imgs * k the chunk's samples split into sample chunks (0: auto) */
   IWAE_KNOB_DW_WG = 28,            /* workgroups the DW_WIDE weight-gradient pass balances its row chunks over (256) */
   IWAE_KNOB_PIWAE_ONE = 29         /* PIWAE on the engine: one unit-weight backward chain for both weightings (1);
-                                      0: the chain twice (IWAE_{k1 k2}, then MIWAE for the encoder) */
+                                      0: the chain twice (IWAE_{k1 k2}, then MIWAE for the encoder) */,
+  IWAE_KNOB_DW_ALPHA = 30          /* DW_WIDE pass cost model: a k step's fixed cost in MFMA tiles (0) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --

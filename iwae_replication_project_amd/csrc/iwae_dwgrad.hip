@@ -24,7 +24,7 @@
 // transposed reads (a 32-lane half: two 4-row blocks 8 rows apart) are free of
 // bank conflicts (checked on the gfx950 bank rules by tools/dw_banks.py).
 //
-// 16 waves as 4 (i) x 4 (j): wave (wi, wj) multiplies i-tiles wi + 4a (a < 4)
+// 8 waves as 2 (i) x 4 (j): wave (wi, wj) multiplies i-tiles wi + 2p (p < 7)
 // by j-tiles wj + 4c (c < 2), bf16x3 (a_hi b_hi + a_hi b_lo + a_lo b_hi, f32
 // accumulate, v_mfma_f32_16x16x32_bf16).  Two LDS images and two register sets
 // of loads: k step it multiplies image it & 1 while the loads of step it + 1
@@ -43,13 +43,22 @@ typedef short dw_s16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned dw_u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned dw_u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int DW_NT = 1024;                   // threads (16 waves)
+constexpr int DW_WI = 2, DW_WJ = 4;           // waves along i (W_aug rows) and j (outputs)
+constexpr int DW_PI = 7, DW_PJ = 2;           // tiles per wave along i (13 / 2) and j (8 / 4)
+constexpr int DW_NT = 64 * DW_WI * DW_WJ;     // threads (8 waves: 256 registers each)
 constexpr int DW_KR = 32;                     // rows per k step (one MFMA k)
 constexpr int DW_CB = 8192;                   // bytes per 128-column block of one plane (32 rows x 256 B)
 constexpr int DW_XP = 2 * DW_CB;              // X plane: 256 columns (up to 13 tiles used)
 constexpr int DW_ZP = DW_CB;                  // dZ plane: 128 columns (up to 8 tiles)
 constexpr int DW_IMG = 2 * DW_XP + 2 * DW_ZP; // X hi, X lo, dZ hi, dZ lo: 48 KiB
-constexpr int DW_TASKS = 3;                   // 16-byte pieces per thread and k step (<= 3072 = 32 x (64 + 32))
+constexpr int DW_TASKS = 3072 / DW_NT;        // 16-byte pieces per thread and k step (<= 3072 = 32 x (64 + 32))
+
+// timing ablations (debug builds only, -DIWAE_DW_ABL=<mask>; WRONG results):
+// 1 loads never advance (L2 hits), 2 no MFMAs, 4 no loads, 8 no LDS staging
+#ifndef IWAE_DW_ABL
+#define IWAE_DW_ABL 0
+#endif
+constexpr int kDwAbl = IWAE_DW_ABL;
 
 extern __shared__ __attribute__((aligned(16))) unsigned char dws[];
 
@@ -63,37 +72,43 @@ __device__ __forceinline__ dw_f32x4 dw_ld4(__amdgpu_buffer_rsrc_t r, unsigned of
   return __builtin_bit_cast(dw_f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
-// one thread's pieces: role 0 none, 1 X, 2 dZ (wave-uniform per slot)
+// one thread's pieces: role 0 none, 1 X, 2 dZ (wave-uniform per slot).  The
+// buffer resources cover the row chunk (rows past its end read 0) and are built
+// once; the per-lane offsets advance by one k step per request.
 struct DwTask {
   int role[DW_TASKS];
-  unsigned goff[DW_TASKS];     // byte offset of the piece in its row chunk's first row (kOOB: past the width)
-  unsigned koff[DW_TASKS];     // byte offset of the row scale (dZ pieces)
+  __amdgpu_buffer_rsrc_t rs[DW_TASKS];   // the piece's matrix (X or dZ) over the chunk
+  unsigned goff[DW_TASKS];     // byte offset of the piece for the next request (kOOB: past the width)
+  unsigned ginc[DW_TASKS];     // bytes per k step (32 rows)
+  unsigned koff[DW_TASKS];     // byte offset of the row scale (dZ pieces) for the next request
+  float kadd[DW_TASKS];        // 1 for X pieces (their row-scale load reads 0), 0 for dZ pieces
   int loff[DW_TASKS];          // LDS byte offset of the piece in the hi plane of its image
+  int lplane[DW_TASKS];        // bytes from the hi to the lo plane
 };
 struct DwSet {
   dw_f32x4 v[DW_TASKS];
   float k[DW_TASKS];
 };
 
-__device__ __forceinline__ void dw_load(const DwJob& J, const DwTask& T, int r0, int rend, DwSet& S) {
-  const unsigned left = rend > r0 ? (unsigned)(rend - r0) : 0u;
-  const __amdgpu_buffer_rsrc_t rx = buf_rsrc(J.A + (size_t)r0 * J.lda, left * (unsigned)J.lda * 4u);
-  const __amdgpu_buffer_rsrc_t rz = buf_rsrc(J.B + (size_t)r0 * J.ldb, left * (unsigned)J.ldb * 4u);
-  const __amdgpu_buffer_rsrc_t rk = buf_rsrc(J.ks + r0, left * 4u);
+__device__ __forceinline__ void dw_load(DwTask& T, __amdgpu_buffer_rsrc_t rk, DwSet& S) {
+  if (kDwAbl & 4) return;
 #pragma unroll
   for (int u = 0; u < DW_TASKS; ++u) {
-    S.v[u] = dw_ld4(T.role[u] == 1 ? rx : rz, T.goff[u]);
+    S.v[u] = dw_ld4(T.rs[u], T.goff[u]);
     S.k[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rk, T.koff[u], 0, 0));
+    if (kDwAbl & 1) continue;
+    T.goff[u] += T.ginc[u];                 // (an out-of-range offset stays out of range: kOOB + steps < 2^32)
+    T.koff[u] += DW_KR * 4u;
   }
 }
 
 // the set's pieces -> bf16 hi / lo, row-major into image `img`
 __device__ __forceinline__ void dw_store(const DwTask& T, const DwSet& S, unsigned char* img) {
+  if (kDwAbl & 8) return;
 #pragma unroll
   for (int u = 0; u < DW_TASKS; ++u) {
     if (T.role[u] == 0) continue;                         // (wave-uniform; no load inside)
-    dw_f32x4 v = S.v[u];
-    if (T.role[u] == 2) v *= S.k[u];                      // dZ times its row scale
+    const dw_f32x4 v = S.v[u] * (S.k[u] + T.kadd[u]);     // dZ times its row scale (X: times 1)
     const dw_f32x2 a = {v[0], v[1]}, b = {v[2], v[3]};
     const unsigned ha = __builtin_bit_cast(unsigned, __builtin_convertvector(a, dw_bf16x2));
     const unsigned hb = __builtin_bit_cast(unsigned, __builtin_convertvector(b, dw_bf16x2));
@@ -101,23 +116,22 @@ __device__ __forceinline__ void dw_store(const DwTask& T, const DwSet& S, unsign
     const dw_f32x2 rb = b - dw_f32x2{__uint_as_float(hb << 16), __uint_as_float(hb & 0xFFFF0000u)};
     const unsigned la = __builtin_bit_cast(unsigned, __builtin_convertvector(ra, dw_bf16x2));
     const unsigned lb = __builtin_bit_cast(unsigned, __builtin_convertvector(rb, dw_bf16x2));
-    const int plane = T.role[u] == 1 ? DW_XP : DW_ZP;
-    unsigned char* p = img + T.loff[u];
-    *reinterpret_cast<dw_u32x2*>(p) = dw_u32x2{ha, hb};
-    *reinterpret_cast<dw_u32x2*>(p + plane) = dw_u32x2{la, lb};
+    *reinterpret_cast<dw_u32x2*>(img + T.loff[u]) = dw_u32x2{ha, hb};
+    *reinterpret_cast<dw_u32x2*>(img + T.lplane[u]) = dw_u32x2{la, lb};
   }
 }
 
-// fragment of 16-column tile t (hi or lo plane at `pl`): two transposed reads,
-// rows 8 g .. 8 g + 3 and 8 g + 4 .. 8 g + 7 of the lane's group g
-__device__ __forceinline__ dw_bf16x8 dw_frag(const unsigned char* pl, int t, int lane) {
+// fragment of a 16-column tile from the plane at `pl`: two transposed reads at
+// the lane's precomputed offsets o0 / o1 (rows 8 g .. 8 g + 3 and 8 g + 4 ..
+// 8 g + 7 of its group g; dw_frag_off)
+__device__ __forceinline__ int dw_frag_off(int t, int lane, int h) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int c = 16 * t + 4 * p;
+  return dw_off(8 * g + 4 * h + q, 16 * t + 4 * p);
+}
+__device__ __forceinline__ dw_bf16x8 dw_frag(const unsigned char* pl, int o0, int o1) {
   typedef __attribute__((address_space(3))) dw_s16x4 lds_s16x4;
-  const dw_s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_s16x4*)(pl + dw_off(8 * g + q, c)));
-  const dw_s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_s16x4*)(pl + dw_off(8 * g + 4 + q, c)));
+  const dw_s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pl + o0));
+  const dw_s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pl + o1));
   const dw_u32x2 ua = __builtin_bit_cast(dw_u32x2, a), ub = __builtin_bit_cast(dw_u32x2, b);
   return __builtin_bit_cast(dw_bf16x8, dw_u32x4{ua[0], ua[1], ub[0], ub[1]});
 }
@@ -138,40 +152,63 @@ __global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
   const int mtb = min(J.mtb, J.mt - J.mtb * ib), ntb = min(J.ntb, J.nt - J.ntb * jbk);
   const int rbase = s * J.chunk, rend = min(J.rows, rbase + J.chunk);
   const int nk = (rend - rbase + DW_KR - 1) / DW_KR;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wi = w >> 2, wj = w & 3;
+  const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), wi = w / DW_WJ,
+            wj = w % DW_WJ;
 
   // the thread's pieces: X quads per row nqx (16-multiple: a 16-lane write group
   // stays on one row), then dZ quads nqz
   const int nqx = (4 * mtb + 15) & ~15, nqz = (4 * ntb + 15) & ~15;
+  const unsigned left = (unsigned)max(0, rend - rbase);
+  const __amdgpu_buffer_rsrc_t rx = buf_rsrc(J.A + (size_t)rbase * J.lda, left * (unsigned)J.lda * 4u);
+  const __amdgpu_buffer_rsrc_t rz = buf_rsrc(J.B + (size_t)rbase * J.ldb, left * (unsigned)J.ldb * 4u);
+  const __amdgpu_buffer_rsrc_t rk = buf_rsrc(J.ks + rbase, left * 4u);
   DwTask T;
 #pragma unroll
   for (int u = 0; u < DW_TASKS; ++u) {
     const int tau = t + DW_NT * u;
     const int role = __builtin_amdgcn_readfirstlane(tau < DW_KR * nqx ? 1 : tau < DW_KR * (nqx + nqz) ? 2 : 0);
     T.role[u] = role;
+    T.rs[u] = role == 1 ? rx : rz;
     int row = 0, c = 0;
     bool ok = false;
     if (role == 1) {
       row = tau / nqx; c = 4 * (tau - row * nqx);
       ok = i0 + c < J.M;
       T.goff[u] = ok ? (unsigned)(row * J.lda + i0 + c) * 4u : kOOB;
+      T.ginc[u] = ok ? (unsigned)(DW_KR * J.lda) * 4u : 0u;
     } else if (role == 2) {
       const int tz = tau - DW_KR * nqx;
       row = tz / nqz; c = 4 * (tz - row * nqz);
       ok = j0 + c < J.N;
       T.goff[u] = ok ? (unsigned)(row * J.ldb + j0 + c) * 4u : kOOB;
+      T.ginc[u] = ok ? (unsigned)(DW_KR * J.ldb) * 4u : 0u;
     } else {
       T.goff[u] = kOOB;
+      T.ginc[u] = 0u;
     }
     T.koff[u] = role == 2 ? (unsigned)row * 4u : kOOB;
+    T.kadd[u] = role == 2 ? 0.f : 1.f;
     T.loff[u] = (role == 2 ? 2 * DW_XP : 0) + dw_off(row, c);
+    T.lplane[u] = T.loff[u] + (role == 2 ? DW_ZP : DW_XP);
   }
+  // the lane's fragment offsets: i-tile slots wi + 2 p, j-tile slots wj + 4 c,
+  // two reads each (slots past the block read image columns that exist: <= 223
+  // of X's 256, <= 127 of dZ's 128 -- every read is unconditional)
+  int oa[DW_PI][2], ob[DW_PJ][2];
+#pragma unroll
+  for (int p = 0; p < DW_PI; ++p)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) oa[p][h] = dw_frag_off(wi + DW_WI * p, lane, h);
+#pragma unroll
+  for (int c = 0; c < DW_PJ; ++c)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) ob[c][h] = dw_frag_off(wj + DW_WJ * c, lane, h);
 
-  dw_f32x4 acc[4][2];
+  dw_f32x4 acc[DW_PI][DW_PJ];
 #pragma unroll
-  for (int p = 0; p < 4; ++p)
+  for (int p = 0; p < DW_PI; ++p)
 #pragma unroll
-    for (int q = 0; q < 2; ++q) acc[p][q] = dw_f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < DW_PJ; ++q) acc[p][q] = dw_f32x4{0.f, 0.f, 0.f, 0.f};
 
   unsigned char* img0 = dws;
   unsigned char* img1 = dws + DW_IMG;
@@ -184,62 +221,65 @@ __global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
     const unsigned char* xl = img + DW_XP;
     const unsigned char* zh = img + 2 * DW_XP;
     const unsigned char* zl = zh + DW_ZP;
-    dw_bf16x8 bh[2], bl[2];
+    dw_bf16x8 bh[DW_PJ], bl[DW_PJ], ah[2], al[2];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int tj = wj + 4 * c;
-      if (tj < ntb) {
-        bh[c] = dw_frag(zh, tj, lane);
-        bl[c] = dw_frag(zl, tj, lane);
-      }
+    for (int c = 0; c < DW_PJ; ++c) {
+      bh[c] = dw_frag(zh, ob[c][0], ob[c][1]);
+      bl[c] = dw_frag(zl, ob[c][0], ob[c][1]);
     }
+    ah[0] = dw_frag(xh, oa[0][0], oa[0][1]);
+    al[0] = dw_frag(xl, oa[0][0], oa[0][1]);
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int ti = wi + 4 * p;
-      if (ti < mtb) {                                     // (wave-uniform)
-        const dw_bf16x8 ah = dw_frag(xh, ti, lane), al = dw_frag(xl, ti, lane);
+    for (int p = 0; p < DW_PI; ++p) {
+      if (p + 1 < DW_PI) {                                // the next i-tile's fragments in flight
+        ah[(p + 1) & 1] = dw_frag(xh, oa[p + 1][0], oa[p + 1][1]);
+        al[(p + 1) & 1] = dw_frag(xl, oa[p + 1][0], oa[p + 1][1]);
+      }
+      if (wi + DW_WI * p < mtb && !(kDwAbl & 2)) {         // (wave-uniform)
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          if (wj + 4 * c < ntb) {
-            acc[p][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[c], acc[p][c], 0, 0, 0);
-            acc[p][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[c], acc[p][c], 0, 0, 0);
-            acc[p][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[c], acc[p][c], 0, 0, 0);
+        for (int c = 0; c < DW_PJ; ++c) {
+          if (wj + DW_WJ * c < ntb) {
+            acc[p][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[p & 1], bh[c], acc[p][c], 0, 0, 0);
+            acc[p][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[p & 1], bl[c], acc[p][c], 0, 0, 0);
+            acc[p][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[p & 1], bh[c], acc[p][c], 0, 0, 0);
           }
         }
       }
     }
   };
-  DwSet S0, S1;
+  DwSet S0{}, S1{};
   if (nk > 0) {
-    dw_load(J, T, rbase, rend, S0);
-    dw_load(J, T, rbase + DW_KR, rend, S1);
+    dw_load(T, rk, S0);
+    dw_load(T, rk, S1);
     dw_store(T, S0, img0);
-    dw_load(J, T, rbase + 2 * DW_KR, rend, S0);
+    dw_load(T, rk, S0);
     __syncthreads();
   }
-  auto step = [&](int it, const unsigned char* rimg, unsigned char* wimg, DwSet& Sn) __attribute__((always_inline)) {
+  // (every step unconditional, the step count rounded up to even: a step past
+  // the chunk multiplies rows that read 0 -- a conditional step or store would
+  // make the compiler merge the two steps and copy the sets, draining the loads)
+  auto step = [&](const unsigned char* rimg, unsigned char* wimg, DwSet& Sn) __attribute__((always_inline)) {
     mul(rimg);
-    if (it + 1 < nk) dw_store(T, Sn, wimg);
+    dw_store(T, Sn, wimg);
     __builtin_amdgcn_sched_barrier(0);
-    // (unconditional: past the chunk the range is empty and the loads return 0)
-    dw_load(J, T, rbase + (it + 3) * DW_KR, rend, Sn);
+    dw_load(T, rk, Sn);
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   };
   for (int it = 0; it < nk; it += 2) {
-    step(it, img0, img1, S1);
-    if (it + 1 < nk) step(it + 1, img1, img0, S0);
+    step(img0, img1, S1);
+    step(img1, img0, S0);
   }
 
   // slab s: rows i < M of the block (the layer's inputs + bias row), columns j < N
   float* out = J.out + (long long)s * J.slab_stride;
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int ti = wi + 4 * p;
+  for (int p = 0; p < DW_PI; ++p) {
+    const int ti = wi + DW_WI * p;
     if (ti >= mtb) break;
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int tj = wj + 4 * c;
+    for (int c = 0; c < DW_PJ; ++c) {
+      const int tj = wj + DW_WJ * c;
       if (tj >= ntb) break;
       const int j = j0 + 16 * tj + (lane & 15);
 #pragma unroll

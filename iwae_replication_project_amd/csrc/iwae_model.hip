@@ -205,6 +205,7 @@ struct iwae_handle {
   long long nll_rows = 1LL << 20;    // sample rows per NLL chunk (measured fastest: 2^17-2^20 within 10 %)
   int nll_imgs = 0;                  // images per NLL chunk when the caller passes chunk 0 (0: nll_rows / k)
   int dw_wg = 256;                   // large-batch weight-gradient pass: workgroups its row chunks aim at
+  int dw_alpha = 0;                  // ... its cost model: a k step's fixed cost in MFMA tiles
   int piwae_one = 1;                 // PIWAE: one unit-weight backward chain serves both weightings (knob)
   bool piwae_ks = false;             // (during a step) the weight gradients apply the per-layer PIWAE weighting
   int tc_rt = 1;                     // row tiles of 16 per engine workgroup below wide_rows
@@ -1631,10 +1632,24 @@ static int run_dw(iwae_handle* h, const Plan& P) {
     J.mt = (int)cdiv(J.M, 16); J.nt = (int)cdiv(J.N, 16);
     J.nib = (int)cdiv(J.mt, 13); J.mtb = (int)cdiv(J.mt, J.nib);
     J.njb = (int)cdiv(J.nt, 8); J.ntb = (int)cdiv(J.nt, J.njb);
-    cost[q] = (double)J.mtb * J.ntb;
+    cost[q] = (double)J.mtb * J.ntb + (double)h->dw_alpha;   // + a k step's fixed cost in tile units
     W += cost[q] * J.nib * J.njb * (double)cdiv(js[q].rows, 32);
   }
-  const double target = W / (double)h->dw_wg;      // block-k-steps of tiles per workgroup
+  // block-k-steps of tiles per workgroup; the grid must not exceed one workgroup
+  // per CU (8 XCDs x 32): a second round would double the pass
+  double target = W / (double)h->dw_wg;
+  for (int tries = 0; tries < 64; ++tries) {
+    long long n = 0;
+    for (size_t q = 0; q < js.size(); ++q) {
+      const long long S = std::max(1LL, std::min<long long>(std::llround((double)cdiv(js[q].rows, 32) * cost[q] /
+                                                                         std::max(target, 1.0)),
+                                                            h->dense[js[q].di].cap_splits));
+      const long long chunk = cdiv(cdiv(js[q].rows, S), 32) * 32;
+      n += (long long)a.job[q].nib * a.job[q].njb * cdiv(js[q].rows, chunk);
+    }
+    if (n <= h->dw_wg) break;
+    target *= 1.02;
+  }
   int items = 0;
   for (size_t q = 0; q < js.size(); ++q) {
     const WJ& w = js[q];
@@ -2830,6 +2845,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_DW_WIDE: h->dw_wide = on; break;
     case IWAE_KNOB_DW_WG: h->dw_wg = (int)std::max(8LL, std::min(value, 4096LL)); break;
     case IWAE_KNOB_PIWAE_ONE: h->piwae_one = on; break;
+    case IWAE_KNOB_DW_ALPHA: h->dw_alpha = (int)std::max(0LL, std::min(value, 1000LL)); break;
     case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/${1:-dw}; shift
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_state.py -x -q --timeout 120 --timeout-method thread -k "dw or slab or wide" > $O/pytest.log 2>&1; rc=$?
+timeout -k 10 300 python -u -m pytest tests/test_gpu_state.py -x -q --timeout 120 --timeout-method thread -k "dw or slab or wide or piwae" > $O/pytest.log 2>&1; rc=$?
 tail -3 $O/pytest.log
 [ $rc -eq 0 ] || exit $rc
 n=0
