@@ -43,14 +43,19 @@ typedef short dw_s16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned dw_u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned dw_u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int DW_WI = 2, DW_WJ = 4;           // waves along i (W_aug rows) and j (outputs)
-constexpr int DW_PI = 7, DW_PJ = 2;           // tiles per wave along i (13 / 2) and j (8 / 4)
-constexpr int DW_NT = 64 * DW_WI * DW_WJ;     // threads (8 waves: 256 registers each)
+// Two block shapes (DwJob::wide): "tall" blocks up to 13 i-tiles x 8 j-tiles
+// (waves 2 (i) x 4 (j), 7 x 2 tiles each: the 200-wide layers' full input
+// width) and "wide" blocks up to 8 x 16 (waves 4 x 2, 2 x 8 tiles each: a
+// 100-input layer's 200 outputs in one block).  Per k step a wave holds the
+// fragments of its short side (2 slots) and streams those of its long side (7
+// or 8 slots, double-buffered).
+constexpr int DW_NS = 8, DW_NH = 2;           // stream / hold slots per wave
+constexpr int DW_NT = 512;                    // threads (8 waves: 256 registers each)
 constexpr int DW_KR = 32;                     // rows per k step (one MFMA k)
 constexpr int DW_CB = 8192;                   // bytes per 128-column block of one plane (32 rows x 256 B)
 constexpr int DW_XP = 2 * DW_CB;              // X plane: 256 columns (up to 13 tiles used)
-constexpr int DW_ZP = DW_CB;                  // dZ plane: 128 columns (up to 8 tiles)
-constexpr int DW_IMG = 2 * DW_XP + 2 * DW_ZP; // X hi, X lo, dZ hi, dZ lo: 48 KiB
+constexpr int DW_ZP = 2 * DW_CB;              // dZ plane: 256 columns (up to 16 tiles)
+constexpr int DW_IMG = 2 * DW_XP + 2 * DW_ZP; // X hi, X lo, dZ hi, dZ lo: 64 KiB
 constexpr int DW_TASKS = 3072 / DW_NT;        // 16-byte pieces per thread and k step (<= 3072 = 32 x (64 + 32))
 
 // timing ablations (debug builds only, -DIWAE_DW_ABL=<mask>; WRONG results):
@@ -128,12 +133,127 @@ __device__ __forceinline__ int dw_frag_off(int t, int lane, int h) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   return dw_off(8 * g + 4 * h + q, 16 * t + 4 * p);
 }
-__device__ __forceinline__ dw_bf16x8 dw_frag(const unsigned char* pl, int o0, int o1) {
+// (o0 / o1: absolute LDS byte addresses; `pl` the plane's byte offset from the
+// first image, a compile-time constant per call, so each read is one
+// ds_read_b64_tr_b16 with an immediate offset and no address arithmetic)
+__device__ __forceinline__ dw_bf16x8 dw_frag(int pl, unsigned o0, unsigned o1) {
   typedef __attribute__((address_space(3))) dw_s16x4 lds_s16x4;
-  const dw_s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pl + o0));
-  const dw_s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pl + o1));
+  const dw_s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(o0 + pl));
+  const dw_s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(o1 + pl));
   const dw_u32x2 ua = __builtin_bit_cast(dw_u32x2, a), ub = __builtin_bit_cast(dw_u32x2, b);
   return __builtin_bit_cast(dw_bf16x8, dw_u32x4{ua[0], ua[1], ub[0], ub[1]});
+}
+
+// The multiply loop and the slab stores of one block.  WIDE: waves 4 (i) x 2
+// (j), hold i-tiles wi + 4 h, stream j-tiles wj + 2 s; else 2 x 4, hold j-tiles
+// wj + 4 h, stream i-tiles wi + 2 s.  Slots past the block read image columns
+// that exist (X <= 223 of 256, dZ <= 255 of 256): every read is unconditional.
+template <bool WIDE>
+__device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask& T, __amdgpu_buffer_rsrc_t rk, unsigned lbase,
+                                          int w, int lane, int i0, int j0, int mtb, int ntb, int s, int nk) {
+  constexpr int WJ = WIDE ? 2 : 4, NS = WIDE ? 8 : 7;
+  const int wi = w / WJ, wj = w % WJ;
+  // tiles of stream slot q / hold slot h
+  auto st_tile = [&](int q) { return WIDE ? wj + 2 * q : wi + 2 * q; };
+  auto hd_tile = [&](int h) { return WIDE ? wi + 4 * h : wj + 4 * h; };
+  const int st_n = WIDE ? ntb : mtb, hd_n = WIDE ? mtb : ntb;
+  unsigned os[NS][2], oh[DW_NH][2];
+#pragma unroll
+  for (int q = 0; q < NS; ++q)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) os[q][r] = lbase + dw_frag_off(st_tile(q), lane, r);
+#pragma unroll
+  for (int h = 0; h < DW_NH; ++h)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) oh[h][r] = lbase + dw_frag_off(hd_tile(h), lane, r);
+
+  dw_f32x4 acc[NS][DW_NH];
+#pragma unroll
+  for (int q = 0; q < NS; ++q)
+#pragma unroll
+    for (int h = 0; h < DW_NH; ++h) acc[q][h] = dw_f32x4{0.f, 0.f, 0.f, 0.f};
+
+  unsigned char* img0 = dws;
+  unsigned char* img1 = dws + DW_IMG;
+  // k step it multiplies image it & 1 while set (it + 1) & 1 (step it + 1,
+  // requested two steps earlier) is split into the other image; that set then
+  // requests step it + 3.  The loop is unrolled by two so each set keeps its
+  // registers (no renaming copy at the back edge, which would drain the loads).
+  auto mul = [&](int img) __attribute__((always_inline)) {    // img: the image's byte offset (0 or DW_IMG)
+    const int xh = img, xl = img + DW_XP, zh = img + 2 * DW_XP, zl = zh + DW_ZP;
+    const int sh_p = WIDE ? zh : xh, sl_p = WIDE ? zl : xl, hh_p = WIDE ? xh : zh, hl_p = WIDE ? xl : zl;
+    dw_bf16x8 hh[DW_NH], hl[DW_NH], sh[2], sl[2];
+#pragma unroll
+    for (int h = 0; h < DW_NH; ++h) {
+      hh[h] = dw_frag(hh_p, oh[h][0], oh[h][1]);
+      hl[h] = dw_frag(hl_p, oh[h][0], oh[h][1]);
+    }
+    sh[0] = dw_frag(sh_p, os[0][0], os[0][1]);
+    sl[0] = dw_frag(sl_p, os[0][0], os[0][1]);
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      if (q + 1 < NS) {                                   // the next stream slot's fragments in flight
+        sh[(q + 1) & 1] = dw_frag(sh_p, os[q + 1][0], os[q + 1][1]);
+        sl[(q + 1) & 1] = dw_frag(sl_p, os[q + 1][0], os[q + 1][1]);
+      }
+      if (st_tile(q) < st_n && !(kDwAbl & 2)) {           // (wave-uniform)
+#pragma unroll
+        for (int h = 0; h < DW_NH; ++h) {
+          if (hd_tile(h) < hd_n) {
+            // bf16x3: A = X^T (i), B = dZ (j): a_hi b_hi + a_hi b_lo + a_lo b_hi
+            const dw_bf16x8& ahi = WIDE ? hh[h] : sh[q & 1];
+            const dw_bf16x8& alo = WIDE ? hl[h] : sl[q & 1];
+            const dw_bf16x8& bhi = WIDE ? sh[q & 1] : hh[h];
+            const dw_bf16x8& blo = WIDE ? sl[q & 1] : hl[h];
+            acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi, acc[q][h], 0, 0, 0);
+            acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo, acc[q][h], 0, 0, 0);
+            acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi, acc[q][h], 0, 0, 0);
+          }
+        }
+      }
+    }
+  };
+  DwSet S0{}, S1{};
+  if (nk > 0) {
+    dw_load(T, rk, S0);
+    dw_load(T, rk, S1);
+    dw_store(T, S0, img0);
+    dw_load(T, rk, S0);
+    __syncthreads();
+  }
+  // (every step unconditional, the step count rounded up to even: a step past
+  // the chunk multiplies rows that read 0 -- a conditional step or store would
+  // make the compiler merge the two steps and copy the sets, draining the loads)
+  auto step = [&](int rimg, unsigned char* wimg, DwSet& Sn) __attribute__((always_inline)) {
+    mul(rimg);
+    dw_store(T, Sn, wimg);
+    __builtin_amdgcn_sched_barrier(0);
+    dw_load(T, rk, Sn);
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+  };
+  for (int it = 0; it < nk; it += 2) {
+    step(0, img1, S1);
+    step(DW_IMG, img0, S0);
+  }
+
+  // slab s: rows i < M of the block (the layer's inputs + bias row), columns j < N
+  float* out = J.out + (long long)s * J.slab_stride;
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    if (st_tile(q) >= st_n) break;
+#pragma unroll
+    for (int h = 0; h < DW_NH; ++h) {
+      if (hd_tile(h) >= hd_n) break;
+      const int ti = WIDE ? hd_tile(h) : st_tile(q), tj = WIDE ? st_tile(q) : hd_tile(h);
+      const int j = j0 + 16 * tj + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + 16 * ti + 4 * (lane >> 4) + r;
+        if (i < J.M && j < J.N) out[(long long)i * J.ldo + j] = acc[q][h][r];
+      }
+    }
+  }
 }
 
 __global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
@@ -152,8 +272,7 @@ __global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
   const int mtb = min(J.mtb, J.mt - J.mtb * ib), ntb = min(J.ntb, J.nt - J.ntb * jbk);
   const int rbase = s * J.chunk, rend = min(J.rows, rbase + J.chunk);
   const int nk = (rend - rbase + DW_KR - 1) / DW_KR;
-  const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), wi = w / DW_WJ,
-            wj = w % DW_WJ;
+  const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
 
   // the thread's pieces: X quads per row nqx (16-multiple: a 16-lane write group
   // stays on one row), then dZ quads nqz
@@ -191,104 +310,10 @@ __global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
     T.loff[u] = (role == 2 ? 2 * DW_XP : 0) + dw_off(row, c);
     T.lplane[u] = T.loff[u] + (role == 2 ? DW_ZP : DW_XP);
   }
-  // the lane's fragment offsets: i-tile slots wi + 2 p, j-tile slots wj + 4 c,
-  // two reads each (slots past the block read image columns that exist: <= 223
-  // of X's 256, <= 127 of dZ's 128 -- every read is unconditional)
-  int oa[DW_PI][2], ob[DW_PJ][2];
-#pragma unroll
-  for (int p = 0; p < DW_PI; ++p)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) oa[p][h] = dw_frag_off(wi + DW_WI * p, lane, h);
-#pragma unroll
-  for (int c = 0; c < DW_PJ; ++c)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) ob[c][h] = dw_frag_off(wj + DW_WJ * c, lane, h);
-
-  dw_f32x4 acc[DW_PI][DW_PJ];
-#pragma unroll
-  for (int p = 0; p < DW_PI; ++p)
-#pragma unroll
-    for (int q = 0; q < DW_PJ; ++q) acc[p][q] = dw_f32x4{0.f, 0.f, 0.f, 0.f};
-
-  unsigned char* img0 = dws;
-  unsigned char* img1 = dws + DW_IMG;
-  // k step it multiplies image it & 1 while set (it + 1) & 1 (step it + 1,
-  // requested two steps earlier) is split into the other image; that set then
-  // requests step it + 3.  The loop is unrolled by two so each set keeps its
-  // registers (no renaming copy at the back edge, which would drain the loads).
-  auto mul = [&](const unsigned char* img) __attribute__((always_inline)) {
-    const unsigned char* xh = img;
-    const unsigned char* xl = img + DW_XP;
-    const unsigned char* zh = img + 2 * DW_XP;
-    const unsigned char* zl = zh + DW_ZP;
-    dw_bf16x8 bh[DW_PJ], bl[DW_PJ], ah[2], al[2];
-#pragma unroll
-    for (int c = 0; c < DW_PJ; ++c) {
-      bh[c] = dw_frag(zh, ob[c][0], ob[c][1]);
-      bl[c] = dw_frag(zl, ob[c][0], ob[c][1]);
-    }
-    ah[0] = dw_frag(xh, oa[0][0], oa[0][1]);
-    al[0] = dw_frag(xl, oa[0][0], oa[0][1]);
-#pragma unroll
-    for (int p = 0; p < DW_PI; ++p) {
-      if (p + 1 < DW_PI) {                                // the next i-tile's fragments in flight
-        ah[(p + 1) & 1] = dw_frag(xh, oa[p + 1][0], oa[p + 1][1]);
-        al[(p + 1) & 1] = dw_frag(xl, oa[p + 1][0], oa[p + 1][1]);
-      }
-      if (wi + DW_WI * p < mtb && !(kDwAbl & 2)) {         // (wave-uniform)
-#pragma unroll
-        for (int c = 0; c < DW_PJ; ++c) {
-          if (wj + DW_WJ * c < ntb) {
-            acc[p][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[p & 1], bh[c], acc[p][c], 0, 0, 0);
-            acc[p][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[p & 1], bl[c], acc[p][c], 0, 0, 0);
-            acc[p][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[p & 1], bh[c], acc[p][c], 0, 0, 0);
-          }
-        }
-      }
-    }
-  };
-  DwSet S0{}, S1{};
-  if (nk > 0) {
-    dw_load(T, rk, S0);
-    dw_load(T, rk, S1);
-    dw_store(T, S0, img0);
-    dw_load(T, rk, S0);
-    __syncthreads();
-  }
-  // (every step unconditional, the step count rounded up to even: a step past
-  // the chunk multiplies rows that read 0 -- a conditional step or store would
-  // make the compiler merge the two steps and copy the sets, draining the loads)
-  auto step = [&](const unsigned char* rimg, unsigned char* wimg, DwSet& Sn) __attribute__((always_inline)) {
-    mul(rimg);
-    dw_store(T, Sn, wimg);
-    __builtin_amdgcn_sched_barrier(0);
-    dw_load(T, rk, Sn);
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
-  };
-  for (int it = 0; it < nk; it += 2) {
-    step(img0, img1, S1);
-    step(img1, img0, S0);
-  }
-
-  // slab s: rows i < M of the block (the layer's inputs + bias row), columns j < N
-  float* out = J.out + (long long)s * J.slab_stride;
-#pragma unroll
-  for (int p = 0; p < DW_PI; ++p) {
-    const int ti = wi + DW_WI * p;
-    if (ti >= mtb) break;
-#pragma unroll
-    for (int c = 0; c < DW_PJ; ++c) {
-      const int tj = wj + DW_WJ * c;
-      if (tj >= ntb) break;
-      const int j = j0 + 16 * tj + (lane & 15);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = i0 + 16 * ti + 4 * (lane >> 4) + q;
-        if (i < J.M && j < J.N) out[(long long)i * J.ldo + j] = acc[p][c][q];
-      }
-    }
-  }
+  typedef __attribute__((address_space(3))) unsigned char lds_u8;
+  const unsigned lbase = (unsigned)(uintptr_t)(lds_u8*)dws;     // the first image's LDS address
+  if (J.wide) dw_blocks<true>(J, T, rk, lbase, w, lane, i0, j0, mtb, ntb, s, nk);
+  else dw_blocks<false>(J, T, rk, lbase, w, lane, i0, j0, mtb, ntb, s, nk);
 }
 
 hipError_t launch_dw(hipStream_t st, const DwArgs& a) {

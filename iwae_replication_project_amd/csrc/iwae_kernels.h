@@ -373,7 +373,8 @@ struct DwJob {
   int lda, ldb, rows;
   float* out; int ldo; long long slab_stride;        // slab s at out + s * slab_stride: [M][ldo]
   int M, N, mt, nt;                                  // M = fin + 1, N = fout; 16-tiles along M / N
-  int mtb, ntb, nib, njb;                            // tiles per block (<= 13 / <= 8), blocks along M / N
+  int mtb, ntb, nib, njb;                            // tiles per block (<= 13 x 8, or wide: <= 8 x 16), blocks along M / N
+  int wide;                                          // 1: wide blocks (waves 4 x 2)
   int nsplit, chunk;                                 // row chunks (chunk % 32 == 0)
   int item0;                                         // first work item of the job (chunk-major, then N, then M block)
 };

@@ -1630,8 +1630,11 @@ static int run_dw(iwae_handle* h, const Plan& P) {
     DwJob& J = a.job[q];
     J.M = d.fin + 1; J.N = d.fout;
     J.mt = (int)cdiv(J.M, 16); J.nt = (int)cdiv(J.N, 16);
-    J.nib = (int)cdiv(J.mt, 13); J.mtb = (int)cdiv(J.mt, J.nib);
-    J.njb = (int)cdiv(J.nt, 8); J.ntb = (int)cdiv(J.nt, J.njb);
+    // blocks of up to 13 x 8 MFMA tiles ("tall"), or 8 x 16 ("wide": a narrow
+    // layer's outputs up to 256 in one block, so each row chunk is read once)
+    J.wide = J.mt <= 8 && J.nt > 8 ? 1 : 0;
+    J.nib = (int)cdiv(J.mt, J.wide ? 8 : 13); J.mtb = (int)cdiv(J.mt, J.nib);
+    J.njb = (int)cdiv(J.nt, J.wide ? 16 : 8); J.ntb = (int)cdiv(J.nt, J.njb);
     cost[q] = (double)J.mtb * J.ntb + (double)h->dw_alpha;   // + a k step's fixed cost in tile units
     W += cost[q] * J.nib * J.njb * (double)cdiv(js[q].rows, 32);
   }
