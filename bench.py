@@ -461,6 +461,23 @@ def main():
                      peak_basis="bf16x3 products: bf16 dense 2.5 PFLOP/s / 3 = 833.3 TFLOP/s per GPU",
                      workload="BASELINE configs[4] per-GPU share (4096 over 8 GPUs)",
                      precision=PRECISION)
+        # the step's kernels against their rooflines: committed rocprofv3 kernel trace + PMC
+        # record of the same step (tools/gpu_lbpmc.sh -> tools/lb_record.py)
+        lbr = os.path.join(ROOT, "profiles", "r04_large_batch_kernels.json")
+        if os.path.exists(lbr):
+            with open(lbr) as f:
+                kr = json.load(f)
+            ks = kr.get("kernels", {})
+            mf = {k: v for k, v in ks.items() if v.get("bound") == "mfma" and "frac" in v}
+            if mf:
+                dom = max(mf, key=lambda k: mf[k]["avg_us"])
+                d = mf[dom]
+                large["roofline"] = dict(bound="mfma", kernel=dom, achieved=d["tflops"], peak=d["peak_tflops"],
+                                         unit="TFLOP/s", frac=d["frac"], avg_us=d["avg_us"],
+                                         traffic=d.get("hbm_MB_per_launch"), traffic_unit="MB/launch",
+                                         source="profiles/r04_large_batch_kernels.json (rocprofv3 trace + PMC "
+                                                "of tools/train_large.py 512)")
+            large["kernels"] = ks
 
     # ---- k=5000 NLL over the test images, sharded by image
     nll = None
