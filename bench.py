@@ -89,12 +89,14 @@ def host_cores():
     return used, avail, os.cpu_count() or 1
 
 
-def _oracle_train_rate(O, seconds, threads):
-    """IWAE train steps of the oracle (B=20, k=50, 2L, float32, incl. the F:340
-    duplicate decoder pass) on `threads` BLAS threads for about `seconds`."""
+def _oracle_train_rate(O, seconds, threads, arch=None, k=None):
+    """IWAE train steps of the oracle (B=20, k=50, 2L by default, float32, incl.
+    the F:340 duplicate decoder pass) on `threads` BLAS threads for about `seconds`."""
     from threadpoolctl import threadpool_limits
+    arch = arch or (HE, HD, LE, LD)
+    k = k or K
     with threadpool_limits(limits=threads):
-        spec = O.ModelSpec(HE, HD, LE, LD)
+        spec = O.ModelSpec(*arch)
         x, pi = synthetic_images(B_PER_GPU, 1)
         rng = np.random.default_rng(2)
         params = O.cast_params(O.glorot_init(spec, rng, out_bias=O.output_bias_from_mean(pi)), np.float32)
@@ -102,8 +104,8 @@ def _oracle_train_rate(O, seconds, threads):
         xf = x.astype(np.float32)
         steps, t0 = 0, time.perf_counter()
         while True:
-            eps = O.draw_eps(spec, K, B_PER_GPU, rng, np.float32)
-            J, g = O.objective_and_grads(params, spec, xf, eps, "IWAE", K, dup_decoder=True)
+            eps = O.draw_eps(spec, k, B_PER_GPU, rng, np.float32)
+            J, g = O.objective_and_grads(params, spec, xf, eps, "IWAE", k, dup_decoder=True)
             flat = O.flatten_params(spec, params)
             new = opt.apply(flat, -O.flatten_params(spec, g).astype(np.float32))
             params = O.unflatten_params(spec, new, dtype=np.float32)
@@ -133,6 +135,19 @@ def cpu_baseline(seconds=12.0):
                 cores_note=CORES_NOTE,
                 sample=f"{steps} IWAE train steps (2L, k={K}, batch {B_PER_GPU}, float32 numpy, incl. the "
                        f"F:340 duplicate decoder pass) in {el:.1f} s on {cores} threads")
+
+
+def cpu_baseline_configs0(seconds=4.0):
+    """BASELINE configs[0] (experiment_example.py: IWAE k=5, 1 stochastic layer
+    784-200-200-50, batch 20; the reference's TF CPU path): the oracle's train
+    steps on the host cores, float32 -- the CPU figure beside configs0_train."""
+    from oracle import iwae_oracle as O
+    cores, avail, nproc = host_cores()
+    _oracle_train_rate(O, 0.3, cores, arch=([200], [200], [50], [784]), k=5)      # warm-up (first BLAS calls)
+    steps, el = _oracle_train_rate(O, seconds, cores, arch=([200], [200], [50], [784]), k=5)
+    return dict(value=steps * B_PER_GPU * 5 / el, unit="image*samples/s", cores=cores, kind="port",
+                sample=f"{steps} IWAE train steps (1L 784-200-200-50, k=5, batch {B_PER_GPU}, float32 numpy, incl. "
+                       f"the F:340 duplicate decoder pass) in {el:.1f} s on {cores} threads")
 
 
 def cpu_baseline_nll(seconds=8.0, k=5000):
@@ -578,10 +593,12 @@ def main():
                   ms_per_step=round(1e3 * el4 / args.c0_steps, 5),
                   tflops=round(1_438_240 * c0rows / el4 / 1e12, 3))
 
-    cpu = cpu_nll = None
+    cpu = cpu_nll = cpu_c0 = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_seconds)
         cpu_nll = cpu_baseline_nll(max(4.0, args.cpu_seconds / 2))
+        if c0 is not None:
+            cpu_c0 = cpu_baseline_configs0(max(2.0, args.cpu_seconds / 3))
 
     if rank == 0:
         out = {
@@ -614,6 +631,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_baseline_nll": cpu_nll,
+            "cpu_baseline_configs0": cpu_c0,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
