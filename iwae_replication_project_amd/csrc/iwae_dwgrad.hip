@@ -81,14 +81,13 @@ __device__ __forceinline__ dw_f32x4 dw_ld4(__amdgpu_buffer_rsrc_t r, unsigned of
 // buffer resources cover the row chunk (rows past its end read 0) and are built
 // once; the per-lane offsets advance by one k step per request.
 struct DwTask {
-  int role[DW_TASKS];
+  int role[DW_TASKS];                    // (wave-uniform)
   __amdgpu_buffer_rsrc_t rs[DW_TASKS];   // the piece's matrix (X or dZ) over the chunk
-  unsigned goff[DW_TASKS];     // byte offset of the piece for the next request (kOOB: past the width)
-  unsigned ginc[DW_TASKS];     // bytes per k step (32 rows)
+  unsigned ginc[DW_TASKS];               // bytes per k step (32 rows; wave-uniform)
+  unsigned goff[DW_TASKS];     // byte offset of the piece for the next request (past the width: >= kOOB,
+                               // which stays out of range however far it advances)
   unsigned koff[DW_TASKS];     // byte offset of the row scale (dZ pieces) for the next request
-  float kadd[DW_TASKS];        // 1 for X pieces (their row-scale load reads 0), 0 for dZ pieces
   int loff[DW_TASKS];          // LDS byte offset of the piece in the hi plane of its image
-  int lplane[DW_TASKS];        // bytes from the hi to the lo plane
 };
 struct DwSet {
   dw_f32x4 v[DW_TASKS];
@@ -113,7 +112,8 @@ __device__ __forceinline__ void dw_store(const DwTask& T, const DwSet& S, unsign
 #pragma unroll
   for (int u = 0; u < DW_TASKS; ++u) {
     if (T.role[u] == 0) continue;                         // (wave-uniform; no load inside)
-    const dw_f32x4 v = S.v[u] * (S.k[u] + T.kadd[u]);     // dZ times its row scale (X: times 1)
+    // dZ times its row scale (X: the scale's load read 0, times 1)
+    const dw_f32x4 v = S.v[u] * (S.k[u] + (T.role[u] == 2 ? 0.f : 1.f));
     const dw_f32x2 a = {v[0], v[1]}, b = {v[2], v[3]};
     const unsigned ha = __builtin_bit_cast(unsigned, __builtin_convertvector(a, dw_bf16x2));
     const unsigned hb = __builtin_bit_cast(unsigned, __builtin_convertvector(b, dw_bf16x2));
@@ -122,7 +122,7 @@ __device__ __forceinline__ void dw_store(const DwTask& T, const DwSet& S, unsign
     const unsigned la = __builtin_bit_cast(unsigned, __builtin_convertvector(ra, dw_bf16x2));
     const unsigned lb = __builtin_bit_cast(unsigned, __builtin_convertvector(rb, dw_bf16x2));
     *reinterpret_cast<dw_u32x2*>(img + T.loff[u]) = dw_u32x2{ha, hb};
-    *reinterpret_cast<dw_u32x2*>(img + T.lplane[u]) = dw_u32x2{la, lb};
+    *reinterpret_cast<dw_u32x2*>(img + T.loff[u] + (T.role[u] == 2 ? DW_ZP : DW_XP)) = dw_u32x2{la, lb};
   }
 }
 
@@ -290,25 +290,25 @@ __global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
     T.rs[u] = role == 1 ? rx : rz;
     int row = 0, c = 0;
     bool ok = false;
+    // (an out-of-range piece starts at kOOB: after at most ~900 k steps of <= 100 KB
+    // it is still below 2^32 and above any buffer range)
     if (role == 1) {
       row = tau / nqx; c = 4 * (tau - row * nqx);
       ok = i0 + c < J.M;
       T.goff[u] = ok ? (unsigned)(row * J.lda + i0 + c) * 4u : kOOB;
-      T.ginc[u] = ok ? (unsigned)(DW_KR * J.lda) * 4u : 0u;
+      T.ginc[u] = (unsigned)(DW_KR * J.lda) * 4u;
     } else if (role == 2) {
       const int tz = tau - DW_KR * nqx;
       row = tz / nqz; c = 4 * (tz - row * nqz);
       ok = j0 + c < J.N;
       T.goff[u] = ok ? (unsigned)(row * J.ldb + j0 + c) * 4u : kOOB;
-      T.ginc[u] = ok ? (unsigned)(DW_KR * J.ldb) * 4u : 0u;
+      T.ginc[u] = (unsigned)(DW_KR * J.ldb) * 4u;
     } else {
       T.goff[u] = kOOB;
       T.ginc[u] = 0u;
     }
     T.koff[u] = role == 2 ? (unsigned)row * 4u : kOOB;
-    T.kadd[u] = role == 2 ? 0.f : 1.f;
     T.loff[u] = (role == 2 ? 2 * DW_XP : 0) + dw_off(row, c);
-    T.lplane[u] = T.loff[u] + (role == 2 ? DW_ZP : DW_XP);
   }
   typedef __attribute__((address_space(3))) unsigned char lds_u8;
   const unsigned lbase = (unsigned)(uintptr_t)(lds_u8*)dws;     // the first image's LDS address
