@@ -128,7 +128,7 @@ enum iwae_knob {
   IWAE_KNOB_MG_WAVES = 16,     /* NLL kernel workgroup: 8 waves / 64 rows or 4 waves / 32 rows (8) */
   IWAE_KNOB_NLL_ROWS = 17,     /* sample rows per NLL chunk (2^20) */
   IWAE_KNOB_WIDE_ROWS = 18,    /* engine: 32 / 64-row workgroups from this many sample rows (4097) */
-  IWAE_KNOB_DW_WIDE = 19,      /* beyond UPD_ROWS: weight gradients on the 208 x 128-block kernel (0) */
+  IWAE_KNOB_DW_WIDE = 19,      /* beyond UPD_ROWS: weight gradients on the 208 x 128-block kernel (1) */
   IWAE_KNOB_LD_ALIGN = 20,     /* workspace row strides: multiples of 4, 8, 16 or 32 floats (4) */
   IWAE_KNOB_NRING = 21,        /* NLL: the weight-ring kernel where its model shapes apply (1) */
   IWAE_KNOB_NRING_TRAIN = 22,  /* train-step forward on the weight-ring kernel (1) ... */
@@ -145,7 +145,10 @@ enum iwae_knob {
   IWAE_KNOB_DW_WG = 28,            /* workgroups the DW_WIDE weight-gradient pass balances its row chunks over (256) */
   IWAE_KNOB_PIWAE_ONE = 29         /* PIWAE on the engine: one unit-weight backward chain for both weightings (1);
                                       0: the chain twice (IWAE_{k1 k2}, then MIWAE for the encoder) */,
-  IWAE_KNOB_DW_ALPHA = 30          /* DW_WIDE pass cost model: a k step's fixed cost in MFMA tiles (0) */
+  IWAE_KNOB_DW_ALPHA = 30,         /* DW_WIDE pass cost model: a k step's fixed cost in MFMA tiles (150) */
+  IWAE_KNOB_IMG_ROWS_FWD = 31,     /* image-row job I (first encoder layer's l2 / head): images per workgroup,
+                                      <= 16 (0: auto, ceil(B / 256)) */
+  IWAE_KNOB_IMG_ROWS_BWD = 32      /* image-row job I' (its backward): images per workgroup (0: auto) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --

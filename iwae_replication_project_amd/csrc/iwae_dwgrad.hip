@@ -67,6 +67,17 @@ constexpr int kDwAbl = IWAE_DW_ABL;
 
 extern __shared__ __attribute__((aligned(16))) unsigned char dws[];
 
+#ifdef IWAE_DW_TRACE
+// per workgroup (<= 256): [0] item, [1] k steps, [2] start, then per k step
+// (<= 80) the s_memtime after the multiply's issue, after the staging + next
+// request, after the barrier; [3 + 240] end (wave 0, lane 0; debug builds)
+constexpr int kDwTr = 3 + 3 * 80 + 1;
+__device__ unsigned long long g_dw_trace[256 * kDwTr];
+#define DW_TR(slot) do { if (tr) g_dw_trace[blockIdx.x * kDwTr + (slot)] = wall_clock64(); } while (0)
+#else
+#define DW_TR(slot) do { } while (0)
+#endif
+
 __device__ __forceinline__ int dw_swz(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
 // byte offset of column c (16-bit elements, 0..255) of row k in a plane
 __device__ __forceinline__ int dw_off(int k, int c) {
@@ -106,12 +117,11 @@ __device__ __forceinline__ void dw_load(DwTask& T, __amdgpu_buffer_rsrc_t rk, Dw
   }
 }
 
-// the set's pieces -> bf16 hi / lo, row-major into image `img`
-__device__ __forceinline__ void dw_store(const DwTask& T, const DwSet& S, unsigned char* img) {
+// piece u of the set -> bf16 hi / lo, row-major into image `img`
+__device__ __forceinline__ void dw_store1(const DwTask& T, const DwSet& S, unsigned char* img, int u) {
   if (kDwAbl & 8) return;
-#pragma unroll
-  for (int u = 0; u < DW_TASKS; ++u) {
-    if (T.role[u] == 0) continue;                         // (wave-uniform; no load inside)
+  {
+    if (T.role[u] == 0) return;                           // (wave-uniform; no load inside)
     // dZ times its row scale (X: the scale's load read 0, times 1)
     const dw_f32x4 v = S.v[u] * (S.k[u] + (T.role[u] == 2 ? 0.f : 1.f));
     const dw_f32x2 a = {v[0], v[1]}, b = {v[2], v[3]};
@@ -124,6 +134,10 @@ __device__ __forceinline__ void dw_store(const DwTask& T, const DwSet& S, unsign
     *reinterpret_cast<dw_u32x2*>(img + T.loff[u]) = dw_u32x2{ha, hb};
     *reinterpret_cast<dw_u32x2*>(img + T.loff[u] + (T.role[u] == 2 ? DW_ZP : DW_XP)) = dw_u32x2{la, lb};
   }
+}
+__device__ __forceinline__ void dw_store(const DwTask& T, const DwSet& S, unsigned char* img) {
+#pragma unroll
+  for (int u = 0; u < DW_TASKS; ++u) dw_store1(T, S, img, u);
 }
 
 // fragment of a 16-column tile from the plane at `pl`: two transposed reads at
@@ -179,7 +193,11 @@ __device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask& T, __amdgpu_bu
   // requested two steps earlier) is split into the other image; that set then
   // requests step it + 3.  The loop is unrolled by two so each set keeps its
   // registers (no renaming copy at the back edge, which would drain the loads).
-  auto mul = [&](int img) __attribute__((always_inline)) {    // img: the image's byte offset (0 or DW_IMG)
+  // the multiply of image img with the staging of set Sn into wimg interleaved:
+  // piece q is split and written after stream slot q's MFMAs are issued (the
+  // VALU and LDS writes overlap the matrix core; a separate staging phase
+  // after the multiply left them serialized behind the barrier)
+  auto mul = [&](int img, const DwSet& Sn, unsigned char* wimg) __attribute__((always_inline)) {
     const int xh = img, xl = img + DW_XP, zh = img + 2 * DW_XP, zl = zh + DW_ZP;
     const int sh_p = WIDE ? zh : xh, sl_p = WIDE ? zl : xl, hh_p = WIDE ? xh : zh, hl_p = WIDE ? xl : zl;
     dw_bf16x8 hh[DW_NH], hl[DW_NH], sh[2], sl[2];
@@ -211,7 +229,10 @@ __device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask& T, __amdgpu_bu
           }
         }
       }
+      if (q >= 1 && q - 1 < DW_TASKS) dw_store1(T, Sn, wimg, q - 1);
     }
+#pragma unroll
+    for (int u = NS - 1; u < DW_TASKS; ++u) dw_store1(T, Sn, wimg, u);
   };
   DwSet S0{}, S1{};
   if (nk > 0) {
@@ -224,18 +245,34 @@ __device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask& T, __amdgpu_bu
   // (every step unconditional, the step count rounded up to even: a step past
   // the chunk multiplies rows that read 0 -- a conditional step or store would
   // make the compiler merge the two steps and copy the sets, draining the loads)
+#ifdef IWAE_DW_TRACE
+  const bool tr = threadIdx.x == 0 && blockIdx.x < 256;
+  if (tr) { g_dw_trace[blockIdx.x * kDwTr + 1] = nk; }
+  int ks = 0;
+#endif
   auto step = [&](int rimg, unsigned char* wimg, DwSet& Sn) __attribute__((always_inline)) {
-    mul(rimg);
-    dw_store(T, Sn, wimg);
+    mul(rimg, Sn, wimg);
+#ifdef IWAE_DW_TRACE
+    if (ks < 80) DW_TR(3 + 3 * ks);
+#endif
     __builtin_amdgcn_sched_barrier(0);
     dw_load(T, rk, Sn);
     __builtin_amdgcn_sched_barrier(0);
+#ifdef IWAE_DW_TRACE
+    if (ks < 80) DW_TR(4 + 3 * ks);
+#endif
     __syncthreads();
+#ifdef IWAE_DW_TRACE
+    if (ks < 80) DW_TR(5 + 3 * ks);
+    ++ks;
+#endif
   };
+  DW_TR(2);
   for (int it = 0; it < nk; it += 2) {
     step(0, img1, S1);
     step(DW_IMG, img0, S0);
   }
+  DW_TR(kDwTr - 1);
 
   // slab s: rows i < M of the block (the layer's inputs + bias row), columns j < N
   float* out = J.out + (long long)s * J.slab_stride;
@@ -261,6 +298,9 @@ __global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
   const int bx = blockIdx.x, x = bx & 7, sl = bx >> 3;
   const int item = x * a.per_xcd + sl;
   if (sl >= a.per_xcd || item >= a.nitems) return;
+#ifdef IWAE_DW_TRACE
+  if (threadIdx.x == 0 && bx < 256) g_dw_trace[bx * kDwTr] = item;
+#endif
   int jb = 0;
   while (jb + 1 < a.njobs && item >= a.job[jb + 1].item0) ++jb;
   const DwJob& J = a.job[jb];
@@ -315,6 +355,15 @@ __global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
   if (J.wide) dw_blocks<true>(J, T, rk, lbase, w, lane, i0, j0, mtb, ntb, s, nk);
   else dw_blocks<false>(J, T, rk, lbase, w, lane, i0, j0, mtb, ntb, s, nk);
 }
+
+#ifdef IWAE_DW_TRACE
+extern "C" int iwae_dw_trace_dump(unsigned long long* out, int cap) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  const int n = 256 * kDwTr < cap ? 256 * kDwTr : cap;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dw_trace), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+  return n;
+}
+#endif
 
 hipError_t launch_dw(hipStream_t st, const DwArgs& a) {
   if (a.nitems <= 0) return hipSuccess;

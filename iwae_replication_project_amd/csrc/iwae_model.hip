@@ -199,13 +199,16 @@ struct iwae_handle {
   int upd_tn32 = 0;                  // ... sample-row layers in 64 x 32 tiles
   int upd_slabs = 1;                 // ... and beyond upd_rows its split-K gradient pass into the slabs
   long long upd_slab_wg = 512;       // sample-row workgroups of that pass
-  int dw_wide = 0;                   // ... run by the 208 x 128-block weight-gradient kernel (iwae_dwgrad.hip)
+  int dw_wide = 1;                   // ... run by the 208 x 128-block weight-gradient kernel (iwae_dwgrad.hip;
+                                     // B = 512: 107 vs 152 us for the update kernel's pass, step 0.513 -> 0.473 ms)
   long long dw_target = 768;         // split-K target workgroups per layer of the grouped weight-gradient GEMMs
   int smallm_rows = 32;              // first encoder layer on the few-row launches up to this many images (0: never)
   long long nll_rows = 1LL << 20;    // sample rows per NLL chunk (measured fastest: 2^17-2^20 within 10 %)
   int nll_imgs = 0;                  // images per NLL chunk when the caller passes chunk 0 (0: nll_rows / k)
   int dw_wg = 256;                   // large-batch weight-gradient pass: workgroups its row chunks aim at
-  int dw_alpha = 0;                  // ... its cost model: a k step's fixed cost in MFMA tiles
+  int dw_alpha = 150;                // ... its cost model: a k step's fixed cost in MFMA tiles (measured: a
+                                     // k step costs ~2 us whatever its tiles; alpha 0 / 45 / 90 / 200: 174 / 127 / 108 / 106 us)
+  int img_rows_fwd = 0, img_rows_bwd = 0;   // image-row jobs I / I': rows per workgroup (0: auto)
   int piwae_one = 1;                 // PIWAE: one unit-weight backward chain serves both weightings (knob)
   bool piwae_ks = false;             // (during a step) the weight gradients apply the per-layer PIWAE weighting
   int tc_rt = 1;                     // row tiles of 16 per engine workgroup below wide_rows
@@ -1998,7 +2001,10 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
   const bool img = which == 2 || which == 3;
   const long long rows = img ? (long long)P.Bimg : (long long)P.Bimg * kS;
   // image rows: one image per workgroup (latency-bound chains of a few rows), up to 256 workgroups
-  const int row_step = img ? (int)std::max<long long>(1, cdiv(P.Bimg, 256)) : 0;
+  // (knobs img_rows_fwd / img_rows_bwd: rows per workgroup of job I / I' instead)
+  int row_step = img ? (int)std::max<long long>(1, cdiv(P.Bimg, 256)) : 0;
+  if (which == 2 && h->img_rows_fwd > 0) row_step = h->img_rows_fwd;
+  if (which == 3 && h->img_rows_bwd > 0) row_step = h->img_rows_bwd;
   // rows per workgroup: 16 (four-set pipeline) below wide_rows, else the
   // widest the LDS allows (two-set pipeline)
   const int want = wide ? (which == 0 ? 4 : h->wide_rt) : h->tc_rt;
@@ -2849,6 +2855,8 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_DW_WG: h->dw_wg = (int)std::max(8LL, std::min(value, 4096LL)); break;
     case IWAE_KNOB_PIWAE_ONE: h->piwae_one = on; break;
     case IWAE_KNOB_DW_ALPHA: h->dw_alpha = (int)std::max(0LL, std::min(value, 1000LL)); break;
+    case IWAE_KNOB_IMG_ROWS_FWD: h->img_rows_fwd = (int)std::max(0LL, std::min(value, 16LL)); break;
+    case IWAE_KNOB_IMG_ROWS_BWD: h->img_rows_bwd = (int)std::max(0LL, std::min(value, 16LL)); break;
     case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;

@@ -1,0 +1,49 @@
+"""Per-workgroup k-step timeline of the large-batch weight-gradient kernel
+(dw_kernel) from a -DIWAE_DW_TRACE build (tools/build_debug.sh), run with
+IWAE_HIP_LIB pointing at it: B=512 train steps with dw_wide=1, then per
+workgroup its item, k steps, duration and the average split of a k step
+(multiply issue / staging + next request / barrier wait), wall_clock64 ticks
+of 10 ns.   python tools/dw_trace.py [alpha]"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+import bench  # noqa: E402
+from iwae_replication_project_amd import Adam, Flexible_Model  # noqa: E402
+
+alpha = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+B = 512
+x, pi = bench.synthetic_images(2 * B, 1)
+m = Flexible_Model(bench.HE, bench.HD, bench.LE, bench.LD, dataset_bias=pi, loss_function="IWAE", k=50, seed=2,
+                   tuning={"dw_wide": 1, "dw_alpha": alpha})
+m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+xd = m._x(x)
+for i in range(4):
+    m.train_step(xd[(i % 2) * B:(i % 2 + 1) * B], sync=False)
+torch.cuda.synchronize()
+K = 3 + 3 * 80 + 1
+buf = (ctypes.c_ulonglong * (256 * K))()
+dump = m._lib.iwae_dw_trace_dump
+dump.restype = ctypes.c_int
+n = dump(buf, 256 * K)
+rows = []
+for b in range(256):
+    r = buf[b * K:(b + 1) * K]
+    item, nk, t0, t1 = r[0], r[1], r[2], r[K - 1]
+    if nk == 0 or t1 <= t0:
+        continue
+    ks = min(nk + (nk & 1), 80)
+    mul = sum(r[3 + 3 * j] - (r[5 + 3 * (j - 1)] if j else t0) for j in range(ks)) / ks
+    stg = sum(r[4 + 3 * j] - r[3 + 3 * j] for j in range(ks)) / ks
+    bar = sum(r[5 + 3 * j] - r[4 + 3 * j] for j in range(ks)) / ks
+    rows.append((t1 - t0, b, item, nk, mul, stg, bar))
+rows.sort(reverse=True)
+tmin = min(buf[b * K + 2] for b in range(256) if buf[b * K + 1])
+print("ticks of 10 ns; per k step: multiply issue / staging + request / barrier wait")
+for d, b, item, nk, mul, stg, bar in rows[:40]:
+    print(f"wg {b:3d} item {item:3d} nk {nk:3d}  start {buf[b * K + 2] - tmin:6d}  dur {d:6d}  per-k {d / max(nk, 1):7.1f}"
+          f"   mul {mul:6.1f} stage {stg:6.1f} barrier {bar:6.1f}")
+print(f"... {len(rows)} workgroups; shortest {rows[-1][0]}")
