@@ -59,7 +59,8 @@ constexpr int DW_IMG = 2 * DW_XP + 2 * DW_ZP; // X hi, X lo, dZ hi, dZ lo: 64 Ki
 constexpr int DW_TASKS = 3072 / DW_NT;        // 16-byte pieces per thread and k step (<= 3072 = 32 x (64 + 32))
 
 // timing ablations (debug builds only, -DIWAE_DW_ABL=<mask>; WRONG results):
-// 1 loads never advance (L2 hits), 2 no MFMAs, 4 no loads, 8 no LDS staging
+// 1 loads never advance (L2 hits), 2 no MFMAs, 4 no loads, 8 no LDS staging,
+// 16 no fragment reads
 #ifndef IWAE_DW_ABL
 #define IWAE_DW_ABL 0
 #endif
@@ -151,6 +152,11 @@ __device__ __forceinline__ int dw_frag_off(int t, int lane, int h) {
 // first image, a compile-time constant per call, so each read is one
 // ds_read_b64_tr_b16 with an immediate offset and no address arithmetic)
 __device__ __forceinline__ dw_bf16x8 dw_frag(int pl, unsigned o0, unsigned o1) {
+  if (kDwAbl & 16) {                                      // (ablation: no fragment reads)
+    dw_u32x4 z = {o0, o1, o0 ^ o1, (unsigned)pl};
+    asm volatile("" : "+v"(z));
+    return __builtin_bit_cast(dw_bf16x8, z);
+  }
   typedef __attribute__((address_space(3))) dw_s16x4 lds_s16x4;
   const dw_s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(o0 + pl));
   const dw_s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(o1 + pl));
@@ -214,10 +220,13 @@ __device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask& T, __amdgpu_bu
         sh[(q + 1) & 1] = dw_frag(sh_p, os[q + 1][0], os[q + 1][1]);
         sl[(q + 1) & 1] = dw_frag(sl_p, os[q + 1][0], os[q + 1][1]);
       }
-      if (st_tile(q) < st_n && !(kDwAbl & 2)) {           // (wave-uniform)
+      // (unconditional: a slot past the block multiplies image columns that exist
+      // and its accumulator is never stored -- branches around the MFMAs kept the
+      // compiler from overlapping the next slot's reads with them)
+      if (!(kDwAbl & 2)) {
 #pragma unroll
         for (int h = 0; h < DW_NH; ++h) {
-          if (hd_tile(h) < hd_n) {
+          {
             // bf16x3: A = X^T (i), B = dZ (j): a_hi b_hi + a_hi b_lo + a_lo b_hi
             const dw_bf16x8& ahi = WIDE ? hh[h] : sh[q & 1];
             const dw_bf16x8& alo = WIDE ? hl[h] : sl[q & 1];
