@@ -48,14 +48,21 @@ __device__ __forceinline__ float ftanh(float x) {
 // base_hi), key = seed; normal q of group g is the noise of column 4g + q.
 // Every kernel that draws noise (fused and layer-wise paths, training and NLL)
 // uses this one function, so both paths draw the identical stream.
+// One Philox multiply: the 64-bit product of a 32-bit constant and a counter
+// word (a single v_mad_u64_u32 in its place measured +0.2 % on the NLL: kept plain)
+__device__ __forceinline__ void philox_mul(unsigned k, unsigned c, unsigned& lo, unsigned& hi) {
+  lo = k * c;
+  hi = __umulhi(k, c);
+}
 __device__ __forceinline__ float4 philox_normal4(uint64_t seed, uint64_t base, unsigned row, unsigned layer,
                                                  unsigned grp) {
   unsigned c0 = row, c1 = (layer << 20) | grp, c2 = (unsigned)base, c3 = (unsigned)(base >> 32);
   unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-    const unsigned lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-    const unsigned lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    unsigned lo0, hi0, lo1, hi1;
+    philox_mul(0xD2511F53u, c0, lo0, hi0);
+    philox_mul(0xCD9E8D57u, c2, lo1, hi1);
     c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
@@ -76,8 +83,9 @@ __device__ __forceinline__ float2 philox_normal2(uint64_t seed, uint64_t base, u
   unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-    const unsigned lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-    const unsigned lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    unsigned lo0, hi0, lo1, hi1;
+    philox_mul(0xD2511F53u, c0, lo0, hi0);
+    philox_mul(0xCD9E8D57u, c2, lo1, hi1);
     c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }

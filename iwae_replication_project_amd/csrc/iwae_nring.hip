@@ -99,7 +99,19 @@ struct NrFrag {
 __device__ __forceinline__ int nr_wave() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 // NLL-path tanh (mega_fwd_kernel's): 1 - 2 / (exp(2x) + 1)
-__device__ __forceinline__ float nr_tanh(float x) { return __builtin_fmaf(-2.f, frcp(fexp(2.f * x) + 1.f), 1.f); }
+// (exp(2x) as one v_mul by 2 log2 e and v_exp: bitwise __expf(2.f * x), whose
+// v_add x + x and v_mul by log2 e round identically -- the doubling is exact)
+__device__ __forceinline__ float nr_tanh(float x) {
+  return __builtin_fmaf(-2.f, frcp(__builtin_amdgcn_exp2f(x * 0x1.715476p+1f) + 1.f), 1.f);
+}
+
+// c ? v : 0 with v computed unconditionally: a select, not an exec-masked
+// branch around v's computation (hipcc sinks `c ? f(x) : 0` into a divergent
+// branch, ~6 scalar instructions and the loss of the epilogue's interleave)
+__device__ __forceinline__ float nr_mask(bool c, float v) {
+  asm volatile("" : "+v"(v));
+  return c ? v : 0.f;
+}
 
 // TFP Normal(mu, sc).log_prob(h), raw v_rcp / v_log (sc >= 1e-6 is normal)
 __device__ __forceinline__ float nr_normal_logp(float h, float mu, float sc) {
@@ -177,10 +189,13 @@ __device__ __forceinline__ void nr_pairs_to_frag(const float2 (&hp)[NT], NrFrag&
 }
 
 // LDS byte offsets (nrs is the kernel's only LDS object, at address 0):
-// the ring, then the pixel cache [2][NR_PIXLD] floats, then the unit table
+// the ring, then the pixel cache [NR_PIXIMG][NR_PIXLD] floats, then the unit table
 // [kNrMaxUnits] (off, ns) pairs (zero past the last unit: ns 0 = no pieces)
 constexpr unsigned NR_PIX_B = NR_D * NR_SLOT_BF16 * 2;
 constexpr unsigned NR_TAB_B = NR_PIX_B + NR_PIXIMG * NR_PIXLD * 4;
+// then the Bernoulli pixel-bit words [NR_PIXIMG][4 lane groups][<= 8 words]
+constexpr unsigned NR_BITS_B = NR_TAB_B + 8 * kNrMaxUnits;
+constexpr unsigned NR_BITS_WORDS = NR_PIXIMG * 4 * 8;
 
 // a wave's row: its index, whether it exists, the log-density sums (natural
 // log q, log p; the Bernoulli sum in log2) and a resource that drops every
@@ -364,12 +379,22 @@ __device__ __forceinline__ auto nr_dense_tanh(NrCtx& C, const NrStage& S, const 
   static_assert(NT <= 2 * NSO, "tiles beyond the reader's k steps");
   const int g = (threadIdx.x & 63) >> 4;
   auto epi = [&S, &OUT, &R, g](int t, const nr_f32x4& a, float (&va)[4], bool real) {
+    // tiles before the last real one are whole (ntile = ceil(N / 16), checked by
+    // nring_shape_id): no column test; the last and the padding tiles select
+    // the value, the ones column at N or zero
+    const bool edge = !real || t == NT - 1;
     float v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = 16 * t + 4 * g + i;
       // (train mode: the train engine's tanh, whose outputs the backward's TGRAD reads)
-      v[i] = (real && f < S.N) ? (TR ? ftanh(a[i]) : nr_tanh(a[i])) : (f == S.N ? 1.f : 0.f);
+      float th = real ? (TR ? ftanh(a[i]) : nr_tanh(a[i])) : 0.f;
+      if (edge) {
+        asm volatile("" : "+v"(th));
+        v[i] = (real && f < S.N) ? th : (f == S.N ? 1.f : 0.f);
+      } else {
+        v[i] = th;
+      }
     }
     if (TR && real) {
       const int f0 = 16 * t + 4 * g;
@@ -428,8 +453,8 @@ __device__ __forceinline__ auto nr_head_sample(NrCtx& C, const NrStage& S, const
       const int j = j0 + c;
       const float sc = fexp(zs[c]) + kScaleEps;
       const float h = (c == 0 ? ep[t].x : ep[t].y) * sc + mu[c];
-      R.q += j < d ? nr_normal_logp(h, mu[c], sc) : 0.f;
-      if (S.stdnormal) R.p += j < d ? -0.5f * (h * h) - kHalfLog2Pi : 0.f;
+      R.q += nr_mask(j < d, nr_normal_logp(h, mu[c], sc));
+      if (S.stdnormal) R.p += nr_mask(j < d, -0.5f * (h * h) - kHalfLog2Pi);
       hv[c] = j < d ? h : (j == d ? 1.f : 0.f);
     }
     hp[t] = make_float2(hv[0], hv[1]);
@@ -517,7 +542,7 @@ __device__ __forceinline__ auto nr_head_prior(NrCtx& C, const NrStage& S, const 
     for (int c = 0; c < 2; ++c) {
       const float sc = fexp(zs[c]) + kScaleEps;
       const float v = nr_normal_logp(c == 0 ? tp[t].x : tp[t].y, mu[c], sc);
-      R.p += j0 + c < d ? v : 0.f;
+      R.p += nr_mask(j0 + c < d, v);
     }
     if (TR) {
       const bool ok = R.valid && j0 < d;
@@ -763,12 +788,17 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
     if constexpr (L2) nr_noise_pairs(A, nullptr, 1, A.st[2].d, base, grow, ep2);
   }
   // pixel bits of this row's image in the Bernoulli epilogues' order: the
-  // epilogue of tile t (columns 16 t + 4 g .. + 3) runs in phase t + 1
-  unsigned pw[(P.NTB + 8) / 8];
+  // epilogue of tile t (columns 16 t + 4 g .. + 3) runs in phase t + 1.  The
+  // words of the workgroup's images ([image][lane group][word]) are built once
+  // into LDS by the first NR_PIXIMG * 4 * NWD threads, not by every row
+  constexpr int NWD = (P.NTB + 8) / 8;
+  static_assert(NWD <= 8 && NR_PIXIMG * 4 * NWD <= NR_W * 64, "pixel-bit words");
+  unsigned pw[NWD];
   {
-    const float* pr = pix + (grow / A.kS - img_a) * NR_PIXLD + 4 * g;
-#pragma unroll
-    for (int w = 0; w < (P.NTB + 8) / 8; ++w) {
+    unsigned* bits = reinterpret_cast<unsigned*>(nrs) + NR_BITS_B / 4;
+    if (t < NR_PIXIMG * 4 * NWD) {
+      const int im = t / (4 * NWD), gg = (t / NWD) % 4, w = t % NWD;
+      const float* pr = pix + im * NR_PIXLD + 4 * gg;
       unsigned b = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -781,8 +811,14 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
           b |= (xv.w != 0.f ? 8u : 0u) << (4 * j);
         }
       }
-      pw[w] = b;
-      asm volatile("" : "+v"(pw[w]));            // built here, not sunk into the ring
+      bits[t] = b;
+    }
+    __syncthreads();                             // before the first DMA: a plain barrier
+    const unsigned* br = bits + ((grow / A.kS - img_a) * 4 + g) * NWD;
+#pragma unroll
+    for (int w = 0; w < NWD; ++w) {
+      pw[w] = br[w];
+      asm volatile("" : "+v"(pw[w]));            // read here, not sunk into the ring
     }
   }
   // ---- h1 = eps * s0 + mu0 of the row's image in the pair layout, log q(h1 | x)
@@ -799,8 +835,8 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
         const int j = j0 + c;
         const float sc = fexp(zs0[tt][c]) + kScaleEps;
         const float h = (c == 0 ? ep1[tt].x : ep1[tt].y) * sc + mu0[tt][c];
-        R.q += j < d ? nr_normal_logp(h, mu0[tt][c], sc) : 0.f;
-        if (!L2) R.p += j < d ? -0.5f * (h * h) - kHalfLog2Pi : 0.f;
+        R.q += nr_mask(j < d, nr_normal_logp(h, mu0[tt][c], sc));
+        if (!L2) R.p += nr_mask(j < d, -0.5f * (h * h) - kHalfLog2Pi);
         hv[c] = j < d ? h : (j == d ? 1.f : 0.f);
       }
       hp1[tt] = make_float2(hv[0], hv[1]);
@@ -887,7 +923,7 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
   }
 }
 
-size_t nring_lds_bytes() { return (size_t)NR_TAB_B + 8 * kNrMaxUnits; }
+size_t nring_lds_bytes() { return (size_t)NR_BITS_B + 4 * NR_BITS_WORDS; }
 
 // host: the shape id of a plan (stage ns / ntile filled), or -1 (mega_fwd_kernel runs)
 static int nring_shape_id(const NrLaunch& L) {
@@ -905,6 +941,9 @@ static int nring_shape_id(const NrLaunch& L) {
            L.st[3].next_ns == P.PH && L.st[4].ns == P.PH && L.st[4].ntile == P.NTP && L.st[4].next_ns == P.PH &&
            L.st[5].ns == P.PH && L.st[5].ntile == P.NTPH && L.st[5].d == L.d0 && P.NTPH <= 4 * P.H1 &&
            L.st[0].N % 4 == 0 && L.st[1].N % 4 == 0 && L.st[3].N % 4 == 0 && L.st[4].N % 4 == 0;
+    // the tanh epilogues take every tile before the last as whole
+    for (int k = (P.L == 2 ? 0 : 6); k < 8; ++k)
+      if (k != 2 && k != 5) ok = ok && L.st[k].ntile == (L.st[k].N + 15) / 16;
     if (ok) return i;
   }
   return -1;
