@@ -54,6 +54,13 @@ __device__ __forceinline__ void philox_mul(unsigned k, unsigned c, unsigned& lo,
   lo = k * c;
   hi = __umulhi(k, c);
 }
+// a ^ b ^ k in one gfx950 v_bitop3_b32 (truth table 0x96); k is the
+// wave-uniform Philox key word
+__device__ __forceinline__ unsigned philox_xor3(unsigned a, unsigned b, unsigned k) {
+  unsigned r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+  return r;
+}
 __device__ __forceinline__ float4 philox_normal4(uint64_t seed, uint64_t base, unsigned row, unsigned layer,
                                                  unsigned grp) {
   unsigned c0 = row, c1 = (layer << 20) | grp, c2 = (unsigned)base, c3 = (unsigned)(base >> 32);
@@ -63,7 +70,7 @@ __device__ __forceinline__ float4 philox_normal4(uint64_t seed, uint64_t base, u
     unsigned lo0, hi0, lo1, hi1;
     philox_mul(0xD2511F53u, c0, lo0, hi0);
     philox_mul(0xCD9E8D57u, c2, lo1, hi1);
-    c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
+    c0 = philox_xor3(hi1, c1, k0); c1 = lo1; c2 = philox_xor3(hi0, c3, k1); c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
   constexpr float k2m32 = 2.3283064365386963e-10f;
@@ -86,7 +93,7 @@ __device__ __forceinline__ float2 philox_normal2(uint64_t seed, uint64_t base, u
     unsigned lo0, hi0, lo1, hi1;
     philox_mul(0xD2511F53u, c0, lo0, hi0);
     philox_mul(0xCD9E8D57u, c2, lo1, hi1);
-    c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
+    c0 = philox_xor3(hi1, c1, k0); c1 = lo1; c2 = philox_xor3(hi0, c3, k1); c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
   constexpr float k2m32 = 2.3283064365386963e-10f;

@@ -519,7 +519,12 @@ __device__ __forceinline__ void nr_noise_pairs(const NrLaunch& A, const float* e
       continue;
     }
     const int q = 2 * t + (g >> 1) + 2 * (g & 1);
+#ifdef IWAE_NR_NOPHILOX   // timing experiment only (wrong results): no Philox draws
+    const float f = 1e-9f * (float)(grow + q);
+    const float4 n = make_float4(f, -f, 0.5f * f, -0.5f * f);
+#else
     const float4 n = philox_normal4(A.seed, base, (unsigned)grow, (unsigned)layer, (unsigned)q);
+#endif
     const auto sx = __builtin_amdgcn_permlane16_swap(__float_as_uint(n.x), __float_as_uint(n.z), false, false);
     const auto sy = __builtin_amdgcn_permlane16_swap(__float_as_uint(n.y), __float_as_uint(n.w), false, false);
     ep[t] = make_float2(__uint_as_float(sx[0]), __uint_as_float(sy[0]));
