@@ -415,13 +415,14 @@ def main():
     # HBM traffic of the same kernel: committed rocprofv3 PMC record (tools/pmc_passes.sh +
     # tools/pmc_to_json.py; FETCH_SIZE x2 per the gfx950 correction, WRITE_SIZE as is)
     traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
+    pmc_name = "r04_pmc_traffic.json"
+    pmc = os.path.join(ROOT, "profiles", pmc_name)
     if os.path.exists(pmc):
         with open(pmc) as f:
             rec = json.load(f).get(dom)          # records keyed by the kernel label used here
         if rec:
             traffic = round(rec["traffic_bytes"] / 1e6, 3)
-            traffic_src = f"profiles/r03_pmc_traffic.json (MB per launch: fetch {rec['fetch_bytes'] / 1e6:.2f} + " \
+            traffic_src = f"profiles/{pmc_name} (MB per launch: fetch {rec['fetch_bytes'] / 1e6:.2f} + " \
                           f"write {rec['write_bytes'] / 1e6:.2f})"
     roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=peak, unit="TFLOP/s",
                     frac=round(achieved / peak, 4), traffic=traffic, traffic_unit="MB/launch",
