@@ -7,7 +7,7 @@
 // kernel's 64 x 64 tiles re-read every 64-column slice of X and dZ per tile
 // (1.6 GB of L2 -> CU traffic per step) and split each loaded element into
 // bf16 hi / lo once per tile that loads it: 6.3 VALU instructions per MFMA,
-// issue-bound (profiles/r04e_*).  Here one 1024-thread workgroup owns up to a
+// issue-bound.  Here one 512-thread workgroup owns up to a
 // 208 x 128 block of W_aug (13 x 8 MFMA tiles: the whole input width of the
 // 200-wide layers) for a chunk of rows, so every element is loaded and split
 // 2.6x less often per MFMA, and the workgroups of one row chunk sit on one XCD

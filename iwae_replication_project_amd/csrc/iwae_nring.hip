@@ -346,10 +346,16 @@ __device__ __forceinline__ nr_f32x4 nr_mma(const __bf16* slot, const NrFrag& IN,
 // train-mode stores: buffer stores through a resource of the tensor, a row
 // past the launch or a column past the width (OOB offset) is dropped
 __device__ __forceinline__ void nr_st4(const float* base, unsigned off, const float (&v)[4]) {
+#ifdef IWAE_NR_NOSTORE    // timing experiment only (wrong results): every store dropped
+  off = kOOB;
+#endif
   const nr_u32x4 u = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
   __builtin_amdgcn_raw_buffer_store_b128(u, buf_rsrc(base), off, 0, 0);
 }
 __device__ __forceinline__ void nr_st2(const float* base, unsigned off, float a, float b) {
+#ifdef IWAE_NR_NOSTORE
+  off = kOOB;
+#endif
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
   const u32x2 u = {__float_as_uint(a), __float_as_uint(b)};
   __builtin_amdgcn_raw_buffer_store_b64(u, buf_rsrc(base), off, 0, 0);
@@ -388,7 +394,11 @@ __device__ __forceinline__ auto nr_dense_tanh(NrCtx& C, const NrStage& S, const 
     for (int i = 0; i < 4; ++i) {
       const int f = 16 * t + 4 * g + i;
       // (train mode: the train engine's tanh, whose outputs the backward's TGRAD reads)
+#ifdef IWAE_NR_TR_FASTTANH   // experiment: the NLL tanh in train mode too
+      float th = real ? nr_tanh(a[i]) : 0.f;
+#else
       float th = real ? (TR ? ftanh(a[i]) : nr_tanh(a[i])) : 0.f;
+#endif
       if (edge) {
         asm volatile("" : "+v"(th));
         v[i] = (real && f < S.N) ? th : (f == S.N ? 1.f : 0.f);
