@@ -62,6 +62,15 @@ constexpr int NR_W = 8;                       // waves, 16 rows each
 #endif
 constexpr int NR_G = IWAE_NR_G;               // units per ring synchronization (1, 2 or 4)
 static_assert(NR_G == 1 || NR_G == 2 || NR_G == 4, "NR_G");
+// the NLL kernel (TR = false) synchronizes once per 4 units: +0.8 % over 2
+// (tools/gpu_nllvar.sh); the train-mode kernels (nring_kernel TR, nre_kernel)
+// keep NR_G, which nre_kernel's phase layout is built on
+#ifndef IWAE_NR_G_NLL
+#define IWAE_NR_G_NLL 4
+#endif
+template <bool TR>
+constexpr int nr_g() { return TR ? NR_G : IWAE_NR_G_NLL; }
+static_assert(nr_g<false>() == 1 || nr_g<false>() == 2 || nr_g<false>() == 4, "NR_G_NLL");
 constexpr int NR_ROWS = 16 * NR_W;            // rows per workgroup
 constexpr int NR_SLOT_BF16 = 8 * 2 * 512;     // one slot: 8 k steps x (hi, lo) x 64 lanes x 8 bf16
 constexpr int NR_PIXLD = 800;                 // floats per image in the pixel cache (>= xdim <= 800)
@@ -242,21 +251,22 @@ template <bool TR>
 __device__ __forceinline__ const __bf16* nr_next(NrCtx& C) {
   // younger than a group's pieces at its wait: the pieces of the two groups
   // requested after it and (TR) the stores of the three groups since
-  constexpr int NV = 2 * (NR_D - 2 * NR_G) + (TR ? 3 * NR_G * NR_SEPI : 0);
+  constexpr int G = nr_g<TR>();
+  constexpr int NV = 2 * (NR_D - 2 * G) + (TR ? 3 * G * NR_SEPI : 0);
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
   NR_TR(C.u, 0)
-  if ((C.u & (NR_G - 1)) == 0) {
-    const int nu = C.u + NR_D - NR_G;            // the first unit to request
+  if ((C.u & (G - 1)) == 0) {
+    const int nu = C.u + NR_D - G;            // the first unit to request
     const unsigned ta = NR_TAB_B + 8u * (unsigned)nu;
     u32x2 e0, e1, e2, e3;
     // younger than this group's pieces: the units of the groups after it
-    if (NR_G == 4)
+    if (G == 4)
       asm volatile("ds_read_b64 %0, %4\n\tds_read_b64 %1, %4 offset:8\n\tds_read_b64 %2, %4 offset:16\n\t"
                    "ds_read_b64 %3, %4 offset:24\n\ts_waitcnt vmcnt(%5)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier"
                    : "=&v"(e0), "=&v"(e1), "=&v"(e2), "=&v"(e3)
                    : "v"(ta), "n"(NV)
                    : "memory");
-    else if (NR_G == 2)
+    else if (G == 2)
       asm volatile("ds_read_b64 %0, %2\n\tds_read_b64 %1, %2 offset:8\n\ts_waitcnt vmcnt(%3)\n\t"
                    "s_waitcnt lgkmcnt(0)\n\ts_barrier"
                    : "=&v"(e0), "=&v"(e1)
@@ -268,9 +278,9 @@ __device__ __forceinline__ const __bf16* nr_next(NrCtx& C) {
                    : "v"(ta), "n"(NV)
                    : "memory");
     nr_issue(C, nu % NR_D, __builtin_amdgcn_readfirstlane(e0[0]), (int)__builtin_amdgcn_readfirstlane(e0[1]));
-    if (NR_G >= 2)
+    if (G >= 2)
       nr_issue(C, (nu + 1) % NR_D, __builtin_amdgcn_readfirstlane(e1[0]), (int)__builtin_amdgcn_readfirstlane(e1[1]));
-    if (NR_G >= 4) {
+    if (G >= 4) {
       nr_issue(C, (nu + 2) % NR_D, __builtin_amdgcn_readfirstlane(e2[0]), (int)__builtin_amdgcn_readfirstlane(e2[1]));
       nr_issue(C, (nu + 3) % NR_D, __builtin_amdgcn_readfirstlane(e3[0]), (int)__builtin_amdgcn_readfirstlane(e3[1]));
     }
@@ -872,12 +882,13 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
   C.u = 0;
   {
     const unsigned* tab = reinterpret_cast<const unsigned*>(nrs) + NR_TAB_B / 4;
+    constexpr int G = nr_g<TR>();
 #pragma unroll
-    for (int i = 0; i < NR_D - NR_G; ++i) {
+    for (int i = 0; i < NR_D - G; ++i) {
       nr_issue(C, i, __builtin_amdgcn_readfirstlane(tab[2 * i]), (int)__builtin_amdgcn_readfirstlane(tab[2 * i + 1]));
-      if (TR && (i % NR_G) == NR_G - 1) {
+      if (TR && (i % G) == G - 1) {
         asm volatile("" ::: "memory");
-        nr_st_pad<NR_G * NR_SEPI>(R);
+        nr_st_pad<G * NR_SEPI>(R);
       }
     }
   }
