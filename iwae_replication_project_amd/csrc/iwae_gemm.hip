@@ -133,7 +133,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
       if (!TA) {
         const int mr = f / (BK / 4), kq = f % (BK / 4);
         const int gk = k0 + 4 * kq;
-        off = (m0 + mr < M && gk < klen) ? (unsigned)(mr * a.lda + gk) * 4u : kOOB;
+        const bool in = m0 + mr < M && gk < klen && (a.a_ones == 0 || kbeg + gk < a.a_ones);
+        off = in ? (unsigned)(mr * a.lda + gk) * 4u : kOOB;
       } else {
         // x3 walks k across lanes (its LDS image is [m][k]: conflict-free 2-byte writes)
         const int kr = X3 ? f % BK : f / (BM / 4), mq = X3 ? f / BK : f % (BM / 4);
@@ -218,7 +219,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
     }
   };
 
-  auto sstore = [&](int buf, int sl) {
+  auto sstore = [&](int buf, int sl, int k0) {      // k0: the slice's k relative to kbeg
     if constexpr (X3) { xstore(buf); return; }
     float* Ab = As + buf * BK * LDSA;
     float* Bb = Bs + buf * BK * LDSB;
@@ -227,10 +228,17 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
       const int f = tid + i * NTH;
       if (!TA) {
         const int mr = f / (BK / 4), kq = f % (BK / 4);
-        Ab[(4 * kq + 0) * LDSA + mr] = ra[sl][i].x;
-        Ab[(4 * kq + 1) * LDSA + mr] = ra[sl][i].y;
-        Ab[(4 * kq + 2) * LDSA + mr] = ra[sl][i].z;
-        Ab[(4 * kq + 3) * LDSA + mr] = ra[sl][i].w;
+        float4 v = ra[sl][i];
+        if (a.a_ones > 0) {
+          const int kg = kbeg + k0 + 4 * kq;
+          if (kg == a.a_ones) v.x = 1.f;            // the quad at a_ones read 0 (out of range)
+          if (a.a_copy && bx == 0 && kg < a.a_ones && kg < kend && m0 + mr < M)
+            *reinterpret_cast<float4*>(a.a_copy + (size_t)(m0 + mr) * a.a_copy_ld + kg) = v;
+        }
+        Ab[(4 * kq + 0) * LDSA + mr] = v.x;
+        Ab[(4 * kq + 1) * LDSA + mr] = v.y;
+        Ab[(4 * kq + 2) * LDSA + mr] = v.z;
+        Ab[(4 * kq + 3) * LDSA + mr] = v.w;
       } else {
         const int kr = f / (BM / 4), mq = f % (BM / 4);
         *reinterpret_cast<float4*>(Ab + kr * LDSA + 4 * mq) = ra[sl][i];
@@ -295,7 +303,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
     for (int d = 0; d + 1 < D; ++d)
       if (d < nk) gload(d * BK, d);
     if (D == 1) gload(0, 0);
-    sstore(0, 0);
+    sstore(0, 0, 0);
   }
   __syncthreads();
   GT(2)
@@ -339,7 +347,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
           }
       }
-      if (t + 1 < nk) sstore(cur ^ 1, 0);
+      if (t + 1 < nk) sstore(cur ^ 1, 0, (t + 1) * BK);
       __syncthreads();
       continue;
     }
@@ -359,7 +367,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& a, const int bx, const
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < nk) sstore(cur ^ 1, (d + 1) % D);
+    if (t + 1 < nk) sstore(cur ^ 1, (d + 1) % D, (t + 1) * BK);
     __syncthreads();
    }
   }

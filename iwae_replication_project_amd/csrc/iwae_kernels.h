@@ -156,6 +156,10 @@ struct GemmArgs {
   int need_bce;               // BERN: write Keras-BCE partials into part2
   int x3;                     // 1: bf16x3 products on v_mfma_f32_32x32x16_bf16 (else exact f32 MFMA)
   const __bf16* Bhi; const __bf16* Blo; int ldbx;   // x3: pre-split B as [n][ldbx] (k contiguous), else null
+  // f32, A not transposed: A is the caller's rows of a_ones floats (lda =
+  // a_ones, a multiple of 4) and column a_ones is a virtual ones column (the
+  // bias row of W_aug); the column-0 workgroups also copy A into a_copy
+  int a_ones; float* a_copy; int a_copy_ld;
 };
 
 // tile: 0 = 64x64 (4 waves), 1 = 128x128 (4 waves, 2x2 MFMA tiles each)

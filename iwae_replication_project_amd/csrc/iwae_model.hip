@@ -218,22 +218,28 @@ struct iwae_handle {
   bool use_graphs = false;
   // a captured train step; its first kernel reads the caller's x directly
   // (x_node: that launch, re-pointed with hipGraphExecKernelNodeSetParams)
+  // the input-layer launch of a captured train step, re-pointed at each call's x
+  struct XLaunch {
+    int kind = 0;                      // 0: smallm_kernel (SmArgs), 1: gemm_kernel (GemmArgs)
+    SmArgs sm{};
+    GemmArgs gm{};
+  };
   struct GraphRec {
     hipGraphExec_t exec = nullptr;
     hipGraph_t graph = nullptr;
     hipGraphNode_t x_node = nullptr;
-    SmArgs x_args{};
+    XLaunch x_args{};
     const float* x_cap = nullptr;
     // multi-step graphs (iwae_train_steps): one input-layer launch per captured step
     std::vector<hipGraphNode_t> xs_node;
-    std::vector<SmArgs> xs_args;
+    std::vector<XLaunch> xs_args;
     std::vector<const float*> xs_cap;
   };
   std::map<std::vector<long long>, GraphRec> graphs;
   const float* x_user = nullptr;       // train step: caller's x read directly by the first kernel
   bool capturing = false;
   hipGraphNode_t cap_x_node = nullptr;
-  SmArgs cap_x_args{};
+  XLaunch cap_x_args{};
   // live kernel timing (HIP events around every launch of one GEMM class)
   float* loss_out = nullptr;           // train-step loss destination (part of the graph key)
   float* loss_slots = nullptr;         // multi-step graphs: step j's loss (kGraphSteps floats)
@@ -1110,7 +1116,8 @@ static int enc0_forward(iwae_handle* h, const Plan& P, bool l1_only = false) {
       size_t nd = 0;
       HIPCHK(hipStreamGetCaptureInfo_v2(h->stream, &cs, &cid, &cg, &deps, &nd));
       h->cap_x_node = nd == 1 ? deps[0] : nullptr;
-      h->cap_x_args = a;
+      h->cap_x_args.kind = 0;
+      h->cap_x_args.sm = a;
     }
     if (l1_only) return IWAE_OK;
     if (ksl > 1) {
@@ -1141,9 +1148,26 @@ static int enc0_forward(iwae_handle* h, const Plan& P, bool l1_only = false) {
     a.kchunk = (int)(cdiv(cdiv(a.K, h->fslab_S), 64) * 64);
     const int S = (int)cdiv(a.K, a.kchunk);
     a.c_split_stride = (long long)P.Bimg * a.ldc;
+    if (h->x_user) {
+      // the caller's x with a virtual ones column; the column-0 workgroups
+      // fill x_in for the later readers (ring forward pixels, weight gradients)
+      a.A = h->x_user; a.lda = h->xdim;
+      a.a_ones = h->xdim; a.a_copy = h->x_in.p; a.a_copy_ld = h->x_in.ld;
+    }
     CHK(prof_begin(h, GEMM_FWD, EPI_STORE, 2.0 * P.Bimg * d.fout * d.fin));
     HIPCHK(launch_gemm(h->stream, GEMM_FWD, EPI_STORE, 0, S, false, a));
     CHK(prof_end(h, GEMM_FWD, EPI_STORE));
+    if (h->capturing && h->x_user) {
+      hipStreamCaptureStatus cs;
+      unsigned long long cid;
+      hipGraph_t cg;
+      const hipGraphNode_t* deps = nullptr;
+      size_t nd = 0;
+      HIPCHK(hipStreamGetCaptureInfo_v2(h->stream, &cs, &cid, &cg, &deps, &nd));
+      h->cap_x_node = nd == 1 ? deps[0] : nullptr;
+      h->cap_x_args.kind = 1;
+      h->cap_x_args.gm = a;
+    }
     if (l1_only) return IWAE_OK;
     // (2) rest of encoder layer 0 on the images: tanh(sum) -> l2 -> head (P0)
     RbFwdLaunch Lf{};
@@ -2376,6 +2400,28 @@ static int train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam)
   return finish_step(h, P, adam);
 }
 
+// The engine step's input Dense as the split-K GEMM (above the few-row
+// launches' 32 images) reads the caller's x itself: a virtual ones column at
+// x_dim (a multiple of 4 floats), and it fills x_in for the later readers.
+static bool gemm_direct(const iwae_handle* h, const Plan& P) {
+  return use_engine(h, P) && !smallm_ok(h, P.Bimg) && h->xdim % 4 == 0;
+}
+
+// re-point a captured input-layer launch at x
+static hipError_t repoint_x(hipGraphExec_t exec, hipGraphNode_t node, const iwae_handle::XLaunch& xa, const float* x) {
+  hipKernelNodeParams kp;
+  hipError_t e = hipGraphKernelNodeGetParams(node, &kp);
+  if (e != hipSuccess) return e;
+  SmArgs sa = xa.sm;
+  GemmArgs ga = xa.gm;
+  sa.A = x;
+  ga.A = x;
+  void* args[] = {xa.kind == 1 ? (void*)&ga : (void*)&sa};
+  kp.kernelParams = args;
+  kp.extra = nullptr;
+  return hipGraphExecKernelNodeSetParams(exec, node, &kp);
+}
+
 static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,
                     const float* const* eps, int n_eps, float* loss_dev, bool adam) {
   if (!x) return fail(h, IWAE_EINVAL, "x is NULL");
@@ -2402,7 +2448,7 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
       (void)nre_plan(h, ne);
     }
   }
-  const bool direct = P.Bimg == P.B && (engine || use_fused(h, P)) && smallm_ok(h, P.Bimg);
+  const bool direct = P.Bimg == P.B && (((engine || use_fused(h, P)) && smallm_ok(h, P.Bimg)) || gemm_direct(h, P));
   if (!direct) CHK(copy_x(h, P, x));
   h->x_user = direct ? x : nullptr;
   const bool philox = (E.a[0] == nullptr);
@@ -2449,14 +2495,7 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
     iwae_handle::GraphRec& g = it->second;
     if (g.x_node && g.x_cap != x) {
       // re-point the input-layer launch at this call's x
-      hipKernelNodeParams kp;
-      HIPCHK(hipGraphKernelNodeGetParams(g.x_node, &kp));
-      SmArgs na = g.x_args;
-      na.A = x;
-      void* args[] = {&na};
-      kp.kernelParams = args;
-      kp.extra = nullptr;
-      HIPCHK(hipGraphExecKernelNodeSetParams(g.exec, g.x_node, &kp));
+      HIPCHK(repoint_x(g.exec, g.x_node, g.x_args, x));
       g.x_cap = x;
     }
     HIPCHK(hipGraphLaunch(g.exec, h->stream));
@@ -2506,7 +2545,7 @@ static int do_train_steps(iwae_handle* h, const iwae_loss_config* lc, const floa
   const bool engine = use_engine(h, P);
   // (the engine step refreshes every copy it reads inside the step; other
   // paths decide their split-copy refreshes on the host at capture time)
-  const bool direct = P.Bimg == P.B && engine && smallm_ok(h, P.Bimg);
+  const bool direct = P.Bimg == P.B && ((engine && smallm_ok(h, P.Bimg)) || gemm_direct(h, P));
   if (!direct) return single();
   {
     CHK(ensure_fx(h));
@@ -2570,14 +2609,7 @@ static int do_train_steps(iwae_handle* h, const iwae_loss_config* lc, const floa
     for (int j = 0; j < S; ++j) {
       const float* xj = xi + j * xstride;
       if (g.xs_cap[j] == xj) continue;
-      hipKernelNodeParams kp;
-      HIPCHK(hipGraphKernelNodeGetParams(g.xs_node[j], &kp));
-      SmArgs na = g.xs_args[j];
-      na.A = xj;
-      void* args[] = {&na};
-      kp.kernelParams = args;
-      kp.extra = nullptr;
-      HIPCHK(hipGraphExecKernelNodeSetParams(g.exec, g.xs_node[j], &kp));
+      HIPCHK(repoint_x(g.exec, g.xs_node[j], g.xs_args[j], xj));
       g.xs_cap[j] = xj;
     }
     HIPCHK(hipGraphLaunch(g.exec, h->stream));
