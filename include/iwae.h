@@ -148,7 +148,8 @@ enum iwae_knob {
   IWAE_KNOB_DW_ALPHA = 30,         /* DW_WIDE pass cost model: a k step's fixed cost in MFMA tiles (150) */
   IWAE_KNOB_IMG_ROWS_FWD = 31,     /* image-row job I (first encoder layer's l2 / head): images per workgroup,
                                       <= 16 (0: auto, ceil(B / 256)) */
-  IWAE_KNOB_IMG_ROWS_BWD = 32      /* image-row job I' (its backward): images per workgroup (0: auto) */
+  IWAE_KNOB_IMG_ROWS_BWD = 32,     /* image-row job I' (its backward): images per workgroup (0: auto) */
+  IWAE_KNOB_X_DIRECT = 33          /* 1: a large-batch engine step's input GEMM reads the caller's x (default); 0: staged copy */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --

@@ -209,6 +209,7 @@ struct iwae_handle {
   int dw_alpha = 150;                // ... its cost model: a k step's fixed cost in MFMA tiles (measured: a
                                      // k step costs ~2 us whatever its tiles; alpha 0 / 45 / 90 / 200: 174 / 127 / 108 / 106 us)
   int img_rows_fwd = 0, img_rows_bwd = 0;   // image-row jobs I / I': rows per workgroup (0: auto)
+  int x_direct = 1;                  // large-batch engine step: the input GEMM reads the caller's x (gemm_direct)
   int piwae_one = 1;                 // PIWAE: one unit-weight backward chain serves both weightings (knob)
   bool piwae_ks = false;             // (during a step) the weight gradients apply the per-layer PIWAE weighting
   int tc_rt = 1;                     // row tiles of 16 per engine workgroup below wide_rows
@@ -2404,7 +2405,7 @@ static int train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam)
 // launches' 32 images) reads the caller's x itself: a virtual ones column at
 // x_dim (a multiple of 4 floats), and it fills x_in for the later readers.
 static bool gemm_direct(const iwae_handle* h, const Plan& P) {
-  return use_engine(h, P) && !smallm_ok(h, P.Bimg) && h->xdim % 4 == 0;
+  return h->x_direct && use_engine(h, P) && !smallm_ok(h, P.Bimg) && h->xdim % 4 == 0;
 }
 
 // re-point a captured input-layer launch at x
@@ -2889,6 +2890,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_DW_ALPHA: h->dw_alpha = (int)std::max(0LL, std::min(value, 1000LL)); break;
     case IWAE_KNOB_IMG_ROWS_FWD: h->img_rows_fwd = (int)std::max(0LL, std::min(value, 16LL)); break;
     case IWAE_KNOB_IMG_ROWS_BWD: h->img_rows_bwd = (int)std::max(0LL, std::min(value, 16LL)); break;
+    case IWAE_KNOB_X_DIRECT: h->x_direct = on; break;
     case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;

@@ -229,14 +229,15 @@ def test_alternating_split_and_single_split_output_jobs_leave_no_stale_rows(big)
     assert np.array_equal(ga, gb)
 
 
-@pytest.mark.parametrize("B,n", [(20, 11), (20, 40), (7, 3), (64, 9)])
+@pytest.mark.parametrize("B,n", [(20, 11), (20, 40), (7, 3), (64, 9), (512, 3)])
 def test_train_steps_equal_single_step_calls(B, n):
-    """fit's batch loop as one call (iwae_train_steps: graphs of up to 8
+    """fit's batch loop as one call (iwae_train_steps: graphs of up to 32
     captured steps, each re-pointed at its own batch) equals n train_step
     calls -- captured one step per graph, and eager -- bit for bit: per-step
     losses, the final weights and Adam state (same seed, same Philox stream).
     Shapes: the bench's B=20 (11 steps: one graph; 40 = 32 + 8: two graphs of
-    different length), a ragged 7, and 64 images (image-row jobs, single steps)."""
+    different length), a ragged 7, 64 images (image-row jobs; the input GEMM
+    reads the caller's x) and the large-batch leg's 512 (ring kernels)."""
     import torch
     rng = np.random.default_rng(11 + B + n)
     xs = (rng.random((n * B + 5, 784)) < 0.25).astype(np.float32)
@@ -259,3 +260,28 @@ def test_train_steps_equal_single_step_calls(B, n):
         np.testing.assert_array_equal(runs[0][1], r[1])
         np.testing.assert_array_equal(runs[0][2], r[2])
         assert runs[0][3] == r[3] == 2 * n
+
+
+@pytest.mark.parametrize("B", [64, 512])
+def test_input_gemm_on_the_callers_x_equals_the_staged_copy(B):
+    """Above the few-row launches' 32 images the engine step's input Dense is
+    a split-K GEMM.  It reads the caller's x with a virtual ones column at
+    x_dim (the bias row of W_aug), and its column-0 workgroups fill the padded
+    x_in that the later launches read (ring-forward pixels, the input layer's
+    weight gradient).  Knob x_direct 0 stages x into x_in with a copy first:
+    both give the same losses, weights and Adam state bit for bit, over graph
+    replays with a moving batch and eagerly."""
+    import torch
+    rng = np.random.default_rng(5 + B)
+    xs = (rng.random((3 * B + 3, 784)) < 0.3).astype(np.float32)
+    runs = []
+    for direct in (1, 0):
+        for graphs in (True, False):
+            m = _model(ARCH2, "IWAE", 50, use_graphs=graphs, tuning={"x_direct": direct})
+            X = torch.from_numpy(xs).to(m.device)
+            losses = [m.train_step(X[i * B + i:(i + 1) * B + i])["IWAE"] for i in range(3)]
+            mm, vv, st = m.get_optimizer_state()
+            runs.append((np.asarray(losses, np.float32), _flat(m.get_weights()), mm, vv))
+    for r in runs[1:]:
+        for u, v in zip(runs[0], r):
+            np.testing.assert_array_equal(u, v)
