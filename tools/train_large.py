@@ -19,12 +19,19 @@ m = Flexible_Model(bench.HE, bench.HD, bench.LE, bench.LD, dataset_bias=pi, loss
                    kernel_path=path, tuning=tuning)
 m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
 xd = m._x(x)
-for i in range(3):
-    m.train_step(xd[(i % 4) * B:(i % 4 + 1) * B], sync=False)
-torch.cuda.synchronize()
-t = time.perf_counter()
-for i in range(steps):
-    m.train_step(xd[(i % 4) * B:(i % 4 + 1) * B], sync=False)
+if os.environ.get("LOOP", "steps") == "calls":      # one train_step call (graph launch) per step
+    for i in range(3):
+        m.train_step(xd[(i % 4) * B:(i % 4 + 1) * B], sync=False)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for i in range(steps):
+        m.train_step(xd[(i % 4) * B:(i % 4 + 1) * B], sync=False)
+else:                                               # fit's loop: train_steps over the steps' batches
+    xs = xd.repeat((steps + 3) // 4, 1)[:steps * B].contiguous()
+    m.train_steps(xs, B, sync=False)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    m.train_steps(xs, B, sync=False)
 torch.cuda.synchronize()
 el = (time.perf_counter() - t) / steps
 rows = B * 50
