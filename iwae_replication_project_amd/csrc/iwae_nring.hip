@@ -62,14 +62,18 @@ constexpr int NR_W = 8;                       // waves, 16 rows each
 #endif
 constexpr int NR_G = IWAE_NR_G;               // units per ring synchronization (1, 2 or 4)
 static_assert(NR_G == 1 || NR_G == 2 || NR_G == 4, "NR_G");
-// the NLL kernel (TR = false) synchronizes once per 4 units: +0.8 % over 2
-// (tools/gpu_nllvar.sh); the train-mode kernels (nring_kernel TR, nre_kernel)
-// keep NR_G, which nre_kernel's phase layout is built on
+// nring_kernel synchronizes once per 4 units: NLL +0.8 % over 2
+// (tools/gpu_nllvar.sh), the B = 512 step 0.427-0.429 vs 0.430 ms
+// (tools/gpu_lbvar.sh); nre_kernel keeps NR_G, which its phase layout is built on
 #ifndef IWAE_NR_G_NLL
 #define IWAE_NR_G_NLL 4
 #endif
+// (nring_kernel in train mode: IWAE_NR_G_TR; nre_kernel passes NR_G itself)
+#ifndef IWAE_NR_G_TR
+#define IWAE_NR_G_TR 4
+#endif
 template <bool TR>
-constexpr int nr_g() { return TR ? NR_G : IWAE_NR_G_NLL; }
+constexpr int nr_g() { return TR ? IWAE_NR_G_TR : IWAE_NR_G_NLL; }
 static_assert(nr_g<false>() == 1 || nr_g<false>() == 2 || nr_g<false>() == 4, "NR_G_NLL");
 constexpr int NR_ROWS = 16 * NR_W;            // rows per workgroup
 constexpr int NR_SLOT_BF16 = 8 * 2 * 512;     // one slot: 8 k steps x (hi, lo) x 64 lanes x 8 bf16
@@ -247,11 +251,10 @@ __device__ __forceinline__ void nr_issue(const NrCtx& C, int slot, unsigned off,
 // one lets the compiler copy the register before the data has arrived.  (The
 // table and the pixel cache are read in asm, or plain with hipcc's own
 // vmcnt(0), because hipcc cannot tell them apart from the DMA-written slots.)
-template <bool TR>
+template <bool TR, int G = nr_g<TR>()>
 __device__ __forceinline__ const __bf16* nr_next(NrCtx& C) {
   // younger than a group's pieces at its wait: the pieces of the two groups
   // requested after it and (TR) the stores of the three groups since
-  constexpr int G = nr_g<TR>();
   constexpr int NV = 2 * (NR_D - 2 * G) + (TR ? 3 * G * NR_SEPI : 0);
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
   NR_TR(C.u, 0)
@@ -1420,7 +1423,7 @@ __device__ __forceinline__ auto nre_dense(NrCtx& C, const NrFrag& IN, NrFrag& OU
   nr_f32x4 prev = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const __bf16* slot = nr_next<true>(C);
+    const __bf16* slot = nr_next<true, NR_G>(C);
     if (t == 0) pend();
     const nr_f32x4 acc = nr_mma<NSI>(slot, IN, C.u - 1);
     if (t > 0) epi(t - 1, prev, va, true);
