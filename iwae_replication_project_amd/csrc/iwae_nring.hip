@@ -240,11 +240,12 @@ __device__ __forceinline__ void nr_issue(const NrCtx& C, int slot, unsigned off,
 }
 
 // Advance the ring to unit C.u; returns its slot.  The ring is synchronized
-// once per NR_G units (a group): at a group's first unit every wave waits for
-// its own pieces of the group's units (counted vmcnt), then lgkmcnt(0) (its
+// once per G units (a group: nr_g<TR>() in nring_kernel, NR_G in nre_kernel):
+// at a group's first unit every wave waits for its own pieces of the group's
+// units (counted vmcnt), then lgkmcnt(0) (its
 // reads of the previous group's slots are done), then the barrier; after it
 // the group's slots are complete and the previous group's slots are free, and
-// each wave requests the NR_G units NR_D - NR_G ahead into them.
+// each wave requests the G units NR_D - G ahead into them.
 // The table entries of those units are read by ds_read_b64 in the SAME asm
 // statement as the waits: hipcc takes an asm output as ready when the
 // statement ends, so an LDS read in one statement and its wait in a later
@@ -876,7 +877,7 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
   nr_keep(R.q);
   nr_keep(R.p);
   NR_TR(kNrMaxUnits - 1, 1)
-  // ---- the ring: the first NR_D - NR_G units (whole groups).  TR: each group
+  // ---- the ring: the first NR_D - G units (whole groups).  TR: each group
   // followed by the stores its phases would have issued (out of range), so
   // the first waits count like every later one
   NrCtx C;
