@@ -830,6 +830,8 @@ hipError_t smallm_setup_attributes() {
 hipError_t launch_gemm(hipStream_t st, GemmKind kind, GemmEpi epi, int tile, int splits, bool ks,
                        const GemmArgs& a) {
   if (a.M <= 0 || a.N <= 0) return hipSuccess;
+  // the virtual ones column is staged by the f32, non-transposed-A path only
+  if (a.a_ones > 0 && (a.x3 || kind != GEMM_FWD || a.a_ones % 4 != 0 || a.lda != a.a_ones)) return hipErrorInvalidValue;
   if (tile == 1) return dispatch_tile<2, 2, 2, 2>(st, kind, epi, splits, ks, a);
   return dispatch_tile<2, 2, 1, 1>(st, kind, epi, splits, ks, a);
 }
