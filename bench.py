@@ -311,6 +311,10 @@ def main():
     rccl_world = dict(torch_world=dist.get_world_size() if world > 1 else 1, backend=backend if world > 1 else None,
                       library_dp_world=dpw.value, library_rccl_comm_ranks=dpc.value,
                       train_reduce=(model._dp.comm if model._dp is not None else None))
+    if world > 1 and backend == "nccl" and (dpc.value != world or dpw.value != world):
+        # the N > 1 headline must run the library's in-graph RCCL all-reduce over every rank
+        raise SystemExit(f"[bench] rank {rank}: library RCCL communicator has {dpc.value} ranks, data-parallel "
+                         f"world {dpw.value}; expected {world}")
     xd = model._x(x_all)
     nb = xd.shape[0] // B_PER_GPU
     batches = [xd[i * B_PER_GPU:(i + 1) * B_PER_GPU] for i in range(nb)]
@@ -334,10 +338,22 @@ def main():
         for i in range(n):
             model.train_step(batches[(off + i) % nb], sync=False)
 
-    # ---- warmup
+    def prepare(n, off=0):
+        # capture (without running) every graph run(n, off) replays: the timed
+        # region then measures fit's steady-state loop, not graph capture
+        while n > 0:
+            o = off % nb
+            m = min(n, nb - o)
+            model.prepare_train_steps(xd[o * B_PER_GPU:(o + m) * B_PER_GPU], B_PER_GPU)
+            n -= m
+            off += m
+
+    # ---- warmup: W steps, then the timed call's graphs captured (no step runs)
     run(args.warmup)
+    prepare(args.steps, args.warmup)
     model._stream.synchronize()
     torch.cuda.synchronize()
+    cap0 = model.graph_captures()
     # ---- timed region: K train steps
     barrier()
     torch.cuda.synchronize()
@@ -347,6 +363,9 @@ def main():
     torch.cuda.synchronize()
     barrier()
     el = time.perf_counter() - t0
+    captures_timed = model.graph_captures() - cap0
+    if captures_timed:
+        raise SystemExit(f"[bench] {captures_timed} graph capture(s) inside the timed region")
     if world > 1:
         t = torch.tensor([el], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -458,6 +477,7 @@ def main():
         xls = xl.repeat((nls + 3) // 4, 1)[:nls * bl].contiguous()
         model.train_steps(xls, bl, sync=False)           # warm-up: captures the multi-step graph
         model._stream.synchronize()
+        cap1 = model.graph_captures()
         barrier()
         torch.cuda.synchronize()
         t2 = time.perf_counter()
@@ -466,6 +486,8 @@ def main():
         torch.cuda.synchronize()
         barrier()
         el3 = time.perf_counter() - t2
+        if model.graph_captures() != cap1:
+            raise SystemExit("[bench] graph capture inside the large-batch timed region")
         if world > 1:
             t = torch.tensor([el3], device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -623,7 +645,9 @@ def main():
                        "global_batch": B_PER_GPU * world, "k": K, "parallelism": f"dp{world}",
                        "noise": "device Philox", "graphs": not args.no_graphs,
                        "loop": "fit's batch loop (E:82): consecutive batches through Flexible_Model.train_steps "
-                               "(iwae_train_steps, up to 32 captured steps per graph launch)"},
+                               "(iwae_train_steps, up to 32 captured steps per graph launch); the timed call's "
+                               "graphs are captured before the clock starts (iwae_train_steps_prepare)",
+                       "graph_captures_in_timed_region": captures_timed},
             "loss": round(loss, 4),
             "train_step_calls": per_call,
             "rccl_world": rccl_world,

@@ -154,8 +154,11 @@ enum iwae_knob {
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --
  * a.b = a_hi b_hi + a_hi b_lo + a_lo b_hi with hi = bf16(x), lo = bf16(x - hi),
- * f32 accumulate on v_mfma_f32_32x32x16_bf16 (~2^-16 relative per product,
- * 5.3x the f32-MFMA rate); 0 exact f32 on v_mfma_f32_32x32x2_f32. */
+ * f32 accumulate on v_mfma_f32_16x16x32_bf16 (the engine, ring, update and
+ * weight-gradient kernels; the tiled GEMMs also 32x32x16_bf16), ~2^-16
+ * relative per product, 5.3x the f32-MFMA rate; 0 exact f32 on
+ * v_mfma_f32_16x16x4_f32 (the tiled GEMMs, row-block and few-row kernels; the
+ * tiled GEMMs' largest tile also 32x32x2_f32). */
 int iwae_set_precision(iwae_handle* h, int mode);
 /* Kernel path: 0 auto (train step on the bf16x3 row-chain engine where it
  * applies -- every loss but L_alpha / VAE_V1 / PIWAE, up to 3 stochastic
@@ -195,6 +198,12 @@ int iwae_train_step(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
  * launch gap between them). */
 int iwae_train_steps(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B, int nsteps,
                      float* loss_dev);
+/* Capture, without launching anything, every graph an iwae_train_steps call
+ * with these arguments would capture (the step counts min(32, nsteps) and
+ * nsteps % 32), so that the call itself only replays; the parameters, Adam
+ * state and noise position are untouched.  Data parallelism with the library
+ * communicator included (each captured step carries its all-reduces). */
+int iwae_train_steps_prepare(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B, int nsteps);
 /* The same without the Adam update (gradient kept on device).  For data
  * parallelism: forward_backward -> all-reduce(grad buffer) -> apply_adam. */
 int iwae_forward_backward(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,
@@ -301,7 +310,9 @@ double iwae_workspace_bytes(const iwae_handle* h);
  * by the weight-ring kernel (nring_kernel, a subset of 0), 4 train-step
  * forwards run by it in train mode, 5 train-step output-MLP backwards run by
  * the weight-ring backward kernel (nrb_kernel), 6 encoder / prior backwards
- * run by nre_kernel; -1 for an unknown id. */
+ * run by nre_kernel, 7 train-step graphs captured (iwae_train_step,
+ * iwae_train_steps, iwae_train_steps_prepare; bench.py asserts it stays flat
+ * across its timed region); -1 for an unknown id. */
 long long iwae_debug_count(const iwae_handle* h, int what);
 /* Live kernel timing: bracket every launch of one kernel class with HIP events
  * on the handle's stream -- a GEMM class (kind: 0 forward, 1 backward-data,

@@ -74,6 +74,7 @@ SIGNATURES = {
     "iwae_set_adam_state": (c_int, [H, FP, FP, c_longlong, c_longlong]),
     "iwae_train_step": (c_int, [H, POINTER(IwaeLossConfig), FP, c_int, FPP, c_int, FP]),
     "iwae_train_steps": (c_int, [H, POINTER(IwaeLossConfig), FP, c_int, c_int, FP]),
+    "iwae_train_steps_prepare": (c_int, [H, POINTER(IwaeLossConfig), FP, c_int, c_int]),
     "iwae_forward_backward": (c_int, [H, POINTER(IwaeLossConfig), FP, c_int, FPP, c_int, FP]),
     "iwae_grad_buffer": (c_int, [H, POINTER(FP), POINTER(c_longlong)]),
     "iwae_bind_grad_buffer": (c_int, [H, FP, c_longlong]),

@@ -176,6 +176,7 @@ struct iwae_handle {
   bool masked = false;               // active-unit masks in force (iwae_nll_masked only)
   long long n_mega = 0, n_mega_eps = 0;  // mega_fwd_kernel launches (all / injected noise), iwae_debug_count
   long long n_tc = 0;                    // train-engine launches (tc_kernel), iwae_debug_count(h, 2)
+  long long n_captures = 0;              // train-step graphs captured (single and multi-step), iwae_debug_count(h, 7)
   const float* mask[IWAE_MAX_LAYERS] = {};
   // row-chain train engine plans (device resident, per shape; iwae_train.hip)
   struct TcRec {
@@ -1406,6 +1407,18 @@ static int fused_encoder_bwd(iwae_handle* h, const Plan& P, const float* dlw, in
   return IWAE_OK;
 }
 
+// the row scale of layer di's dZ in the weight gradients: ks as given, or under
+// piwae_unit the layer's weighting
+static const float* dz_scale(const iwae_handle* h, int di, const float* ks) {
+  if (!h->piwae_ks) return ks;
+  if (di == h->o1 || di == h->o2 || di == h->o3) return h->dpx;
+  for (int i = 0; i < h->L - 1; ++i)
+    if (di == h->dec[i].l1 || di == h->dec[i].l2 || di == h->dec[i].head) return h->dlw;
+  for (int i = 1; i < h->L; ++i)
+    if (di == h->enc[i].l1 || di == h->enc[i].l2 || di == h->enc[i].head) return h->dlw2;
+  return ks;                          // the first encoder layer: its image-row dZ are weighted already
+}
+
 // all weight gradients (X_aug^T dZ, split over rows) in grouped launches
 static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const float* dpx) {
   const int L = h->L, M = P.Bimg * P.kS;
@@ -1448,7 +1461,7 @@ static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const
       d.splits = (int)S;
       a.kchunk = kchunk;
       a.c_split_stride = d.size();
-      a.kscale = w.ks;
+      a.kscale = dz_scale(h, w.di, w.ks);      // PIWAE's unit chain: the layer's own weighting
       gg.splits[gg.n] = (int)S;
       gg.n++;
     }
@@ -1463,18 +1476,6 @@ static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const
 // bf16x3 products, and up to upd_rows sample rows (one workgroup reduces a
 // tile over all rows: beyond that the split-K GEMM + Adam launches parallelise
 // better).
-// the row scale of layer di's dZ in the weight gradients: ks as given, or under
-// piwae_unit the layer's weighting
-static const float* dz_scale(const iwae_handle* h, int di, const float* ks) {
-  if (!h->piwae_ks) return ks;
-  if (di == h->o1 || di == h->o2 || di == h->o3) return h->dpx;
-  for (int i = 0; i < h->L - 1; ++i)
-    if (di == h->dec[i].l1 || di == h->dec[i].l2 || di == h->dec[i].head) return h->dlw;
-  for (int i = 1; i < h->L; ++i)
-    if (di == h->enc[i].l1 || di == h->enc[i].l2 || di == h->enc[i].head) return h->dlw2;
-  return ks;                          // the first encoder layer: its image-row dZ are weighted already
-}
-
 static bool upd_tiles_ok(const iwae_handle* h) {
   long long tiles = 0;
   for (const DenseL& d : h->dense) tiles += cdiv(d.fin + 1, 64) * cdiv(d.fout, h->upd_tn32 ? 32 : 64);
@@ -2477,11 +2478,20 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
       int rc = train_body(h, P, E, adam);
       hipError_t ec = hipStreamEndCapture(h->stream, &graph);
       h->capturing = false;
-      if (rc != IWAE_OK) return rc;
-      HIPCHK(ec);
+      if (rc != IWAE_OK || ec != hipSuccess) {
+        if (ec == hipSuccess && graph) (void)hipGraphDestroy(graph);
+        if (rc != IWAE_OK) return rc;
+        HIPCHK(ec);
+      }
       iwae_handle::GraphRec g;
       g.graph = graph;
-      HIPCHK(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
+      const hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+      if (ei != hipSuccess) {
+        g.exec = nullptr;
+        destroy_graph(g);
+        HIPCHK(ei);
+      }
+      h->n_captures++;
       if (direct) {
         if (!h->cap_x_node) {
           destroy_graph(g);
@@ -2521,15 +2531,82 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
 // profiling) runs as nsteps single steps.
 static constexpr int kGraphSteps = 32;
 
+// The graph of S consecutive steps from batch xi (captured on first use; a
+// capture is counted in n_captures, iwae_debug_count id 7).
+static int steps_graph(iwae_handle* h, const iwae_loss_config* lc, const Plan& P, const EpsSet& E, int B, int S,
+                       const float* xi, iwae_handle::GraphRec** out) {
+  const long long xstride = (long long)B * h->xdim;
+  std::vector<long long> key = {2, lc->loss, B, lc->k, lc->k1, lc->k2, S, 1};
+  float fk[3] = {lc->p, lc->alpha, lc->beta};
+  for (float f : fk) {
+    int bits;
+    std::memcpy(&bits, &f, 4);
+    key.push_back(bits);
+  }
+  auto it = h->graphs.find(key);
+  if (it == h->graphs.end()) {
+    iwae_handle::GraphRec g;
+    hipGraph_t graph = nullptr;
+    h->capturing = true;
+    HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
+    int rc = IWAE_OK;
+    for (int j = 0; j < S && rc == IWAE_OK; ++j) {
+      h->x_user = xi + j * xstride;
+      h->loss_out = h->loss_slots + j;
+      h->cap_x_node = nullptr;
+      rc = train_body(h, P, E, true);
+      g.xs_node.push_back(h->cap_x_node);
+      g.xs_args.push_back(h->cap_x_args);
+      g.xs_cap.push_back(h->x_user);
+    }
+    const hipError_t ec = hipStreamEndCapture(h->stream, &graph);
+    h->capturing = false;
+    if (rc != IWAE_OK || ec != hipSuccess) {
+      if (ec == hipSuccess && graph) (void)hipGraphDestroy(graph);
+      if (rc != IWAE_OK) return rc;
+      HIPCHK(ec);
+    }
+    g.graph = graph;
+    const hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+      g.exec = nullptr;
+      destroy_graph(g);
+      HIPCHK(ei);
+    }
+    for (hipGraphNode_t n : g.xs_node)
+      if (!n) {
+        destroy_graph(g);
+        return fail(h, IWAE_EHIP, "multi-step capture: input-layer launch not found");
+      }
+    h->n_captures++;
+    it = h->graphs.emplace(key, g).first;
+  }
+  *out = &it->second;
+  return IWAE_OK;
+}
+
+// consecutive Philox train steps on the batches x + i * B * x_dim (fit's loop,
+// E:82): graphs of up to kGraphSteps captured steps, so consecutive steps run
+// without the per-graph launch gap; step j of a graph reads its own batch (its
+// input-layer launch re-pointed when the batch moves) and writes its loss to
+// loss_slots[j], copied to loss_dev + i after the graph.  Data parallel with
+// the library communicator: each captured step carries its all-reduces.
+// Anything the multi-step graph does not cover (no graphs, staged x, data
+// parallel without the library communicator, live profiling) runs as nsteps
+// single steps.  prepare_only: capture every graph such a call uses (the
+// lengths min(32, n) and n % 32) without launching anything, and leave the
+// host's view of the parameters (versions) as it was.
 static int do_train_steps(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B, int nsteps,
-                          float* loss_dev) {
+                          float* loss_dev, bool prepare_only = false) {
   if (!x) return fail(h, IWAE_EINVAL, "x is NULL");
   if (nsteps < 0) return fail(h, IWAE_EINVAL, "nsteps must be >= 0");
   if (nsteps == 0) return IWAE_OK;
   const long long xstride = (long long)B * h->xdim;
+  const bool multi = nsteps > 1 && h->use_graphs && h->prof_kind < 0 && (!h->dp_weighted || h->comm);
   // (single steps write the loss to the handle's scalar, then copy it: one
   // captured graph per shape, not one per loss address)
   auto single = [&]() -> int {
+    if (prepare_only) return IWAE_OK;      // single steps capture on their first call
     for (int i = 0; i < nsteps; ++i) {
       CHK(do_train(h, lc, x + i * xstride, B, nullptr, 0, nullptr, true));
       if (loss_dev)
@@ -2537,7 +2614,7 @@ static int do_train_steps(iwae_handle* h, const iwae_loss_config* lc, const floa
     }
     return IWAE_OK;
   };
-  if (nsteps == 1 || !h->use_graphs || h->prof_kind >= 0 || h->dp_weighted) return single();
+  if (!multi) return single();
   Plan P;
   CHK(make_plan(h, lc, B, P));
   EpsSet E;
@@ -2561,6 +2638,7 @@ static int do_train_steps(iwae_handle* h, const iwae_loss_config* lc, const floa
   }
   if (!h->loss_slots) HIPCHK(hipMalloc(&h->loss_slots, kGraphSteps * sizeof(float)));
   h->in_train_step = true;
+  const long long pv = h->params_version, wv = h->wsplit_version, fv = h->fx_version;
   struct Reset {
     iwae_handle* h;
     ~Reset() {
@@ -2570,43 +2648,16 @@ static int do_train_steps(iwae_handle* h, const iwae_loss_config* lc, const floa
   for (int i0 = 0; i0 < nsteps; i0 += kGraphSteps) {
     const int S = std::min(kGraphSteps, nsteps - i0);
     const float* xi = x + i0 * xstride;
-    std::vector<long long> key = {2, lc->loss, B, lc->k, lc->k1, lc->k2, S, 1};
-    float fk[3] = {lc->p, lc->alpha, lc->beta};
-    for (float f : fk) {
-      int bits;
-      std::memcpy(&bits, &f, 4);
-      key.push_back(bits);
+    iwae_handle::GraphRec* gp = nullptr;
+    CHK(steps_graph(h, lc, P, E, B, S, xi, &gp));
+    if (prepare_only) {
+      // a capture bumps the host's parameter versions as if it had run: undo
+      h->params_version = pv;
+      h->wsplit_version = wv;
+      h->fx_version = fv;
+      continue;
     }
-    auto it = h->graphs.find(key);
-    if (it == h->graphs.end()) {
-      iwae_handle::GraphRec g;
-      hipGraph_t graph;
-      h->capturing = true;
-      HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
-      int rc = IWAE_OK;
-      for (int j = 0; j < S && rc == IWAE_OK; ++j) {
-        h->x_user = xi + j * xstride;
-        h->loss_out = h->loss_slots + j;
-        h->cap_x_node = nullptr;
-        rc = train_body(h, P, E, true);
-        g.xs_node.push_back(h->cap_x_node);
-        g.xs_args.push_back(h->cap_x_args);
-        g.xs_cap.push_back(h->x_user);
-      }
-      hipError_t ec = hipStreamEndCapture(h->stream, &graph);
-      h->capturing = false;
-      if (rc != IWAE_OK) return rc;
-      HIPCHK(ec);
-      g.graph = graph;
-      HIPCHK(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
-      for (hipGraphNode_t n : g.xs_node)
-        if (!n) {
-          destroy_graph(g);
-          return fail(h, IWAE_EHIP, "multi-step capture: input-layer launch not found");
-        }
-      it = h->graphs.emplace(key, g).first;
-    }
-    iwae_handle::GraphRec& g = it->second;
+    iwae_handle::GraphRec& g = *gp;
     for (int j = 0; j < S; ++j) {
       const float* xj = xi + j * xstride;
       if (g.xs_cap[j] == xj) continue;
@@ -3022,6 +3073,12 @@ int iwae_train_steps(iwae_handle* h, const iwae_loss_config* lc, const float* x,
   if (!h) return IWAE_EINVAL;
   if (!lc) return fail(h, IWAE_EINVAL, "loss config is NULL");
   return do_train_steps(h, lc, x, B, nsteps, loss_dev);
+}
+
+int iwae_train_steps_prepare(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B, int nsteps) {
+  if (!h) return IWAE_EINVAL;
+  if (!lc) return fail(h, IWAE_EINVAL, "loss config is NULL");
+  return do_train_steps(h, lc, x, B, nsteps, nullptr, true);
 }
 
 int iwae_forward_backward(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,
@@ -3751,6 +3808,7 @@ long long iwae_debug_count(const iwae_handle* h, int what) {
     case 4: return h->n_nring_train;
     case 5: return h->n_nrb;
     case 6: return h->n_nre;
+    case 7: return h->n_captures;
     default: return -1;
   }
 }

@@ -400,6 +400,24 @@ class Flexible_Model:
         self._stream.synchronize()
         return losses.cpu().numpy()
 
+    def prepare_train_steps(self, x, batch_size):
+        """Capture every graph train_steps(x, batch_size) will replay, without
+        running a step (iwae_train_steps_prepare): a timed loop then measures
+        replays only.  Parameters, Adam state and noise are untouched."""
+        if self.optimizer is None:
+            self.compile()
+        xd = self._x(x)
+        B = int(batch_size)
+        if B <= 0:
+            raise ValueError("batch_size must be positive")
+        n = xd.shape[0] // B
+        if n and not (self._dp is not None and self._dp.comm != "library"):
+            self._call(self._lib.iwae_train_steps_prepare(self._h, self._lc(), _lib.fptr(xd), B, n))
+
+    def graph_captures(self):
+        """Train-step graphs captured so far (iwae_debug_count id 7)."""
+        return int(self._lib.iwae_debug_count(self._h, 7))
+
     def fit(self, x, epochs=1, batch_size=100, shuffle=True, verbose=0, seed=None):
         """Keras-style loop (E:82): per epoch shuffle, batches of batch_size
         (last partial batch included), one train step each (the whole batches

@@ -191,6 +191,73 @@ def test_library_rccl_communicator_single_rank_step():
     assert np.linalg.norm(gb - ga) <= 1e-4 * np.linalg.norm(ga), np.linalg.norm(gb - ga)
 
 
+def test_library_rccl_train_steps_equal_single_step_calls():
+    """With the library communicator, train_steps captures the data-parallel
+    step (gradient pass, in-graph ncclAllReduce buckets, Adam) as multi-step
+    graphs (45 steps: graphs of 32 and 13); losses, weights and Adam state equal
+    45 train_step calls (one graph each) bit for bit, and the prepared call
+    captures nothing.  World size 1: this pool's boxes have one GPU."""
+    import torch
+    from iwae_replication_project_amd import distributed as D
+    mean, _, _ = _data()
+    rng = np.random.default_rng(77)
+    n = 45
+    xs = (rng.random((n * B, 784)) < mean).astype(np.float32)
+    runs = []
+    for mode in ("steps", "calls"):
+        m = _model(mean, seed=5)
+        D.enable_data_parallel(m, comm="library")
+        X = torch.from_numpy(xs).to(m.device)
+        if mode == "steps":
+            m.prepare_train_steps(X, B)
+            c0 = m.graph_captures()
+            losses = list(m.train_steps(X, B))
+            assert m.graph_captures() == c0
+        else:
+            losses = [m.train_step(X[i * B:(i + 1) * B])["IWAE"] for i in range(n)]
+        mm, vv, st = m.get_optimizer_state()
+        runs.append((np.asarray(losses, np.float32), _flat(m.get_weights()), mm, vv, st))
+    for a, b in zip(runs[0], runs[1]):
+        np.testing.assert_array_equal(a, b)
+    assert runs[0][4] == n
+
+
+def _dp_train_steps(rank, world):
+    import torch
+    from iwae_replication_project_amd import distributed as D
+    mean, _, _ = _data()
+    rng = np.random.default_rng(78)
+    n = 6
+    xs = (rng.random((n * 2 * B, 784)) < mean).astype(np.float32)
+    out = []
+    for mode in ("steps", "calls"):
+        m = _model(mean, seed=300 + rank)
+        D.enable_data_parallel(m)
+        # this rank's half of every global batch of 2B images
+        xl = np.concatenate([xs[(2 * i + rank) * B:(2 * i + rank + 1) * B] for i in range(n)])
+        X = torch.from_numpy(xl).to(m.device)
+        if mode == "steps":
+            losses = list(m.train_steps(X, B))
+        else:
+            losses = [m.train_step(X[i * B:(i + 1) * B])["IWAE"] for i in range(n)]
+        mm, vv, st = m.get_optimizer_state()
+        out.append((np.asarray(losses, np.float32), _flat(m.get_weights()), mm, vv, st))
+    return out
+
+
+def test_dp_train_steps_equal_per_step_dp_calls():
+    """Two ranks (gloo, torch-reduced gradient buffer): fit's loop through
+    train_steps equals per-step data-parallel train_step calls bit for bit on
+    every rank, and the replicas stay identical."""
+    out = _launch(_dp_train_steps)
+    for r in (0, 1):
+        steps, calls = out[r]
+        for a, b in zip(steps, calls):
+            np.testing.assert_array_equal(a, b)
+        assert steps[4] == 6
+    np.testing.assert_array_equal(out[0][0][1], out[1][0][1])
+
+
 def _snr(rank, world):
     mean, x, _ = _data()
     from iwae_replication_project_amd import Flexible_Model

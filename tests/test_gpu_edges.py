@@ -262,6 +262,42 @@ def test_train_steps_equal_single_step_calls(B, n):
         assert runs[0][3] == r[3] == 2 * n
 
 
+@pytest.mark.parametrize("B,n", [(20, 20), (20, 45), (512, 3)])
+def test_prepared_train_steps_capture_nothing_more_and_equal_unprepared(B, n):
+    """iwae_train_steps_prepare captures the graphs of a later train_steps call
+    (one per step count: 45 = 32 + 13 gives two) without running anything:
+    weights, Adam step and an evaluation on injected noise are those of an
+    unprepared model; the call then captures nothing (capture counter, id 7)
+    and its losses, weights and Adam state equal the unprepared run bit for
+    bit.  bench.py relies on this to time steady-state replays only."""
+    import torch
+    rng = np.random.default_rng(31 + B + n)
+    xs = (rng.random((n * B, 784)) < 0.25).astype(np.float32)
+    xe = xs[:4]
+    eps = [rng.standard_normal((5, 4, d)).astype(np.float32) for d in ARCH2[2]]
+    runs = []
+    for prep in (False, True):
+        m = _model(ARCH2, "IWAE", 50)
+        X = torch.from_numpy(xs).to(m.device)
+        w0 = _flat(m.get_weights())
+        if prep:
+            c0 = m.graph_captures()
+            m.prepare_train_steps(X, B)
+            assert m.graph_captures() - c0 == (2 if n > 32 and n % 32 else 1)
+            np.testing.assert_array_equal(_flat(m.get_weights()), w0)
+            assert m.get_optimizer_state()[2] == 0
+        lw = m.get_log_weights(xe, 5, eps=eps).cpu().numpy()
+        c1 = m.graph_captures()
+        losses = m.train_steps(X, B)
+        if prep:
+            assert m.graph_captures() == c1
+        mm, vv, st = m.get_optimizer_state()
+        runs.append((lw, np.asarray(losses, np.float32), _flat(m.get_weights()), mm, st))
+    for a, b in zip(runs[0], runs[1]):
+        np.testing.assert_array_equal(a, b)
+    assert runs[0][4] == n
+
+
 @pytest.mark.parametrize("B", [64, 512])
 def test_input_gemm_on_the_callers_x_equals_the_staged_copy(B):
     """Above the few-row launches' 32 images the engine step's input Dense is

@@ -320,21 +320,32 @@ def test_weight_ring_train_forward_runs_at_large_batch_only():
         assert (m._lib.iwae_debug_count(m._h, 4) > n0) == want, B
 
 
-@pytest.mark.parametrize("B,k1,k2", [(20, 8, 8), (7, 4, 3)])
-def test_piwae_one_unit_chain_matches_two_chains(B, k1, k2):
+ARCH1 = ([200], [200], [50], [784])
+
+
+@pytest.mark.parametrize("B,k1,k2,arch,tune", [
+    (20, 8, 8, ARCH2, {}),                                  # fused update (run_update)
+    (7, 4, 3, ARCH2, {}),
+    (20, 8, 8, ARCH1, {}),                                  # one stochastic layer: only o1 / o2 / o3 rescaled
+    (128, 8, 8, ARCH2, {"nring_train": 0}),                 # 8192 rows > upd_rows: the dw_kernel pass (run_dw)
+    (128, 8, 8, ARCH2, {"nring_train": 0, "dw_wide": 0}),   # ... the update kernel's slab pass
+    (20, 8, 8, ARCH2, {"upd": 0, "upd_slabs": 0}),          # grouped split-K weight-gradient GEMMs
+], ids=["b20", "b7", "1L", "b128-dw", "b128-slabs", "grouped-gemm"])
+def test_piwae_one_unit_chain_matches_two_chains(B, k1, k2, arch, tune):
     """PIWAE (PDF p7) with ONE backward chain at unit row weights, the decoder's
     weight gradients scaled by the IWAE_{k1 k2} weighting and the encoder's by
     the MIWAE(k1, k2) one (knob piwae_one, default), against the chain run twice
-    (piwae_one 0): same loss bits, gradient and post-Adam weights to rounding."""
+    (piwae_one 0): same loss bits, gradient and post-Adam weights to rounding --
+    through every weight-gradient pass the unit chain can feed."""
     from iwae_replication_project_amd import Adam, Flexible_Model
     rng = np.random.default_rng(68 + B)
     k = k1 * k2
     x = (rng.random((B, 784)) < 0.2).astype(np.float32)
-    eps = [rng.standard_normal((k, B, d)).astype(np.float32) for d in ARCH2[2]]
+    eps = [rng.standard_normal((k, B, d)).astype(np.float32) for d in arch[2]]
 
     def step(flag):
-        m = Flexible_Model(*ARCH2, dataset_bias=None, loss_function="PIWAE", k=k, k1=k1, k2=k2, seed=14,
-                           tuning={"piwae_one": flag})
+        m = Flexible_Model(*arch, dataset_bias=None, loss_function="PIWAE", k=k, k1=k1, k2=k2, seed=14,
+                           tuning=dict(tune, piwae_one=flag))
         m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
         n0 = m._lib.iwae_debug_count(m._h, 2)
         loss = m.train_step(x, eps=eps)["PIWAE"]

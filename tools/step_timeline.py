@@ -17,9 +17,10 @@ def load(path):
                 c.execute("select name, start, end, grid_x, workgroup_x from kernels order by start")]
     rows = []
     for r in csv.DictReader(open(path)):
-        rows.append((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
-                     int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0),
-                     int(r.get("Workgroup_Size_X", r.get("Workgroup_Size", 1)) or 1)))
+        gx = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)
+        wx = int(r.get("Workgroup_Size_X", r.get("Workgroup_Size", 1)) or 1)
+        gy = int(r.get("Grid_Size_Y", 1) or 1) // max(1, int(r.get("Workgroup_Size_Y", 1) or 1))
+        rows.append((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]), gx * gy, wx))
     rows.sort(key=lambda r: r[1])
     return rows
 
@@ -29,7 +30,11 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 12
     first = sys.argv[3] if len(sys.argv) > 3 else None
     if first:
-        idx = max(i for i, r in enumerate(rows) if first in r[0])
+        # "name" or "name@workgroups"; the last such launch with n launches after it
+        name, _, wg = first.partition("@")
+        hit = [i for i, r in enumerate(rows) if name in r[0] and (not wg or r[3] // max(r[4], 1) == int(wg))]
+        full = [i for i in hit if i + n <= len(rows)]
+        idx = max(full or hit)
         sel = rows[idx:idx + n]
     else:
         sel = rows[-n:]
