@@ -48,6 +48,96 @@ FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32
 BF16_PEAK_TFLOPS = 2500.0          # MI355X_MICROARCH.md: BF16 MFMA dense peak
 BF16X3_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 3, 1)   # f32-accurate bf16x3 products: 3 bf16 MFMAs each
 HBM_PEAK_GBS = 8000.0
+# ---- roofline model: algorithmic FLOP and HBM bytes per launch
+# of the train step's kernels, 2L model, from the layer widths.  Bytes count every
+# tensor a launch must read or write across its boundary ONCE (f32, 4 B): the
+# weights it multiplies, its inputs, and what a later launch reads; split-K
+# partials, re-reads and padding are implementation traffic (the PMC "traffic"
+# beside it shows them).  A kernel is MFMA-bound when its FLOP / byte ratio is
+# above the ridge (833.3 TFLOP/s / 8 TB/s = 104 FLOP/B), else HBM-bound; frac =
+# max(t_mfma, t_hbm) / t.
+# (fin, fout, image rows?) per Dense layer: encoder layer 1 (per image), encoder
+# layer 2, decoder prior layer, output MLP
+LAYERS_2L = {"e1.l1": (784, 200, True), "e1.l2": (200, 200, True), "e1.head": (200, 200, True),
+             "e2.l1": (100, 100, False), "e2.l2": (100, 100, False), "e2.head": (100, 100, False),
+             "p.l1": (50, 100, False), "p.l2": (100, 100, False), "p.head": (100, 200, False),
+             "o1": (100, 200, False), "o2": (200, 200, False), "o3": (200, 784, False)}
+ROW_LAYERS = [k for k, v in LAYERS_2L.items() if not v[2]]
+OUT_MLP, ENC_PRIOR = ["o1", "o2", "o3"], ["e2.l1", "e2.l2", "e2.head", "p.l1", "p.l2", "p.head"]
+# floats per sample row the forward stores for later launches: h1, eps1; e2: y1, y2, (mu|zs), h2, eps2;
+# prior: y1, y2, (mu|zs); output MLP: y1, y2, g; log q, log p, Bernoulli sum
+FWD_STORE_ROW = 200 + (100 + 100 + 100 + 50 + 50) + (100 + 100 + 200) + (200 + 200 + 784) + 3
+# output-MLP backward-data: reads g, dpx, y2, y1; writes dY2, dY1, dL/dh1
+OUT_BWD_ROW = (784 + 1 + 200 + 200) + (200 + 200 + 100)
+# encoder / prior backward-data: reads dlw; prior (mu|zs), its target h1, y2, y1; e2 (mu|zs), h2, eps2, y2,
+# y1; writes prior dP, dY2, dY1, dL/dh1 (prior); e2 dP, dY2, dY1, dL/dh1 (encoder)
+ENC_BWD_ROW = 1 + (200 + 100 + 100 + 100) + (100 + 50 + 50 + 100 + 100) + (200 + 100 + 100 + 100) + \
+    (100 + 100 + 100 + 100)
+# weight gradients of the sample-row layers: every X and dZ operand once (h1 feeds e2.l1 and o1: once), dpx
+WGRAD_ROW = (100 + 100 + 100 + 50 + 100 + 100 + 200 + 200) + (100 + 100 + 100 + 100 + 100 + 200 + 200 + 200 + 784) + 1
+# the first encoder layer's backward on image rows: reads per sample row h1, eps1, dlw and three dL/dh1
+# sources; per image (mu|zs), y2, y1; writes per image dP0, dY2, dY1
+IMG_BWD_ROW, IMG_BWD_IMG = 100 + 100 + 1 + 300, 200 + 200 + 200 + 600
+
+
+def layer_params(names):
+    return sum((LAYERS_2L[n][0] + 1) * LAYERS_2L[n][1] for n in names)
+
+
+def layer_macs(names, bias=False):
+    return sum((LAYERS_2L[n][0] + (1 if bias else 0)) * LAYERS_2L[n][1] for n in names)
+
+
+N_PARAMS = layer_params(LAYERS_2L)
+
+
+def kernel_work(kind, rows, images):
+    """(algorithmic FLOP, algorithmic HBM bytes) of one launch of a train-step
+    kernel kind over `rows` sample rows of `images` images (see above)."""
+    W = 4.0 * layer_params(ROW_LAYERS)
+    if kind == "fwd":          # sample-row forward: engine jobs E + O, or the ring kernel in train mode
+        return 2.0 * rows * SAMPLE_ROW_MACS, W + 4.0 * (images * (784 + 200) + rows * FWD_STORE_ROW)
+    if kind == "bwd":          # the engine's backward launch: jobs O' + E' (and the bound, a few KB)
+        return 2.0 * rows * SAMPLE_ROW_MACS, W + 4.0 * rows * (OUT_BWD_ROW + ENC_BWD_ROW)
+    if kind == "nrb":
+        return 2.0 * rows * layer_macs(OUT_MLP), 4.0 * layer_params(OUT_MLP) + 4.0 * rows * OUT_BWD_ROW
+    if kind == "nre":
+        return 2.0 * rows * layer_macs(ENC_PRIOR), 4.0 * layer_params(ENC_PRIOR) + 4.0 * rows * ENC_BWD_ROW
+    if kind == "dw":           # the sample-row layers' dW_aug = X_aug^T dZ, written once
+        return 2.0 * rows * layer_macs(ROW_LAYERS, bias=True), 4.0 * (rows * WGRAD_ROW + layer_params(ROW_LAYERS))
+    if kind == "img_bwd":      # job I': the first encoder layer's Gaussian backward (sum over k) + head^T, l2^T
+        return (2.0 * images * (200 * 200 + 200 * 200),
+                4.0 * (rows * IMG_BWD_ROW + images * IMG_BWD_IMG + layer_params(["e1.l2", "e1.head"])))
+    if kind == "img_fwd":      # job I: the first encoder layer's l2 and head on image rows (after its input Dense)
+        return (2.0 * images * (200 * 200 + 200 * 200),
+                4.0 * (images * (200 + 200 + 200 + 200) + layer_params(["e1.l2", "e1.head"])))
+    if kind == "upd":          # every layer's dW + Adam (p, m, v read; p, m, v, g written) + FX / GX bf16 copies
+        img_xz = images * (785 + 201 + 201 + 200 + 200 + 200)
+        fl = 2.0 * (rows * layer_macs(ROW_LAYERS, bias=True) +
+                    images * layer_macs(["e1.l1", "e1.l2", "e1.head"], bias=True))
+        return fl, 4.0 * (rows * WGRAD_ROW + img_xz + 7 * N_PARAMS) + 8.0 * N_PARAMS
+    raise ValueError(kind)
+
+
+def roofline_of(flop, nbytes, us, peak_tflops=None, hbm_gbs=None):
+    """Binding roofline of a launch: MFMA if flop / byte is above the ridge,
+    else HBM; frac = max(t_mfma, t_hbm) / t."""
+    pk = peak_tflops or round(2500.0 / 3, 1)
+    hb = hbm_gbs or 8000.0
+    t = us * 1e-6
+    t_mfma, t_hbm = flop / (pk * 1e12), nbytes / (hb * 1e9)
+    ai = flop / nbytes if nbytes else float("inf")
+    if t_mfma >= t_hbm:
+        return dict(bound="mfma", achieved=round(flop / t / 1e12, 3), peak=pk, unit="TFLOP/s",
+                    frac=round(t_mfma / t, 4), flop_per_byte=round(ai, 1), ridge=round(pk * 1e3 / hb, 1),
+                    alg_bytes=nbytes, flop=flop)
+    return dict(bound="hbm", achieved=round(nbytes / t / 1e9, 1), peak=hb, unit="GB/s", frac=round(t_hbm / t, 4),
+                flop_per_byte=round(ai, 1), ridge=round(pk * 1e3 / hb, 1), alg_bytes=nbytes, flop=flop)
+
+
+LB_RECORD = "r04_large_batch_kernels.json"     # the large-batch step's committed kernel record
+
+
 PRECISION = ("fp32 values and fp32 accumulation everywhere; every sample-row matrix product of the train step "
              "(forward, backward-data and weight gradients) and of the NLL is a bf16x3 split product "
              "(a_hi b_hi + a_hi b_lo + a_lo b_hi on bf16 MFMA, ~2^-16 relative per product); the first encoder "
@@ -409,28 +499,28 @@ def main():
             return None
         return ms.value / args.steps, fl.value / args.steps
 
-    # algorithmic FLOP per launch: the forward and backward launches each do one
-    # product per sample-row Dense layer (281,800 MACs per row);
-    # the library's own count of the forward includes the output MLP's two
-    # hidden layers that its column-split jobs recompute (reported as executed)
+    # algorithmic FLOP and bytes per launch (kernel_work): the forward and backward
+    # launches each do one product per sample-row Dense layer (281,800 MACs per
+    # row); the library's own count of the forward includes the
+    # output MLP's two hidden layers that its column-split jobs recompute
+    # (reported as executed).  Each kernel is priced against the roofline its
+    # FLOP / byte ratio puts it under (roofline_of).
     rows_step = B_PER_GPU * K
-    alg = {10: 2.0 * SAMPLE_ROW_MACS * rows_step, 11: 2.0 * SAMPLE_ROW_MACS * rows_step}
-    specs = {"tc_kernel forward (train engine, bf16x3)": (10, 0, BF16X3_PEAK_TFLOPS),
-             "tc_kernel backward (train engine, bf16x3)": (11, 0, BF16X3_PEAK_TFLOPS),
-             "gemm_kernel<FWD, EPI_BERN> (output layer, f32 MFMA)": (0, 2, FP32_MFMA_PEAK_TFLOPS),
-             "upd_kernel (weight gradients + Adam + FX copies, bf16x3)": (15, 0, BF16X3_PEAK_TFLOPS)}
+    specs = {"tc_kernel forward (train engine, bf16x3)": (10, 0, "fwd"),
+             "tc_kernel backward (train engine, bf16x3)": (11, 0, "bwd"),
+             "upd_kernel (weight gradients + Adam + FX copies, bf16x3)": (15, 0, "upd")}
     kern = {}
-    for name, (kind, epi, pk) in specs.items():
+    for name, (kind, epi, wk) in specs.items():
         v = live(kind, epi)
         if v is None:
             continue
-        fl = alg.get(kind, v[1])
+        fl, nby = kernel_work(wk, rows_step, B_PER_GPU)
+        r = roofline_of(fl, nby, v[0] * 1e3)
         kern[name] = dict(avg_us=round(v[0] * 1e3, 3), flop_per_launch=fl, flop_executed=v[1],
-                          tflops=round(fl / (v[0] * 1e-3) / 1e12, 3), peak=pk)
+                          alg_bytes_per_launch=nby, tflops=round(fl / (v[0] * 1e-3) / 1e12, 3),
+                          bound=r["bound"], frac=r["frac"], flop_per_byte=r["flop_per_byte"])
     dom = max(kern, key=lambda k: kern[k]["avg_us"])
     kd = kern[dom]
-    achieved = kd["tflops"]
-    peak = kd["peak"]
     # HBM traffic of the same kernel: committed rocprofv3 PMC record (tools/pmc_passes.sh +
     # tools/pmc_to_json.py; FETCH_SIZE x2 per the gfx950 correction, WRITE_SIZE as is)
     traffic, traffic_src = None, None
@@ -443,13 +533,16 @@ def main():
             traffic = round(rec["traffic_bytes"] / 1e6, 3)
             traffic_src = f"profiles/{pmc_name} (MB per launch: fetch {rec['fetch_bytes'] / 1e6:.2f} + " \
                           f"write {rec['write_bytes'] / 1e6:.2f})"
-    roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=peak, unit="TFLOP/s",
-                    frac=round(achieved / peak, 4), traffic=traffic, traffic_unit="MB/launch",
-                    traffic_source=traffic_src, kernel=dom, avg_us=kd["avg_us"],
-                    flop_per_launch=kd["flop_per_launch"], launches=args.steps,
-                    peak_basis=("bf16 dense 2.5 PFLOP/s / 3 bf16 MFMAs per bf16x3 product" if peak == BF16X3_PEAK_TFLOPS
-                                else "f32 MFMA 157.3 TFLOP/s"),
-                    frac_of_bf16_dense_peak=round(achieved / BF16_PEAK_TFLOPS, 4),
+    fl, nby = kd["flop_per_launch"], kd["alg_bytes_per_launch"]
+    roofline = roofline_of(fl, nby, kd["avg_us"])
+    roofline.update(traffic=traffic, traffic_unit="MB/launch", traffic_source=traffic_src,
+                    traffic_over_alg=(round(traffic * 1e6 / nby, 2) if traffic else None),
+                    kernel=dom, avg_us=kd["avg_us"], flop_per_launch=fl, alg_MB_per_launch=round(nby / 1e6, 3),
+                    launches=args.steps,
+                    peak_basis=("mfma: bf16 dense 2.5 PFLOP/s / 3 bf16 MFMAs per bf16x3 product; hbm: 8 TB/s; "
+                                "bound = the larger of FLOP / 833.3 TFLOP/s and bytes / 8 TB/s (ridge 104 FLOP/B)"),
+                    mfma_frac=round(fl / (kd["avg_us"] * 1e-6) / 1e12 / BF16X3_PEAK_TFLOPS, 4),
+                    frac_of_bf16_dense_peak=round(fl / (kd["avg_us"] * 1e-6) / 1e12 / BF16_PEAK_TFLOPS, 4),
                     kernels=kern, step_tflops=round(TRAIN_FLOP_PER_ROW * rows / el / 1e12, 3))
 
     # ---- the train step's memory-bound launches (Adam, bound, FX refresh), same
@@ -503,20 +596,22 @@ def main():
                      precision=PRECISION)
         # the step's kernels against their rooflines: committed rocprofv3 kernel trace + PMC
         # record of the same step (tools/gpu_lbpmc.sh -> tools/lb_record.py)
-        lbr = os.path.join(ROOT, "profiles", "r04_large_batch_kernels.json")
+        lbr = os.path.join(ROOT, "profiles", LB_RECORD)
         if os.path.exists(lbr):
             with open(lbr) as f:
                 kr = json.load(f)
             ks = kr.get("kernels", {})
-            mf = {k: v for k, v in ks.items() if v.get("bound") == "mfma" and "frac" in v}
-            if mf:
-                dom = max(mf, key=lambda k: mf[k]["avg_us"])
-                d = mf[dom]
-                large["roofline"] = dict(bound="mfma", kernel=dom, achieved=d["tflops"], peak=d["peak_tflops"],
-                                         unit="TFLOP/s", frac=d["frac"], avg_us=d["avg_us"],
+            pr = {k: v for k, v in ks.items() if "frac" in v and "bound" in v}
+            if pr:
+                dom = max(pr, key=lambda k: pr[k]["avg_us"])
+                d = pr[dom]
+                large["roofline"] = dict(bound=d["bound"], kernel=dom, achieved=d.get("achieved"), peak=d.get("peak"),
+                                         unit=d.get("unit"), frac=d["frac"], avg_us=d["avg_us"],
+                                         flop_per_byte=d.get("flop_per_byte"),
+                                         alg_MB_per_launch=d.get("alg_MB_per_launch"),
                                          traffic=d.get("hbm_MB_per_launch"), traffic_unit="MB/launch",
-                                         source="profiles/r04_large_batch_kernels.json (rocprofv3 trace + PMC "
-                                                "of tools/train_large.py 512)")
+                                         source=f"profiles/{LB_RECORD} (rocprofv3 trace + PMC of "
+                                                "tools/train_large.py 512; tools/lb_record.py)")
             large["kernels"] = ks
 
     # ---- k=5000 NLL over the test images, sharded by image

@@ -149,7 +149,9 @@ enum iwae_knob {
   IWAE_KNOB_IMG_ROWS_FWD = 31,     /* image-row job I (first encoder layer's l2 / head): images per workgroup,
                                       <= 16 (0: auto, ceil(B / 256)) */
   IWAE_KNOB_IMG_ROWS_BWD = 32,     /* image-row job I' (its backward): images per workgroup (0: auto) */
-  IWAE_KNOB_X_DIRECT = 33          /* 1: a large-batch engine step's input GEMM reads the caller's x (default); 0: staged copy */
+  IWAE_KNOB_X_DIRECT = 33,         /* 1: a large-batch engine step's input GEMM reads the caller's x (default); 0: staged copy */
+  IWAE_KNOB_TCU = 34               /* the first encoder layer's image-row backward (job I') and the fused update in one
+                                      launch, its tiles of that layer waiting in-launch for job I' (1) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --
@@ -312,7 +314,10 @@ double iwae_workspace_bytes(const iwae_handle* h);
  * the weight-ring backward kernel (nrb_kernel), 6 encoder / prior backwards
  * run by nre_kernel, 7 train-step graphs captured (iwae_train_step,
  * iwae_train_steps, iwae_train_steps_prepare; bench.py asserts it stays flat
- * across its timed region); -1 for an unknown id. */
+ * across its timed region), 8 in-launch waits of the combined image-row
+ * backward + update launch that gave up (synchronous; 0 unless the GPU was
+ * shared with a kernel that held CUs for ~1 s), 9 such combined launches
+ * issued (a captured step counts once, at capture); -1 for an unknown id. */
 long long iwae_debug_count(const iwae_handle* h, int what);
 /* Live kernel timing: bracket every launch of one kernel class with HIP events
  * on the handle's stream -- a GEMM class (kind: 0 forward, 1 backward-data,

@@ -383,7 +383,15 @@ struct UpdArgs {
   int waves;                                          // 4, or 8 (64-column tiles: two waves per SIMD)
 };
 hipError_t launch_update(hipStream_t st, const UpdArgs& a);
+// in-launch wait of the update's first-encoder-layer tiles on the image-row
+// backward workgroups of tcu_kernel (iwae_update_dev.h, upd_wait)
+struct UpdWait {
+  unsigned* ctr;              // [0] producers done, [1] consumers through, [2] spin give-ups
+  unsigned wait_mask;         // jobs whose tiles wait
+  int n_prod, n_cons;
+};
 hipError_t upd_setup_attributes();
+size_t upd_lds_bytes();             // dynamic LDS of an update workgroup
 
 // Large-batch weight gradients into split-K slabs (iwae_dwgrad.hip): per layer,
 // workgroup blocks of 7 x 16 W_aug rows by 8 * nb x 16 columns over a row chunk.
@@ -696,6 +704,8 @@ struct TcArgs {
   BoundArgs bnd; int bnd_rows, bnd_block, bnd_ld, bnd_lds;
 };
 hipError_t launch_tc(hipStream_t st, const TcArgs& a, int rt, size_t lds_bytes);
+// job I' (a one-job image-row plan, RT = 1) and the fused update (8 waves) in one launch
+hipError_t launch_tcu(hipStream_t st, const TcArgs& a, const UpdArgs& u, const UpdWait& w, size_t lds_bytes);
 hipError_t tc_setup_attributes();
 
 hipError_t launch_fill_col(hipStream_t st, float* buf, int rows, int ld, int col, float v);

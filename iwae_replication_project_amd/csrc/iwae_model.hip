@@ -177,6 +177,7 @@ struct iwae_handle {
   long long n_mega = 0, n_mega_eps = 0;  // mega_fwd_kernel launches (all / injected noise), iwae_debug_count
   long long n_tc = 0;                    // train-engine launches (tc_kernel), iwae_debug_count(h, 2)
   long long n_captures = 0;              // train-step graphs captured (single and multi-step), iwae_debug_count(h, 7)
+  long long n_tcu = 0;                   // combined job I' + update launches (tcu_kernel), iwae_debug_count(h, 9)
   const float* mask[IWAE_MAX_LAYERS] = {};
   // row-chain train engine plans (device resident, per shape; iwae_train.hip)
   struct TcRec {
@@ -211,6 +212,16 @@ struct iwae_handle {
                                      // k step costs ~2 us whatever its tiles; alpha 0 / 45 / 90 / 200: 174 / 127 / 108 / 106 us)
   int img_rows_fwd = 0, img_rows_bwd = 0;   // image-row jobs I / I': rows per workgroup (0: auto)
   int x_direct = 1;                  // large-batch engine step: the input GEMM reads the caller's x (gemm_direct)
+  int tcu = 1;                       // job I' and the fused update in one launch (tcu_kernel) where it fits
+  unsigned* tcu_ctr = nullptr;       // its in-launch counters (zero between launches; [2] spin give-ups)
+  bool defer_launch = false;         // (during a step) tc_run / run_update record their launch instead
+  bool pend_tc_have = false, pend_upd_have = false;
+  TcArgs pend_tc{};
+  int pend_tc_rt = 1;
+  size_t pend_tc_lds = 0;
+  UpdArgs pend_upd{};
+  unsigned pend_upd_mask = 0;        // update jobs that read job I''s output (the first encoder layer's)
+  int pend_upd_cons = 0;             // their tiles
   int piwae_one = 1;                 // PIWAE: one unit-weight backward chain serves both weightings (knob)
   bool piwae_ks = false;             // (during a step) the weight gradients apply the per-layer PIWAE weighting
   int tc_rt = 1;                     // row tiles of 16 per engine workgroup below wide_rows
@@ -1596,7 +1607,21 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int bucket = 0, 
   a.gscale = slabs ? 1.f : gscale; a.tail = (slabs || apply) ? nullptr : tail; a.tail_val = gscale;
   a.apply = apply ? 1 : 0; a.scale_dev = scale_dev;
   a.waves = h->upd_waves;
-  HIPCHK(launch_update(st, a));
+  if (h->defer_launch && st == h->stream && !slabs && !apply) {
+    // recorded for a combined launch (tcu_kernel) with job I': the first
+    // encoder layer's jobs are the ones that wait for it
+    h->pend_upd = a; h->pend_upd_have = true;
+    h->pend_upd_mask = 0; h->pend_upd_cons = 0;
+    for (int j = 0; j < a.njobs; ++j) {
+      const int di = js[j].di;
+      if (di == h->enc[0].l1 || di == h->enc[0].l2 || di == h->enc[0].head) {
+        h->pend_upd_mask |= 1u << j;
+        h->pend_upd_cons += a.job[j].tiles_m * a.job[j].tiles_n;
+      }
+    }
+  } else {
+    HIPCHK(launch_update(st, a));
+  }
   if (a.do_adam) h->params_version++;
   if (h->prof_kind == 15 && adam && !h->prof_have) {
     // replays repeat this step's update on scratch copies of the parameters,
@@ -2148,6 +2173,11 @@ static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which, con
   }
   const bool prof = which <= 1 && h->prof_kind == 10 + which;
   h->n_tc++;
+  if (h->defer_launch) {
+    // recorded for a combined launch (tcu_kernel); launch_pending issues it
+    h->pend_tc = a; h->pend_tc_rt = rec.rt; h->pend_tc_lds = rec.lds; h->pend_tc_have = true;
+    return IWAE_OK;
+  }
   if (prof) {
     if (h->prof_used + 2 > h->prof_ev.size()) {
       for (int i = 0; i < 256; ++i) {
@@ -2223,6 +2253,33 @@ static bool nring_train_backward_enc(iwae_handle* h, const Plan& P, bool& ran);
 static bool piwae_unit(const iwae_handle* h, const Plan& P, bool ring) {
   return P.piwae && !ring && (h->engine_img_bwd || (h->engine_img && !smallm_ok(h, P.Bimg))) && h->piwae_one;
 }
+// Issue the launches tc_run / run_update recorded under defer_launch: job I'
+// and the fused update as ONE tcu_kernel launch when every workgroup of it is
+// resident at once (grid <= 256 at one 512-thread workgroup per CU: the
+// update's 147 KiB of LDS), else as the two launches they would have been.
+static int launch_pending(iwae_handle* h) {
+  const bool tc = h->pend_tc_have, up = h->pend_upd_have;
+  h->pend_tc_have = h->pend_upd_have = false;
+  if (tc && up) {
+    const TcArgs& a = h->pend_tc;
+    const UpdArgs& u = h->pend_upd;
+    const int n_tc = a.block_start[kTcMaxJobs];
+    const int grid = ((n_tc + 7) & ~7) + 8 * (u.per_xcd + u.per_xcd2);
+    const bool ok = h->pend_tc_rt == 1 && a.xcd_slots == 0 && a.bnd_block < 0 && !u.search && !u.apply &&
+                    grid <= 256 && n_tc > 0 && h->pend_upd_cons > 0;
+    if (ok) {
+      UpdWait w;
+      w.ctr = h->tcu_ctr; w.wait_mask = h->pend_upd_mask; w.n_prod = n_tc; w.n_cons = h->pend_upd_cons;
+      HIPCHK(launch_tcu(h->stream, a, u, w, std::max(h->pend_tc_lds, upd_lds_bytes())));
+      h->n_tcu++;
+      return IWAE_OK;
+    }
+  }
+  if (tc) HIPCHK(launch_tc(h->stream, h->pend_tc, h->pend_tc_rt, h->pend_tc_lds));
+  if (up) HIPCHK(launch_update(h->stream, h->pend_upd));
+  return IWAE_OK;
+}
+
 static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, bool adam) {
   // The first encoder layer's l2 / head: up to 32 images the few-row N-split
   // launches (one 16-column tile per workgroup; at B = 20 the image-row jobs,
@@ -2301,6 +2358,14 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   // Its image-row job also at small batches (B = 20: step 128.1 -> 126.4 us
   // against the row-block Gaussian backward + two few-row launches)
   const bool img_bwd = img || h->engine_img_bwd;
+  // job I' and the fused update as one launch (tcu_kernel): recorded here,
+  // issued by launch_pending below
+  const bool tcu = img_bwd && h->tcu && use_update(h, P) && !h->dp_weighted && h->prof_kind < 0 && !h->upd_tn32;
+  struct DeferReset {
+    iwae_handle* h;
+    ~DeferReset() { h->defer_launch = false; h->pend_tc_have = h->pend_upd_have = false; }
+  } defer_reset{h};
+  h->defer_launch = tcu;
   if (img_bwd) CHK(tc_run(h, P, E, 3, nullptr, enc_dlw, nullptr, unit));
   else CHK(fused_encoder_bwd(h, P, P.piwae ? h->dlw2 : h->dlw, 0));
   if (use_update(h, P) && h->dp_weighted) {
@@ -2336,6 +2401,8 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   if (use_update(h, P)) {
     // weight gradients, Adam and the fragment-major copies in one launch
     CHK(run_update(h, P, adam));
+    h->defer_launch = false;
+    CHK(launch_pending(h));
     if (adam) h->fx_version = h->params_version;
     return IWAE_OK;
   }
@@ -2747,6 +2814,8 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (e == hipSuccess) e = hipMalloc(&h->adam_v, pb);
   if (e == hipSuccess) e = hipMalloc(&h->grad_own, pb + 4 * sizeof(float));   // + the DP batch-size tail
   if (e == hipSuccess) e = hipMalloc(&h->ds, sizeof(DevState));
+  if (e == hipSuccess) e = hipMalloc(&h->tcu_ctr, 4 * sizeof(unsigned));
+  if (e == hipSuccess) e = hipMemset(h->tcu_ctr, 0, 4 * sizeof(unsigned));
   if (e == hipSuccess) e = hipMalloc(&h->wsplit_hi, (size_t)(2 * h->wsplit_elems) * sizeof(__bf16));
   if (e == hipSuccess) e = hipMalloc(&h->fx_hi, (size_t)(2 * h->fx_elems) * sizeof(__bf16));
   if (e == hipSuccess) e = hipMemset(h->fx_hi, 0, (size_t)(2 * h->fx_elems) * sizeof(__bf16));
@@ -2798,6 +2867,7 @@ void iwae_destroy(iwae_handle* h) {
   if (h->adam_v) (void)hipFree(h->adam_v);
   if (h->grad_own) (void)hipFree(h->grad_own);
   if (h->ds) (void)hipFree(h->ds);
+  if (h->tcu_ctr) (void)hipFree(h->tcu_ctr);
   if (h->loss_slots) (void)hipFree(h->loss_slots);
   if (h->nr_units) (void)hipFree(h->nr_units);
   if (h->nrb_units) (void)hipFree(h->nrb_units);
@@ -2942,6 +3012,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_IMG_ROWS_FWD: h->img_rows_fwd = (int)std::max(0LL, std::min(value, 16LL)); break;
     case IWAE_KNOB_IMG_ROWS_BWD: h->img_rows_bwd = (int)std::max(0LL, std::min(value, 16LL)); break;
     case IWAE_KNOB_X_DIRECT: h->x_direct = on; break;
+    case IWAE_KNOB_TCU: h->tcu = on; break;
     case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;
@@ -3809,6 +3880,13 @@ long long iwae_debug_count(const iwae_handle* h, int what) {
     case 5: return h->n_nrb;
     case 6: return h->n_nre;
     case 7: return h->n_captures;
+    case 8: {                           // tcu_kernel spin give-ups so far (synchronous read)
+      unsigned v[4] = {};
+      if (hipStreamSynchronize(h->stream) != hipSuccess ||
+          hipMemcpy(v, h->tcu_ctr, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+      return v[2];
+    }
+    case 9: return h->n_tcu;
     default: return -1;
   }
 }

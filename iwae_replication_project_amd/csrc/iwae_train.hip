@@ -31,6 +31,7 @@
 // store per LDS plane.
 #include "iwae_kernels.h"
 #include "iwae_bound.h"
+#include "iwae_update_dev.h"
 
 namespace iwae {
 
@@ -1092,10 +1093,10 @@ __device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int r
 
 // ----------------------------------------------------------------- kernel
 template <int RT>
-__global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
+__device__ __forceinline__ void tc_body(const TcArgs& A, const int bid) {
   constexpr int R = 16 * RT;
   CPlan* plan = (CPlan*)A.plan;
-  if ((int)blockIdx.x == A.bnd_block) {
+  if (bid == A.bnd_block) {
     // the step's bound (bound_kernel's work in this launch's spare workgroup)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float* red = tcs;
@@ -1107,13 +1108,13 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
   }
   int jb = 0, blk;
   if (A.xcd_slots > 0) {
-    const int x = (int)blockIdx.x & 7;
+    const int x = bid & 7;
     jb = A.xcd_job[x];
-    blk = ((int)blockIdx.x >> 3) * A.xcd_count[jb] + A.xcd_rank[x];
+    blk = (bid >> 3) * A.xcd_count[jb] + A.xcd_rank[x];
     if (blk >= A.block_start[jb + 1] - A.block_start[jb]) return;     // idle: before any barrier
   } else {
-    while (jb + 1 < plan->njobs && (int)blockIdx.x >= A.block_start[jb + 1]) ++jb;
-    blk = (int)blockIdx.x - A.block_start[jb];
+    while (jb + 1 < plan->njobs && bid >= A.block_start[jb + 1]) ++jb;
+    blk = bid - A.block_start[jb];
   }
   CJob& J = plan->job[jb];
   tc_warm_descriptors(J);
@@ -1257,6 +1258,56 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
   }
 }
 
+template <int RT>
+__global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
+  tc_body<RT>(A, (int)blockIdx.x);
+}
+
+// The first encoder layer's image-row backward (job I', one row tile per
+// workgroup) and the fused update in ONE launch (B = 20: 20 + 186 workgroups
+// on 256 CUs): blocks [0, n_tc) run job I' and publish (every wave's stores
+// drained, the workgroup's barrier, one agent-scope release, a counter add);
+// blocks from n_tc_pad run upd_kernel's body, whose first-encoder-layer tiles
+// (the jobs in W.wait_mask) wait on that counter -- the sample-row tiles, the
+// bulk of the launch, run beside job I' instead of after it.
+__global__ __launch_bounds__(TC_NW * 64) void tcu_kernel(TcArgs A, UpdArgs U, UpdWait W, int n_tc, int n_tc_pad) {
+  const int b = (int)blockIdx.x;
+#ifdef IWAE_TCU_TRACE
+  if (threadIdx.x == 0 && b < 512) { g_tcu_trace[b * 4] = wall_clock64(); g_tcu_trace[b * 4 + 3] = b < n_tc ? 0 : 1; }
+#endif
+  if (b < n_tc_pad) {
+    if (b >= n_tc) return;
+    tc_body<1>(A, b);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's stores done
+    __syncthreads();
+#ifdef IWAE_TCU_TRACE
+    if (threadIdx.x == 0) g_tcu_trace[b * 4 + 1] = wall_clock64();
+#endif
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the XCD's L2 written back
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(W.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#ifdef IWAE_TCU_TRACE
+    if (threadIdx.x == 0) g_tcu_trace[b * 4 + 2] = wall_clock64();
+#endif
+    return;
+  }
+  upd_body<TC_NW>(U, b - n_tc_pad, &W);
+#ifdef IWAE_TCU_TRACE
+  __syncthreads();
+  if (threadIdx.x == 0 && b < 512) g_tcu_trace[b * 4 + 2] = wall_clock64();
+#endif
+}
+
+hipError_t launch_tcu(hipStream_t st, const TcArgs& a, const UpdArgs& u, const UpdWait& w, size_t lds_bytes) {
+  const int n_tc = a.block_start[kTcMaxJobs];
+  const int n_pad = (n_tc + 7) & ~7;                      // the update's blocks keep their b % 8 XCD groups
+  const int grid = n_pad + 8 * (u.per_xcd + u.per_xcd2);
+  hipLaunchKernelGGL(tcu_kernel, dim3(grid), dim3(TC_NW * 64), lds_bytes, st, a, u, w, n_tc, n_pad);
+  return hipGetLastError();
+}
+
 hipError_t launch_tc(hipStream_t st, const TcArgs& a, int rt, size_t lds_bytes) {
   const int nb = (a.xcd_slots > 0 ? 8 * a.xcd_slots : a.block_start[kTcMaxJobs]) + (a.bnd_block >= 0 ? 1 : 0);
   if (nb <= 0) return hipSuccess;
@@ -1270,7 +1321,8 @@ hipError_t launch_tc(hipStream_t st, const TcArgs& a, int rt, size_t lds_bytes) 
 }
 
 hipError_t tc_setup_attributes() {
-  const void* fns[] = {(const void*)tc_kernel<1>, (const void*)tc_kernel<2>, (const void*)tc_kernel<4>};
+  const void* fns[] = {(const void*)tc_kernel<1>, (const void*)tc_kernel<2>, (const void*)tc_kernel<4>,
+                       (const void*)tcu_kernel};
   for (const void* f : fns) {
     const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
@@ -1302,5 +1354,14 @@ extern "C" int iwae_tc_trace_dump(unsigned long long* out, int cap) {
   unsigned zero = 0;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(iwae::g_tc_trace_n), &zero, sizeof(zero));
   return m;
+}
+#endif
+
+#ifdef IWAE_TCU_TRACE
+extern "C" int iwae_tcu_trace_dump(unsigned long long* out, int cap) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  const int n = 512 * 4 < cap ? 512 * 4 : cap;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(iwae::g_tcu_trace), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+  return n;
 }
 #endif

@@ -356,3 +356,37 @@ def test_piwae_one_unit_chain_matches_two_chains(B, k1, k2, arch, tune):
     assert na == nb - 1                       # one engine backward launch fewer
     assert np.linalg.norm(ga - gb) <= 1e-5 * np.linalg.norm(gb)
     assert np.abs(wa - wb).max() <= 1e-5
+
+
+@pytest.mark.parametrize("B,arch,loss", [(20, ARCH2, "IWAE"), (7, ARCH2, "IWAE"), (33, ARCH2, "IWAE"),
+                                         (20, ARCH1, "IWAE"), (20, ARCH2, "PIWAE"), (20, ARCH2, "CIWAE")],
+                         ids=["b20", "b7", "b33", "1L", "piwae", "ciwae"])
+def test_image_row_backward_and_update_in_one_launch_equal_two_launches(B, arch, loss):
+    """Job I' (the first encoder layer's image-row backward) and the fused
+    update as ONE launch (knob tcu, tcu_kernel: the update's first-layer tiles
+    wait in-launch for job I' through an agent-scope counter) against the two
+    launches: bit-identical losses, gradients and post-Adam weights over graph-
+    replayed Philox steps and an eager injected-noise step; the combined launch
+    ran (counter 9) and no in-launch wait gave up (counter 8)."""
+    from iwae_replication_project_amd import Adam, Flexible_Model
+    rng = np.random.default_rng(91 + B)
+    k = 64 if loss == "PIWAE" else 50
+    x = (rng.random((B, 784)) < 0.2).astype(np.float32)
+    nd = 2 if loss == "CIWAE" else 1
+    eps = [rng.standard_normal((k, B, d)).astype(np.float32) for _ in range(nd) for d in arch[2]]
+    kw = dict(k1=8, k2=8) if loss == "PIWAE" else dict(beta=0.5) if loss == "CIWAE" else {}
+    runs = []
+    for flag in (1, 0):
+        m = Flexible_Model(*arch, dataset_bias=None, loss_function=loss, k=k, seed=17, tuning={"tcu": flag}, **kw)
+        m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+        n0 = m._lib.iwae_debug_count(m._h, 9)
+        losses = [m.train_step(x)[loss] for _ in range(3)]
+        losses.append(m.train_step(x, eps=eps)[loss])
+        runs.append((np.asarray(losses, np.float32), _flat(m.get_gradients()), _flat(m.get_weights()),
+                     m._lib.iwae_debug_count(m._h, 9) - n0, m._lib.iwae_debug_count(m._h, 8)))
+    (la, ga, wa, na, fa), (lb, gb, wb, nb, fb) = runs
+    assert na > 0 and nb == 0, (na, nb)
+    assert fa == 0 and fb == 0
+    np.testing.assert_array_equal(la, lb)
+    np.testing.assert_array_equal(ga, gb)
+    np.testing.assert_array_equal(wa, wb)
