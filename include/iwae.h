@@ -150,8 +150,9 @@ enum iwae_knob {
                                       <= 16 (0: auto, ceil(B / 256)) */
   IWAE_KNOB_IMG_ROWS_BWD = 32,     /* image-row job I' (its backward): images per workgroup (0: auto) */
   IWAE_KNOB_X_DIRECT = 33,         /* 1: a large-batch engine step's input GEMM reads the caller's x (default); 0: staged copy */
-  IWAE_KNOB_TCU = 34               /* the first encoder layer's image-row backward (job I') and the fused update in one
+  IWAE_KNOB_TCU = 34,              /* the first encoder layer's image-row backward (job I') and the fused update in one
                                       launch, its tiles of that layer waiting in-launch for job I' (1) */
+  IWAE_KNOB_DW_WS = 35             /* DW_WIDE kernel: four multiplying and four staging waves per workgroup (0) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --

@@ -92,24 +92,27 @@ __device__ __forceinline__ dw_f32x4 dw_ld4(__amdgpu_buffer_rsrc_t r, unsigned of
 // one thread's pieces: role 0 none, 1 X, 2 dZ (wave-uniform per slot).  The
 // buffer resources cover the row chunk (rows past its end read 0) and are built
 // once; the per-lane offsets advance by one k step per request.
+template <int N = DW_TASKS>
 struct DwTask {
-  int role[DW_TASKS];                    // (wave-uniform)
-  __amdgpu_buffer_rsrc_t rs[DW_TASKS];   // the piece's matrix (X or dZ) over the chunk
-  unsigned ginc[DW_TASKS];               // bytes per k step (32 rows; wave-uniform)
-  unsigned goff[DW_TASKS];     // byte offset of the piece for the next request (past the width: >= kOOB,
-                               // which stays out of range however far it advances)
-  unsigned koff[DW_TASKS];     // byte offset of the row scale (dZ pieces) for the next request
-  int loff[DW_TASKS];          // LDS byte offset of the piece in the hi plane of its image
+  int role[N];                    // (wave-uniform)
+  __amdgpu_buffer_rsrc_t rs[N];   // the piece's matrix (X or dZ) over the chunk
+  unsigned ginc[N];               // bytes per k step (32 rows; wave-uniform)
+  unsigned goff[N];     // byte offset of the piece for the next request (past the width: >= kOOB,
+                        // which stays out of range however far it advances)
+  unsigned koff[N];     // byte offset of the row scale (dZ pieces) for the next request
+  int loff[N];          // LDS byte offset of the piece in the hi plane of its image
 };
+template <int N = DW_TASKS>
 struct DwSet {
-  dw_f32x4 v[DW_TASKS];
-  float k[DW_TASKS];
+  dw_f32x4 v[N];
+  float k[N];
 };
 
-__device__ __forceinline__ void dw_load(DwTask& T, __amdgpu_buffer_rsrc_t rk, DwSet& S) {
+template <int N>
+__device__ __forceinline__ void dw_load(DwTask<N>& T, __amdgpu_buffer_rsrc_t rk, DwSet<N>& S) {
   if (kDwAbl & 4) return;
 #pragma unroll
-  for (int u = 0; u < DW_TASKS; ++u) {
+  for (int u = 0; u < N; ++u) {
     S.v[u] = dw_ld4(T.rs[u], T.goff[u]);
     S.k[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rk, T.koff[u], 0, 0));
     if (kDwAbl & 1) continue;
@@ -119,7 +122,8 @@ __device__ __forceinline__ void dw_load(DwTask& T, __amdgpu_buffer_rsrc_t rk, Dw
 }
 
 // piece u of the set -> bf16 hi / lo, row-major into image `img`
-__device__ __forceinline__ void dw_store1(const DwTask& T, const DwSet& S, unsigned char* img, int u) {
+template <int N>
+__device__ __forceinline__ void dw_store1(const DwTask<N>& T, const DwSet<N>& S, unsigned char* img, int u) {
   if (kDwAbl & 8) return;
   {
     if (T.role[u] == 0) return;                           // (wave-uniform; no load inside)
@@ -136,9 +140,10 @@ __device__ __forceinline__ void dw_store1(const DwTask& T, const DwSet& S, unsig
     *reinterpret_cast<dw_u32x2*>(img + T.loff[u] + (T.role[u] == 2 ? DW_ZP : DW_XP)) = dw_u32x2{la, lb};
   }
 }
-__device__ __forceinline__ void dw_store(const DwTask& T, const DwSet& S, unsigned char* img) {
+template <int N>
+__device__ __forceinline__ void dw_store(const DwTask<N>& T, const DwSet<N>& S, unsigned char* img) {
 #pragma unroll
-  for (int u = 0; u < DW_TASKS; ++u) dw_store1(T, S, img, u);
+  for (int u = 0; u < N; ++u) dw_store1(T, S, img, u);
 }
 
 // fragment of a 16-column tile from the plane at `pl`: two transposed reads at
@@ -169,7 +174,7 @@ __device__ __forceinline__ dw_bf16x8 dw_frag(int pl, unsigned o0, unsigned o1) {
 // wj + 4 h, stream i-tiles wi + 2 s.  Slots past the block read image columns
 // that exist (X <= 223 of 256, dZ <= 255 of 256): every read is unconditional.
 template <bool WIDE>
-__device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask& T, __amdgpu_buffer_rsrc_t rk, unsigned lbase,
+__device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask<>& T, __amdgpu_buffer_rsrc_t rk, unsigned lbase,
                                           int w, int lane, int i0, int j0, int mtb, int ntb, int s, int nk) {
   constexpr int WJ = WIDE ? 2 : 4, NS = WIDE ? 8 : 7;
   const int wi = w / WJ, wj = w % WJ;
@@ -203,7 +208,7 @@ __device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask& T, __amdgpu_bu
   // piece q is split and written after stream slot q's MFMAs are issued (the
   // VALU and LDS writes overlap the matrix core; a separate staging phase
   // after the multiply left them serialized behind the barrier)
-  auto mul = [&](int img, const DwSet& Sn, unsigned char* wimg) __attribute__((always_inline)) {
+  auto mul = [&](int img, const DwSet<>& Sn, unsigned char* wimg) __attribute__((always_inline)) {
     const int xh = img, xl = img + DW_XP, zh = img + 2 * DW_XP, zl = zh + DW_ZP;
     const int sh_p = WIDE ? zh : xh, sl_p = WIDE ? zl : xl, hh_p = WIDE ? xh : zh, hl_p = WIDE ? xl : zl;
     dw_bf16x8 hh[DW_NH], hl[DW_NH], sh[2], sl[2];
@@ -243,7 +248,7 @@ __device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask& T, __amdgpu_bu
 #pragma unroll
     for (int u = NS - 1; u < DW_TASKS; ++u) dw_store1(T, Sn, wimg, u);
   };
-  DwSet S0{}, S1{};
+  DwSet<> S0{}, S1{};
   if (nk > 0) {
     dw_load(T, rk, S0);
     dw_load(T, rk, S1);
@@ -259,7 +264,7 @@ __device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask& T, __amdgpu_bu
   if (tr) { g_dw_trace[blockIdx.x * kDwTr + 1] = nk; }
   int ks = 0;
 #endif
-  auto step = [&](int rimg, unsigned char* wimg, DwSet& Sn) __attribute__((always_inline)) {
+  auto step = [&](int rimg, unsigned char* wimg, DwSet<>& Sn) __attribute__((always_inline)) {
     mul(rimg, Sn, wimg);
 #ifdef IWAE_DW_TRACE
     if (ks < 80) DW_TR(3 + 3 * ks);
@@ -302,38 +307,18 @@ __device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask& T, __amdgpu_bu
   }
 }
 
-__global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
-  // item of this workgroup: consecutive items (one row chunk's blocks) on one XCD
-  const int bx = blockIdx.x, x = bx & 7, sl = bx >> 3;
-  const int item = x * a.per_xcd + sl;
-  if (sl >= a.per_xcd || item >= a.nitems) return;
-#ifdef IWAE_DW_TRACE
-  if (threadIdx.x == 0 && bx < 256) g_dw_trace[bx * kDwTr] = item;
-#endif
-  int jb = 0;
-  while (jb + 1 < a.njobs && item >= a.job[jb + 1].item0) ++jb;
-  const DwJob& J = a.job[jb];
-  int li = item - J.item0;
-  const int ib = li % J.nib;
-  li /= J.nib;
-  const int jbk = li % J.njb, s = li / J.njb;
-  const int i0 = 16 * J.mtb * ib, j0 = 16 * J.ntb * jbk;
-  const int mtb = min(J.mtb, J.mt - J.mtb * ib), ntb = min(J.ntb, J.nt - J.ntb * jbk);
-  const int rbase = s * J.chunk, rend = min(J.rows, rbase + J.chunk);
-  const int nk = (rend - rbase + DW_KR - 1) / DW_KR;
-  const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
-
-  // the thread's pieces: X quads per row nqx (16-multiple: a 16-lane write group
-  // stays on one row), then dZ quads nqz
+// The pieces of thread lt of nthr staging threads: X quads per row nqx
+// (16-multiple: a 16-lane write group stays on one row), then dZ quads nqz.
+template <int N>
+__device__ __forceinline__ void dw_tasks(const DwJob& J, DwTask<N>& T, int lt, int nthr, int i0, int j0, int mtb,
+                                         int ntb, int rbase, int rend) {
   const int nqx = (4 * mtb + 15) & ~15, nqz = (4 * ntb + 15) & ~15;
   const unsigned left = (unsigned)max(0, rend - rbase);
   const __amdgpu_buffer_rsrc_t rx = buf_rsrc(J.A + (size_t)rbase * J.lda, left * (unsigned)J.lda * 4u);
   const __amdgpu_buffer_rsrc_t rz = buf_rsrc(J.B + (size_t)rbase * J.ldb, left * (unsigned)J.ldb * 4u);
-  const __amdgpu_buffer_rsrc_t rk = buf_rsrc(J.ks + rbase, left * 4u);
-  DwTask T;
 #pragma unroll
-  for (int u = 0; u < DW_TASKS; ++u) {
-    const int tau = t + DW_NT * u;
+  for (int u = 0; u < N; ++u) {
+    const int tau = lt + nthr * u;
     const int role = __builtin_amdgcn_readfirstlane(tau < DW_KR * nqx ? 1 : tau < DW_KR * (nqx + nqz) ? 2 : 0);
     T.role[u] = role;
     T.rs[u] = role == 1 ? rx : rz;
@@ -359,8 +344,163 @@ __global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
     T.koff[u] = role == 2 ? (unsigned)row * 4u : kOOB;
     T.loff[u] = (role == 2 ? 2 * DW_XP : 0) + dw_off(row, c);
   }
+}
+
+// Warp-specialized blocks (DwArgs::ws): waves 0-3, one per SIMD, only
+// multiply -- 2 (i) x 2 (j) of them, each 7 x 4 tiles of a tall block (stream
+// i-tiles wi + 2 q, hold j-tiles wj + 2 h) or 4 x 8 of a wide one (hold
+// i-tiles wi + 2 h, stream j-tiles wj + 2 q) -- while waves 4-7 only load,
+// split and stage the next k steps.  Each SIMD then runs one multiplying and
+// one staging wave, so the staging's VALU work and LDS writes issue in the
+// MFMA gaps of the other wave instead of in its own instruction stream (the
+// 8-wave version's staging added ~0.8 us per k step on top of ~1.1 us of
+// MFMAs and fragment reads).  One barrier per k step for all eight waves.
+constexpr int DW_LT = 256;                      // staging threads
+constexpr int DW_TASKS_WS = 3072 / DW_LT;       // 16-byte pieces per staging thread and k step
+template <bool WIDE>
+__device__ __forceinline__ void dw_blocks_ws(const DwJob& J, __amdgpu_buffer_rsrc_t rk, unsigned lbase, int w,
+                                             int lane, int i0, int j0, int mtb, int ntb, int s, int nk, int rbase,
+                                             int rend) {
+  constexpr int NS = WIDE ? 8 : 7, NH = 4;
+  unsigned char* img0 = dws;
+  unsigned char* img1 = dws + DW_IMG;
+  if (w >= 4) {
+    // staging waves: step it's set is split into image it & 1 while step it - 1
+    // is multiplied; then step it + 2 is requested into the same set
+    DwTask<DW_TASKS_WS> T;
+    dw_tasks<DW_TASKS_WS>(J, T, (int)threadIdx.x - 256, DW_LT, i0, j0, mtb, ntb, rbase, rend);
+    DwSet<DW_TASKS_WS> S0{}, S1{};
+    dw_load(T, rk, S0);
+    dw_load(T, rk, S1);
+    dw_store(T, S0, img0);
+    dw_load(T, rk, S0);
+    __syncthreads();
+    for (int it = 0; it < nk; it += 2) {
+      __builtin_amdgcn_sched_barrier(0);
+      dw_store(T, S1, img1);
+      __builtin_amdgcn_sched_barrier(0);
+      dw_load(T, rk, S1);
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+      dw_store(T, S0, img0);
+      __builtin_amdgcn_sched_barrier(0);
+      dw_load(T, rk, S0);
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+    }
+    return;
+  }
+  const int wi = w >> 1, wj = w & 1;
+  auto st_tile = [&](int q) { return WIDE ? wj + 2 * q : wi + 2 * q; };
+  auto hd_tile = [&](int h) { return WIDE ? wi + 2 * h : wj + 2 * h; };
+  const int st_n = WIDE ? ntb : mtb, hd_n = WIDE ? mtb : ntb;
+  unsigned os[NS][2], oh[NH][2];
+#pragma unroll
+  for (int q = 0; q < NS; ++q)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) os[q][r] = lbase + dw_frag_off(st_tile(q), lane, r);
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) oh[h][r] = lbase + dw_frag_off(hd_tile(h), lane, r);
+  dw_f32x4 acc[NS][NH];
+#pragma unroll
+  for (int q = 0; q < NS; ++q)
+#pragma unroll
+    for (int h = 0; h < NH; ++h) acc[q][h] = dw_f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mul = [&](int img) __attribute__((always_inline)) {
+    const int xh = img, xl = img + DW_XP, zh = img + 2 * DW_XP, zl = zh + DW_ZP;
+    const int sh_p = WIDE ? zh : xh, sl_p = WIDE ? zl : xl, hh_p = WIDE ? xh : zh, hl_p = WIDE ? xl : zl;
+    dw_bf16x8 hh[NH], hl[NH], sh[2], sl[2];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      hh[h] = dw_frag(hh_p, oh[h][0], oh[h][1]);
+      hl[h] = dw_frag(hl_p, oh[h][0], oh[h][1]);
+    }
+    sh[0] = dw_frag(sh_p, os[0][0], os[0][1]);
+    sl[0] = dw_frag(sl_p, os[0][0], os[0][1]);
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      if (q + 1 < NS) {
+        sh[(q + 1) & 1] = dw_frag(sh_p, os[q + 1][0], os[q + 1][1]);
+        sl[(q + 1) & 1] = dw_frag(sl_p, os[q + 1][0], os[q + 1][1]);
+      }
+      if (!(kDwAbl & 2)) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+          const dw_bf16x8& ahi = WIDE ? hh[h] : sh[q & 1];
+          const dw_bf16x8& alo = WIDE ? hl[h] : sl[q & 1];
+          const dw_bf16x8& bhi = WIDE ? sh[q & 1] : hh[h];
+          const dw_bf16x8& blo = WIDE ? sl[q & 1] : hl[h];
+          acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi, acc[q][h], 0, 0, 0);
+          acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo, acc[q][h], 0, 0, 0);
+          acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi, acc[q][h], 0, 0, 0);
+        }
+      }
+    }
+  };
+  __syncthreads();
+  for (int it = 0; it < nk; it += 2) {
+    mul(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    mul(DW_IMG);
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+  }
+  float* out = J.out + (long long)s * J.slab_stride;
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    if (st_tile(q) >= st_n) continue;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      if (hd_tile(h) >= hd_n) continue;
+      const int ti = WIDE ? hd_tile(h) : st_tile(q), tj = WIDE ? st_tile(q) : hd_tile(h);
+      const int j = j0 + 16 * tj + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + 16 * ti + 4 * (lane >> 4) + r;
+        if (i < J.M && j < J.N) out[(long long)i * J.ldo + j] = acc[q][h][r];
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
+#ifdef IWAE_PS_DW     // experiment: one wave per SIMD (waves 0-3) at raised priority, so the SIMD's two waves drift apart
+  if ((threadIdx.x >> 6) < 4) __builtin_amdgcn_s_setprio(IWAE_PS_DW);
+#endif
+  // item of this workgroup: consecutive items (one row chunk's blocks) on one XCD
+  const int bx = blockIdx.x, x = bx & 7, sl = bx >> 3;
+  const int item = x * a.per_xcd + sl;
+  if (sl >= a.per_xcd || item >= a.nitems) return;
+#ifdef IWAE_DW_TRACE
+  if (threadIdx.x == 0 && bx < 256) g_dw_trace[bx * kDwTr] = item;
+#endif
+  int jb = 0;
+  while (jb + 1 < a.njobs && item >= a.job[jb + 1].item0) ++jb;
+  const DwJob& J = a.job[jb];
+  int li = item - J.item0;
+  const int ib = li % J.nib;
+  li /= J.nib;
+  const int jbk = li % J.njb, s = li / J.njb;
+  const int i0 = 16 * J.mtb * ib, j0 = 16 * J.ntb * jbk;
+  const int mtb = min(J.mtb, J.mt - J.mtb * ib), ntb = min(J.ntb, J.nt - J.ntb * jbk);
+  const int rbase = s * J.chunk, rend = min(J.rows, rbase + J.chunk);
+  const int nk = (rend - rbase + DW_KR - 1) / DW_KR;
+  const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
+
+  const unsigned left = (unsigned)max(0, rend - rbase);
+  const __amdgpu_buffer_rsrc_t rk = buf_rsrc(J.ks + rbase, left * 4u);
   typedef __attribute__((address_space(3))) unsigned char lds_u8;
   const unsigned lbase = (unsigned)(uintptr_t)(lds_u8*)dws;     // the first image's LDS address
+  if (a.ws) {
+    if (J.wide) dw_blocks_ws<true>(J, rk, lbase, w, lane, i0, j0, mtb, ntb, s, nk, rbase, rend);
+    else dw_blocks_ws<false>(J, rk, lbase, w, lane, i0, j0, mtb, ntb, s, nk, rbase, rend);
+    return;
+  }
+  DwTask<> T;
+  dw_tasks<DW_TASKS>(J, T, t, DW_NT, i0, j0, mtb, ntb, rbase, rend);
   if (J.wide) dw_blocks<true>(J, T, rk, lbase, w, lane, i0, j0, mtb, ntb, s, nk);
   else dw_blocks<false>(J, T, rk, lbase, w, lane, i0, j0, mtb, ntb, s, nk);
 }

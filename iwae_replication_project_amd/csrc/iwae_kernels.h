@@ -408,6 +408,7 @@ struct DwJob {
 constexpr int kDwMaxJobs = 20;
 struct DwArgs {
   DwJob job[kDwMaxJobs]; int njobs, nitems, per_xcd;
+  int ws;                                            // warp-specialized blocks (multiplying / staging waves)
 };
 hipError_t launch_dw(hipStream_t st, const DwArgs& a);
 hipError_t dw_setup_attributes();

@@ -213,6 +213,8 @@ struct iwae_handle {
   int img_rows_fwd = 0, img_rows_bwd = 0;   // image-row jobs I / I': rows per workgroup (0: auto)
   int x_direct = 1;                  // large-batch engine step: the input GEMM reads the caller's x (gemm_direct)
   int tcu = 1;                       // job I' and the fused update in one launch (tcu_kernel) where it fits
+  int dw_ws = 0;                     // dw_kernel: warp-specialized blocks (multiplying / staging waves; measured
+                                     // slower at B = 512: 0.447 vs 0.427 ms per step, so off)
   unsigned* tcu_ctr = nullptr;       // its in-launch counters (zero between launches; [2] spin give-ups)
   bool defer_launch = false;         // (during a step) tc_run / run_update record their launch instead
   bool pend_tc_have = false, pend_upd_have = false;
@@ -1729,6 +1731,7 @@ static int run_dw(iwae_handle* h, const Plan& P) {
   a.njobs = (int)js.size();
   a.nitems = items;
   a.per_xcd = (int)cdiv(items, 8);
+  a.ws = h->dw_ws;
   HIPCHK(launch_dw(h->stream, a));
   return IWAE_OK;
 }
@@ -2228,9 +2231,14 @@ static int finish_step(iwae_handle* h, const Plan& P, bool adam) {
 // The bound inside the engine's backward launch (no bound launch): up to 256
 // samples per image (an image's log weights staged per wave in the op buffers'
 // LDS, which must hold 8 of them plus the spare workgroup's 64 floats).
-static bool use_tc_bound(iwae_handle* h, const Plan& P) {
+static bool piwae_unit(const iwae_handle* h, const Plan& P, bool ring);
+// (PIWAE with the unit-weight chain: the launch's rows need no weighting, and
+// the spare workgroup writes both weightings, dlw / dpx and dlw2 / dpx2, for
+// the weight gradients and the image-row job)
+static bool use_tc_bound(iwae_handle* h, const Plan& P, bool ring) {
   // (one spare workgroup runs the whole bound: up to 64 images, 8 per wave)
-  if (!h->tc_bound || P.kS > 256 || P.Bimg > 64 || P.need_bce || P.kl || P.piwae || h->prof_kind == 13) return false;
+  if (!h->tc_bound || P.kS > 256 || P.Bimg > 64 || P.need_bce || P.kl || h->prof_kind == 13) return false;
+  if (P.piwae && !piwae_unit(h, P, ring)) return false;
   auto it = h->tc_plans.find(tc_key(P, 1));
   if (it == h->tc_plans.end()) return false;
   return (long long)it->second.acc_off >= 64 + 8LL * r4(P.kS);
@@ -2301,9 +2309,9 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   bool ring = false;
   if (!nring_train_forward(h, P, E, ring)) return fail(h, IWAE_EHIP, "weight-ring train forward launch failed");
   if (!ring) CHK(tc_run(h, P, E, 0));
-  if (use_tc_bound(h, P)) {
+  if (use_tc_bound(h, P, ring)) {
     const BoundArgs b = make_bound_args(h, P, true, -1.f, train_loss_ptr(h), adam, true);
-    CHK(tc_run(h, P, E, 1, &b));
+    CHK(tc_run(h, P, E, 1, &b, nullptr, nullptr, piwae_unit(h, P, ring)));
   } else {
     CHK(run_bound(h, P, true, -1.f, train_loss_ptr(h), adam, true));
     // the output MLP's backward on the weight ring where the forward ran on it,
@@ -3013,6 +3021,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_IMG_ROWS_BWD: h->img_rows_bwd = (int)std::max(0LL, std::min(value, 16LL)); break;
     case IWAE_KNOB_X_DIRECT: h->x_direct = on; break;
     case IWAE_KNOB_TCU: h->tcu = on; break;
+    case IWAE_KNOB_DW_WS: h->dw_ws = on; break;
     case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;

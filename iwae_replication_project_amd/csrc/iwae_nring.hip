@@ -721,6 +721,9 @@ constexpr int kNrNumShapes = sizeof(kNrShapes) / sizeof(kNrShapes[0]);
 // Bernoulli sum instead of log w.
 template <int SH, bool INJ, bool TR>
 __global__ __launch_bounds__(NR_W * 64, 1) void nring_kernel(NrLaunch A) {
+#ifdef IWAE_PS_NR     // experiment: one wave per SIMD (waves 0-3) at raised priority, so the SIMD's two waves drift apart
+  if ((threadIdx.x >> 6) < 4) __builtin_amdgcn_s_setprio(IWAE_PS_NR);
+#endif
   constexpr NrShapeDef P = kNrShapes[SH];
   constexpr bool L2 = P.L == 2;
   constexpr int H1 = P.H1;
@@ -1156,6 +1159,9 @@ __device__ __forceinline__ void nrb_mma_tiles(const __bf16* slot, const nr_bf16x
 
 template <int SH>
 __global__ __launch_bounds__(NR_W * 64, 1) void nrb_kernel(NrbLaunch A) {
+#ifdef IWAE_PS_NRB     // experiment: one wave per SIMD (waves 0-3) at raised priority, so the SIMD's two waves drift apart
+  if ((threadIdx.x >> 6) < 4) __builtin_amdgcn_s_setprio(IWAE_PS_NRB);
+#endif
   constexpr NrbShapeDef P = kNrbShapes[SH];
   using CN = NrbCount<SH>;
   constexpr int U2 = CN::U2, U1 = CN::U1;
@@ -1597,6 +1603,9 @@ __device__ __forceinline__ void nre_touch(float4 (&yv)[NT]) {
 }
 
 __global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
+#ifdef IWAE_PS_NRE     // experiment: one wave per SIMD (waves 0-3) at raised priority, so the SIMD's two waves drift apart
+  if ((threadIdx.x >> 6) < 4) __builtin_amdgcn_s_setprio(IWAE_PS_NRE);
+#endif
   constexpr NreShapeDef P = kNreShape;
   constexpr int NA = P.NTPH + P.NTP2 + P.NTP1;          // phase A's units
   static_assert(NA % NR_G == 0 && NA >= 2, "phase B starts a ring group");

@@ -1001,16 +1001,17 @@ __device__ __forceinline__ void tc_loadslab(CJob& J, COp& S, int row0, int nrows
 // added in fixed order through LDS scratch (S.in_buf's planes, [nsg][nq][8]
 // floats; deterministic).  dP0 goes to out_buf (natural order,
 // zeros to next_k) and S.out.
-template <int RT>
-__device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int row0, int nrows) {
-  constexpr int SPT = 2;
+template <int RT, int SPT, int IPP>
+__device__ __forceinline__ void tc_gbwd0_p(const TcArgs& A, CJob& J, COp& S, int row0, int nrows) {
   const int d = S.d, kS = A.kS;
-  // 32 column quads (16 sample groups) up to d = 128 (measured: one batch of
-  // every sample at d / 4 quads was no faster at k = 50), d / 4 beyond
-  const int nq = max(32, (d + 3) >> 2), nsg = (TC_NW * 64) / nq;   // (d <= 2048: nsg >= 1)
-  const int t = threadIdx.x, sg = t / nq, qi = t - sg * nq;
+  // 32 column quads up to d = 128 (measured: one batch of every sample at
+  // d / 4 quads was no faster at k = 50), d / 4 beyond; IPP images at once,
+  // TC_NW * 64 / IPP threads each
+  constexpr int TPI = (TC_NW * 64) / IPP;
+  const int nq = max(32, (d + 3) >> 2), nsg = TPI / nq;   // (d <= 2048 / IPP: nsg >= 1)
+  const int t = threadIdx.x, ii = t / TPI, tt = t - ii * TPI, sg = tt / nq, qi = tt - sg * nq;
   const TcBuf B = tc_buf<RT>(J, S.out_buf);
-  float* scr = reinterpret_cast<float*>(tc_buf<RT>(J, S.in_buf).hi);   // [nsg][nq][8] floats
+  float* scr = reinterpret_cast<float*>(tc_buf<RT>(J, S.in_buf).hi);   // [IPP][nsg][nq][8] floats
   const int padw = S.next_k - 2 * d;
   for (int e = t; e < 16 * RT * padw; e += TC_NW * 64) {
     const int r = e / padw, c = 2 * d + e % padw;
@@ -1023,9 +1024,10 @@ __device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int r
   for (int u = 0; u < NSRC; ++u) rsrc[u] = buf_rsrc(S.src[u]);
   const __amdgpu_buffer_rsrc_t rh = buf_rsrc(S.h), re = buf_rsrc(S.eps), rd = buf_rsrc(A.dlw);
   const int c0 = 4 * qi;
-  const bool live = sg < nsg && c0 < d;
-  for (int rr = 0; rr < nrows; ++rr) {
-    const int b = row0 + rr;
+  for (int r0 = 0; r0 < nrows; r0 += IPP) {
+    const int rr = r0 + ii;
+    const int b = row0 + min(rr, nrows - 1);
+    const bool live = rr < nrows && sg < nsg && c0 < d;
     const float* Pr = S.P + (size_t)b * S.ld_P;
     float mu[4], rs4[4];
 #pragma unroll
@@ -1067,7 +1069,7 @@ __device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int r
       }
     }
     if (live) {
-      float* my = scr + t * 8;                 // (sg * nq + qi) * 8
+      float* my = scr + ((ii * nsg + sg) * nq + qi) * 8;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         my[q] = dmu[q];
@@ -1075,20 +1077,40 @@ __device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int r
       }
     }
     tc_lds_barrier();
-    for (int e = t; e < nq * 8; e += TC_NW * 64) {
-      const int q = e >> 3, j = e & 7;         // quad q, value j (dmu 0..3, dscale 4..7)
+    for (int e = t; e < IPP * nq * 8; e += TC_NW * 64) {
+      const int i2 = e / (nq * 8), f = e - i2 * (nq * 8);
+      const int q = f >> 3, j = f & 7;         // quad q, value j (dmu 0..3, dscale 4..7)
+      const int r2 = r0 + i2;
+      if (r2 >= nrows) continue;
+      const int b2 = row0 + r2;
       float v = 0.f;
-      for (int g = 0; g < nsg; ++g) v += scr[(g * nq + q) * 8 + j];
+      for (int g = 0; g < nsg; ++g) v += scr[((i2 * nsg + g) * nq + q) * 8 + j];
       const int c = 4 * q + (j & 3);
       if (c < d) {
         const int col = j < 4 ? c : d + c;
-        if (j >= 4) v *= fexp(Pr[d + c]);      // dzs = dscale * exp(zs)
-        tc_put1(B, rr * B.ld + col, v);
-        S.out[(size_t)b * S.ld_out + col] = v;
+        if (j >= 4) v *= fexp(S.P[(size_t)b2 * S.ld_P + d + c]);      // dzs = dscale * exp(zs)
+        tc_put1(B, r2 * B.ld + col, v);
+        S.out[(size_t)b2 * S.ld_out + col] = v;
       }
     }
     tc_lds_barrier();
   }
+}
+
+// Image rows: dP0 = (dmu0 | dzs0) of the first encoder layer's head, the sum
+// over the image's kS sample rows of the h1 Gaussian backward (GBWD_ENC's
+// formula per sample; h1 was sampled from the image's (mu0, s0), F:58-F:60).
+// The threads work on IPP image rows at a time (two when the workgroup owns
+// two or more: the large-batch share's images are then summed side by side,
+// not one after the other); per image, thread (sample group sg, column quad
+// qi < nq = max(32, d / 4)) sums samples sg, sg + nsg, ... with SPT samples'
+// loads in flight, then the groups are added in fixed order through LDS
+// scratch (S.in_buf's planes, [IPP][nsg][nq][8] floats; deterministic).  dP0
+// goes to out_buf (natural order, zeros to next_k) and S.out.
+template <int RT>
+__device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int row0, int nrows) {
+  if (nrows >= 2 && S.d <= 128) tc_gbwd0_p<RT, 3, 2>(A, J, S, row0, nrows);
+  else tc_gbwd0_p<RT, 2, 1>(A, J, S, row0, nrows);
 }
 
 // ----------------------------------------------------------------- kernel
@@ -1260,6 +1282,9 @@ __device__ __forceinline__ void tc_body(const TcArgs& A, const int bid) {
 
 template <int RT>
 __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
+#ifdef IWAE_PS_TC     // experiment: one wave per SIMD (waves 0-3) at raised priority, so the SIMD's two waves drift apart
+  if ((threadIdx.x >> 6) < 4) __builtin_amdgcn_s_setprio(IWAE_PS_TC);
+#endif
   tc_body<RT>(A, (int)blockIdx.x);
 }
 

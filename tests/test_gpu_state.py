@@ -352,7 +352,9 @@ def test_piwae_one_unit_chain_matches_two_chains(B, k1, k2, arch, tune):
         return loss, _flat(m.get_gradients()), _flat(m.get_weights()), m._lib.iwae_debug_count(m._h, 2) - n0
     la, ga, wa, na = step(1)
     lb, gb, wb, nb = step(0)
-    assert la == lb
+    # (the unit chain computes the bound inside the backward launch, the two-chain
+    # step in bound_kernel: the same sums in another order)
+    assert abs(la - lb) <= 1e-6 * abs(lb)
     assert na == nb - 1                       # one engine backward launch fewer
     assert np.linalg.norm(ga - gb) <= 1e-5 * np.linalg.norm(gb)
     assert np.abs(wa - wb).max() <= 1e-5
@@ -390,3 +392,24 @@ def test_image_row_backward_and_update_in_one_launch_equal_two_launches(B, arch,
     np.testing.assert_array_equal(la, lb)
     np.testing.assert_array_equal(ga, gb)
     np.testing.assert_array_equal(wa, wb)
+
+
+@pytest.mark.parametrize("B", [100, 512])
+def test_dw_kernel_warp_specialized_equals_eight_wave_blocks(B):
+    """dw_kernel with four multiplying and four staging waves (knob dw_ws,
+    default) against the eight-wave blocks: the same products summed in the
+    same order, so losses, gradients and post-Adam weights agree bit for bit
+    over graph-replayed Philox steps and an injected-noise step."""
+    rng = np.random.default_rng(67 + B)
+    x = (rng.random((B, 784)) < 0.2).astype(np.float32)
+    eps = [rng.standard_normal((50, B, d)).astype(np.float32) for d in ARCH2[2]]
+    runs = []
+    for flag in (1, 0):
+        from iwae_replication_project_amd import Adam, Flexible_Model
+        m = Flexible_Model(*ARCH2, dataset_bias=None, loss_function="IWAE", k=50, seed=13, tuning={"dw_ws": flag})
+        m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+        losses = [m.train_step(x)["IWAE"] for _ in range(2)]
+        losses.append(m.train_step(x, eps=eps)["IWAE"])
+        runs.append((np.asarray(losses, np.float32), _flat(m.get_gradients()), _flat(m.get_weights())))
+    for a, b in zip(runs[0], runs[1]):
+        np.testing.assert_array_equal(a, b)
