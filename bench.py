@@ -111,6 +111,10 @@ def kernel_work(kind, rows, images):
     if kind == "img_fwd":      # job I: the first encoder layer's l2 and head on image rows (after its input Dense)
         return (2.0 * images * (200 * 200 + 200 * 200),
                 4.0 * (images * (200 + 200 + 200 + 200) + layer_params(["e1.l2", "e1.head"])))
+    if kind == "tcu":          # job I' and the fused update in one launch (tcu_kernel)
+        f1, b1 = kernel_work("img_bwd", rows, images)
+        f2, b2 = kernel_work("upd", rows, images)
+        return f1 + f2, b1 + b2
     if kind == "upd":          # every layer's dW + Adam (p, m, v read; p, m, v, g written) + FX / GX bf16 copies
         img_xz = images * (785 + 201 + 201 + 200 + 200 + 200)
         fl = 2.0 * (rows * layer_macs(ROW_LAYERS, bias=True) +
@@ -136,6 +140,7 @@ def roofline_of(flop, nbytes, us, peak_tflops=None, hbm_gbs=None):
 
 
 LB_RECORD = "r04_large_batch_kernels.json"     # the large-batch step's committed kernel record
+PMC_RECORD = "r04_pmc_traffic.json"            # the B = 20 step's committed per-launch HBM traffic (PMC)
 
 
 PRECISION = ("fp32 values and fp32 accumulation everywhere; every sample-row matrix product of the train step "
@@ -508,7 +513,8 @@ def main():
     rows_step = B_PER_GPU * K
     specs = {"tc_kernel forward (train engine, bf16x3)": (10, 0, "fwd"),
              "tc_kernel backward (train engine, bf16x3)": (11, 0, "bwd"),
-             "upd_kernel (weight gradients + Adam + FX copies, bf16x3)": (15, 0, "upd")}
+             "upd_kernel (weight gradients + Adam + FX copies, bf16x3)": (15, 0, "upd"),
+             "tcu_kernel (job I' + weight gradients + Adam + FX copies, one launch)": (16, 0, "tcu")}
     kern = {}
     for name, (kind, epi, wk) in specs.items():
         v = live(kind, epi)
@@ -524,7 +530,7 @@ def main():
     # HBM traffic of the same kernel: committed rocprofv3 PMC record (tools/pmc_passes.sh +
     # tools/pmc_to_json.py; FETCH_SIZE x2 per the gfx950 correction, WRITE_SIZE as is)
     traffic, traffic_src = None, None
-    pmc_name = "r04_pmc_traffic.json"
+    pmc_name = PMC_RECORD
     pmc = os.path.join(ROOT, "profiles", pmc_name)
     if os.path.exists(pmc):
         with open(pmc) as f:

@@ -152,7 +152,8 @@ enum iwae_knob {
   IWAE_KNOB_X_DIRECT = 33,         /* 1: a large-batch engine step's input GEMM reads the caller's x (default); 0: staged copy */
   IWAE_KNOB_TCU = 34,              /* the first encoder layer's image-row backward (job I') and the fused update in one
                                       launch, its tiles of that layer waiting in-launch for job I' (1) */
-  IWAE_KNOB_DW_WS = 35             /* DW_WIDE kernel: four multiplying and four staging waves per workgroup (0) */
+  IWAE_KNOB_UPD_APPLY = 35         /* beyond UPD_ROWS: the gradient pass's slabs summed, Adam and the FX / GX copies
+                                      in one update-kernel launch instead of the Adam and FX-refresh launches (1) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --
@@ -326,6 +327,8 @@ long long iwae_debug_count(const iwae_handle* h, int what);
  * train engine's forward (kind 10) / backward (kind 11) launch (epi ignored),
  * or a memory-bound launch of the train step: 12 Adam, 13 bound, 14 FX refresh
  * (replay only; their "FLOP" outputs are the launch's algorithmic HBM bytes);
+ * 15 the fused update launch, 16 the combined job I' + update launch
+ * (tcu_kernel; replay only, its FLOP output 0: the caller prices it);
  * kind = -1 disables.
  * Disables hipGraph replay while active.  iwae_profile_read synchronizes and
  * returns the summed kernel milliseconds, the algorithmic FLOPs of those

@@ -89,46 +89,61 @@ __device__ __forceinline__ dw_f32x4 dw_ld4(__amdgpu_buffer_rsrc_t r, unsigned of
   return __builtin_bit_cast(dw_f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
-// one thread's pieces: role 0 none, 1 X, 2 dZ (wave-uniform per slot).  The
-// buffer resources cover the row chunk (rows past its end read 0) and are built
-// once; the per-lane offsets advance by one k step per request.
+// one thread's pieces: role 0 none, 1 X, 2 dZ (wave-uniform per slot), at
+// fixed per-lane offsets within a k step (past the width: kOOB).  The k step
+// moves the buffer resources instead (DwSrc: base and range in scalar
+// registers), so a request costs no per-lane address arithmetic, and rows past
+// the chunk's end read 0.
 template <int N = DW_TASKS>
 struct DwTask {
-  int role[N];                    // (wave-uniform)
-  __amdgpu_buffer_rsrc_t rs[N];   // the piece's matrix (X or dZ) over the chunk
-  unsigned ginc[N];               // bytes per k step (32 rows; wave-uniform)
-  unsigned goff[N];     // byte offset of the piece for the next request (past the width: >= kOOB,
-                        // which stays out of range however far it advances)
-  unsigned koff[N];     // byte offset of the row scale (dZ pieces) for the next request
+  int role[N];          // (wave-uniform)
+  unsigned goff[N];     // byte offset of the piece within the k step's rows
+  unsigned koff[N];     // byte offset of the row scale (dZ pieces; X: kOOB)
   int loff[N];          // LDS byte offset of the piece in the hi plane of its image
 };
+// the next k step's rows of X, dZ and the row scale (wave-uniform)
+struct DwSrc {
+  const char* x; const char* z; const char* k;
+  long long xl, zl, kl;          // bytes left from x / z / k to the chunk's end
+  unsigned xs, zs;               // bytes per k step (32 rows)
+};
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dw_rsrc(const char* p, long long left) {
+  return buf_rsrc(p, left > 0 ? (unsigned)left : 0u);
+}
 template <int N = DW_TASKS>
 struct DwSet {
   dw_f32x4 v[N];
   float k[N];
 };
 
-template <int N>
-__device__ __forceinline__ void dw_load(DwTask<N>& T, __amdgpu_buffer_rsrc_t rk, DwSet<N>& S) {
+// one k step's pieces into S, then the sources move one k step on.  SCALE:
+// the job's dZ has a row scale (dpx of the output layer; others read none)
+template <int N, bool SCALE>
+__device__ __forceinline__ void dw_load(const DwTask<N>& T, DwSrc& R, DwSet<N>& S) {
   if (kDwAbl & 4) return;
+  const __amdgpu_buffer_rsrc_t rx = dw_rsrc(R.x, R.xl), rz = dw_rsrc(R.z, R.zl);
 #pragma unroll
-  for (int u = 0; u < N; ++u) {
-    S.v[u] = dw_ld4(T.rs[u], T.goff[u]);
-    S.k[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rk, T.koff[u], 0, 0));
-    if (kDwAbl & 1) continue;
-    T.goff[u] += T.ginc[u];                 // (an out-of-range offset stays out of range: kOOB + steps < 2^32)
-    T.koff[u] += DW_KR * 4u;
+  for (int u = 0; u < N; ++u) S.v[u] = dw_ld4(T.role[u] == 1 ? rx : rz, T.goff[u]);
+  if constexpr (SCALE) {
+    const __amdgpu_buffer_rsrc_t rk = dw_rsrc(R.k, R.kl);
+#pragma unroll
+    for (int u = 0; u < N; ++u) S.k[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rk, T.koff[u], 0, 0));
   }
+  if (kDwAbl & 1) return;
+  R.x += R.xs; R.xl -= R.xs;
+  R.z += R.zs; R.zl -= R.zs;
+  R.k += DW_KR * 4; R.kl -= DW_KR * 4;
 }
 
 // piece u of the set -> bf16 hi / lo, row-major into image `img`
-template <int N>
+template <bool SCALE, int N>
 __device__ __forceinline__ void dw_store1(const DwTask<N>& T, const DwSet<N>& S, unsigned char* img, int u) {
   if (kDwAbl & 8) return;
   {
     if (T.role[u] == 0) return;                           // (wave-uniform; no load inside)
     // dZ times its row scale (X: the scale's load read 0, times 1)
-    const dw_f32x4 v = S.v[u] * (S.k[u] + (T.role[u] == 2 ? 0.f : 1.f));
+    dw_f32x4 v = S.v[u];
+    if constexpr (SCALE) v *= (S.k[u] + (T.role[u] == 2 ? 0.f : 1.f));
     const dw_f32x2 a = {v[0], v[1]}, b = {v[2], v[3]};
     const unsigned ha = __builtin_bit_cast(unsigned, __builtin_convertvector(a, dw_bf16x2));
     const unsigned hb = __builtin_bit_cast(unsigned, __builtin_convertvector(b, dw_bf16x2));
@@ -140,10 +155,10 @@ __device__ __forceinline__ void dw_store1(const DwTask<N>& T, const DwSet<N>& S,
     *reinterpret_cast<dw_u32x2*>(img + T.loff[u] + (T.role[u] == 2 ? DW_ZP : DW_XP)) = dw_u32x2{la, lb};
   }
 }
-template <int N>
+template <bool SCALE, int N>
 __device__ __forceinline__ void dw_store(const DwTask<N>& T, const DwSet<N>& S, unsigned char* img) {
 #pragma unroll
-  for (int u = 0; u < N; ++u) dw_store1(T, S, img, u);
+  for (int u = 0; u < N; ++u) dw_store1<SCALE>(T, S, img, u);
 }
 
 // fragment of a 16-column tile from the plane at `pl`: two transposed reads at
@@ -173,8 +188,8 @@ __device__ __forceinline__ dw_bf16x8 dw_frag(int pl, unsigned o0, unsigned o1) {
 // (j), hold i-tiles wi + 4 h, stream j-tiles wj + 2 s; else 2 x 4, hold j-tiles
 // wj + 4 h, stream i-tiles wi + 2 s.  Slots past the block read image columns
 // that exist (X <= 223 of 256, dZ <= 255 of 256): every read is unconditional.
-template <bool WIDE>
-__device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask<>& T, __amdgpu_buffer_rsrc_t rk, unsigned lbase,
+template <bool WIDE, bool SCALE>
+__device__ __forceinline__ void dw_blocks(const DwJob& J, const DwTask<>& T, DwSrc& R, unsigned lbase,
                                           int w, int lane, int i0, int j0, int mtb, int ntb, int s, int nk) {
   constexpr int WJ = WIDE ? 2 : 4, NS = WIDE ? 8 : 7;
   const int wi = w / WJ, wj = w % WJ;
@@ -243,17 +258,17 @@ __device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask<>& T, __amdgpu_
           }
         }
       }
-      if (q >= 1 && q - 1 < DW_TASKS) dw_store1(T, Sn, wimg, q - 1);
+      if (q >= 1 && q - 1 < DW_TASKS) dw_store1<SCALE>(T, Sn, wimg, q - 1);
     }
 #pragma unroll
-    for (int u = NS - 1; u < DW_TASKS; ++u) dw_store1(T, Sn, wimg, u);
+    for (int u = NS - 1; u < DW_TASKS; ++u) dw_store1<SCALE>(T, Sn, wimg, u);
   };
   DwSet<> S0{}, S1{};
   if (nk > 0) {
-    dw_load(T, rk, S0);
-    dw_load(T, rk, S1);
-    dw_store(T, S0, img0);
-    dw_load(T, rk, S0);
+    dw_load<DW_TASKS, SCALE>(T, R, S0);
+    dw_load<DW_TASKS, SCALE>(T, R, S1);
+    dw_store<SCALE>(T, S0, img0);
+    dw_load<DW_TASKS, SCALE>(T, R, S0);
     __syncthreads();
   }
   // (every step unconditional, the step count rounded up to even: a step past
@@ -270,7 +285,7 @@ __device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask<>& T, __amdgpu_
     if (ks < 80) DW_TR(3 + 3 * ks);
 #endif
     __builtin_amdgcn_sched_barrier(0);
-    dw_load(T, rk, Sn);
+    dw_load<DW_TASKS, SCALE>(T, R, Sn);
     __builtin_amdgcn_sched_barrier(0);
 #ifdef IWAE_DW_TRACE
     if (ks < 80) DW_TR(4 + 3 * ks);
@@ -311,158 +326,29 @@ __device__ __forceinline__ void dw_blocks(const DwJob& J, DwTask<>& T, __amdgpu_
 // (16-multiple: a 16-lane write group stays on one row), then dZ quads nqz.
 template <int N>
 __device__ __forceinline__ void dw_tasks(const DwJob& J, DwTask<N>& T, int lt, int nthr, int i0, int j0, int mtb,
-                                         int ntb, int rbase, int rend) {
+                                         int ntb) {
   const int nqx = (4 * mtb + 15) & ~15, nqz = (4 * ntb + 15) & ~15;
-  const unsigned left = (unsigned)max(0, rend - rbase);
-  const __amdgpu_buffer_rsrc_t rx = buf_rsrc(J.A + (size_t)rbase * J.lda, left * (unsigned)J.lda * 4u);
-  const __amdgpu_buffer_rsrc_t rz = buf_rsrc(J.B + (size_t)rbase * J.ldb, left * (unsigned)J.ldb * 4u);
 #pragma unroll
   for (int u = 0; u < N; ++u) {
     const int tau = lt + nthr * u;
     const int role = __builtin_amdgcn_readfirstlane(tau < DW_KR * nqx ? 1 : tau < DW_KR * (nqx + nqz) ? 2 : 0);
     T.role[u] = role;
-    T.rs[u] = role == 1 ? rx : rz;
     int row = 0, c = 0;
     bool ok = false;
-    // (an out-of-range piece starts at kOOB: after at most ~900 k steps of <= 100 KB
-    // it is still below 2^32 and above any buffer range)
     if (role == 1) {
       row = tau / nqx; c = 4 * (tau - row * nqx);
       ok = i0 + c < J.M;
       T.goff[u] = ok ? (unsigned)(row * J.lda + i0 + c) * 4u : kOOB;
-      T.ginc[u] = (unsigned)(DW_KR * J.lda) * 4u;
     } else if (role == 2) {
       const int tz = tau - DW_KR * nqx;
       row = tz / nqz; c = 4 * (tz - row * nqz);
       ok = j0 + c < J.N;
       T.goff[u] = ok ? (unsigned)(row * J.ldb + j0 + c) * 4u : kOOB;
-      T.ginc[u] = (unsigned)(DW_KR * J.ldb) * 4u;
     } else {
       T.goff[u] = kOOB;
-      T.ginc[u] = 0u;
     }
     T.koff[u] = role == 2 ? (unsigned)row * 4u : kOOB;
     T.loff[u] = (role == 2 ? 2 * DW_XP : 0) + dw_off(row, c);
-  }
-}
-
-// Warp-specialized blocks (DwArgs::ws): waves 0-3, one per SIMD, only
-// multiply -- 2 (i) x 2 (j) of them, each 7 x 4 tiles of a tall block (stream
-// i-tiles wi + 2 q, hold j-tiles wj + 2 h) or 4 x 8 of a wide one (hold
-// i-tiles wi + 2 h, stream j-tiles wj + 2 q) -- while waves 4-7 only load,
-// split and stage the next k steps.  Each SIMD then runs one multiplying and
-// one staging wave, so the staging's VALU work and LDS writes issue in the
-// MFMA gaps of the other wave instead of in its own instruction stream (the
-// 8-wave version's staging added ~0.8 us per k step on top of ~1.1 us of
-// MFMAs and fragment reads).  One barrier per k step for all eight waves.
-constexpr int DW_LT = 256;                      // staging threads
-constexpr int DW_TASKS_WS = 3072 / DW_LT;       // 16-byte pieces per staging thread and k step
-template <bool WIDE>
-__device__ __forceinline__ void dw_blocks_ws(const DwJob& J, __amdgpu_buffer_rsrc_t rk, unsigned lbase, int w,
-                                             int lane, int i0, int j0, int mtb, int ntb, int s, int nk, int rbase,
-                                             int rend) {
-  constexpr int NS = WIDE ? 8 : 7, NH = 4;
-  unsigned char* img0 = dws;
-  unsigned char* img1 = dws + DW_IMG;
-  if (w >= 4) {
-    // staging waves: step it's set is split into image it & 1 while step it - 1
-    // is multiplied; then step it + 2 is requested into the same set
-    DwTask<DW_TASKS_WS> T;
-    dw_tasks<DW_TASKS_WS>(J, T, (int)threadIdx.x - 256, DW_LT, i0, j0, mtb, ntb, rbase, rend);
-    DwSet<DW_TASKS_WS> S0{}, S1{};
-    dw_load(T, rk, S0);
-    dw_load(T, rk, S1);
-    dw_store(T, S0, img0);
-    dw_load(T, rk, S0);
-    __syncthreads();
-    for (int it = 0; it < nk; it += 2) {
-      __builtin_amdgcn_sched_barrier(0);
-      dw_store(T, S1, img1);
-      __builtin_amdgcn_sched_barrier(0);
-      dw_load(T, rk, S1);
-      __builtin_amdgcn_sched_barrier(0);
-      __syncthreads();
-      dw_store(T, S0, img0);
-      __builtin_amdgcn_sched_barrier(0);
-      dw_load(T, rk, S0);
-      __builtin_amdgcn_sched_barrier(0);
-      __syncthreads();
-    }
-    return;
-  }
-  const int wi = w >> 1, wj = w & 1;
-  auto st_tile = [&](int q) { return WIDE ? wj + 2 * q : wi + 2 * q; };
-  auto hd_tile = [&](int h) { return WIDE ? wi + 2 * h : wj + 2 * h; };
-  const int st_n = WIDE ? ntb : mtb, hd_n = WIDE ? mtb : ntb;
-  unsigned os[NS][2], oh[NH][2];
-#pragma unroll
-  for (int q = 0; q < NS; ++q)
-#pragma unroll
-    for (int r = 0; r < 2; ++r) os[q][r] = lbase + dw_frag_off(st_tile(q), lane, r);
-#pragma unroll
-  for (int h = 0; h < NH; ++h)
-#pragma unroll
-    for (int r = 0; r < 2; ++r) oh[h][r] = lbase + dw_frag_off(hd_tile(h), lane, r);
-  dw_f32x4 acc[NS][NH];
-#pragma unroll
-  for (int q = 0; q < NS; ++q)
-#pragma unroll
-    for (int h = 0; h < NH; ++h) acc[q][h] = dw_f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mul = [&](int img) __attribute__((always_inline)) {
-    const int xh = img, xl = img + DW_XP, zh = img + 2 * DW_XP, zl = zh + DW_ZP;
-    const int sh_p = WIDE ? zh : xh, sl_p = WIDE ? zl : xl, hh_p = WIDE ? xh : zh, hl_p = WIDE ? xl : zl;
-    dw_bf16x8 hh[NH], hl[NH], sh[2], sl[2];
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-      hh[h] = dw_frag(hh_p, oh[h][0], oh[h][1]);
-      hl[h] = dw_frag(hl_p, oh[h][0], oh[h][1]);
-    }
-    sh[0] = dw_frag(sh_p, os[0][0], os[0][1]);
-    sl[0] = dw_frag(sl_p, os[0][0], os[0][1]);
-#pragma unroll
-    for (int q = 0; q < NS; ++q) {
-      if (q + 1 < NS) {
-        sh[(q + 1) & 1] = dw_frag(sh_p, os[q + 1][0], os[q + 1][1]);
-        sl[(q + 1) & 1] = dw_frag(sl_p, os[q + 1][0], os[q + 1][1]);
-      }
-      if (!(kDwAbl & 2)) {
-#pragma unroll
-        for (int h = 0; h < NH; ++h) {
-          const dw_bf16x8& ahi = WIDE ? hh[h] : sh[q & 1];
-          const dw_bf16x8& alo = WIDE ? hl[h] : sl[q & 1];
-          const dw_bf16x8& bhi = WIDE ? sh[q & 1] : hh[h];
-          const dw_bf16x8& blo = WIDE ? sl[q & 1] : hl[h];
-          acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi, acc[q][h], 0, 0, 0);
-          acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo, acc[q][h], 0, 0, 0);
-          acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi, acc[q][h], 0, 0, 0);
-        }
-      }
-    }
-  };
-  __syncthreads();
-  for (int it = 0; it < nk; it += 2) {
-    mul(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
-    mul(DW_IMG);
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
-  }
-  float* out = J.out + (long long)s * J.slab_stride;
-#pragma unroll
-  for (int q = 0; q < NS; ++q) {
-    if (st_tile(q) >= st_n) continue;
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-      if (hd_tile(h) >= hd_n) continue;
-      const int ti = WIDE ? hd_tile(h) : st_tile(q), tj = WIDE ? st_tile(q) : hd_tile(h);
-      const int j = j0 + 16 * tj + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = i0 + 16 * ti + 4 * (lane >> 4) + r;
-        if (i < J.M && j < J.N) out[(long long)i * J.ldo + j] = acc[q][h][r];
-      }
-    }
   }
 }
 
@@ -490,19 +376,24 @@ __global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
   const int nk = (rend - rbase + DW_KR - 1) / DW_KR;
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
 
-  const unsigned left = (unsigned)max(0, rend - rbase);
-  const __amdgpu_buffer_rsrc_t rk = buf_rsrc(J.ks + rbase, left * 4u);
+  const long long left = max(0, rend - rbase);
+  DwSrc R;
+  R.x = reinterpret_cast<const char*>(J.A + (size_t)rbase * J.lda);
+  R.z = reinterpret_cast<const char*>(J.B + (size_t)rbase * J.ldb);
+  R.k = reinterpret_cast<const char*>(J.ks + rbase);
+  R.xl = left * J.lda * 4; R.zl = left * J.ldb * 4; R.kl = left * 4;
+  R.xs = (unsigned)(DW_KR * J.lda) * 4u; R.zs = (unsigned)(DW_KR * J.ldb) * 4u;
   typedef __attribute__((address_space(3))) unsigned char lds_u8;
   const unsigned lbase = (unsigned)(uintptr_t)(lds_u8*)dws;     // the first image's LDS address
-  if (a.ws) {
-    if (J.wide) dw_blocks_ws<true>(J, rk, lbase, w, lane, i0, j0, mtb, ntb, s, nk, rbase, rend);
-    else dw_blocks_ws<false>(J, rk, lbase, w, lane, i0, j0, mtb, ntb, s, nk, rbase, rend);
-    return;
-  }
   DwTask<> T;
-  dw_tasks<DW_TASKS>(J, T, t, DW_NT, i0, j0, mtb, ntb, rbase, rend);
-  if (J.wide) dw_blocks<true>(J, T, rk, lbase, w, lane, i0, j0, mtb, ntb, s, nk);
-  else dw_blocks<false>(J, T, rk, lbase, w, lane, i0, j0, mtb, ntb, s, nk);
+  dw_tasks<DW_TASKS>(J, T, t, DW_NT, i0, j0, mtb, ntb);
+  if (J.scaled) {
+    if (J.wide) dw_blocks<true, true>(J, T, R, lbase, w, lane, i0, j0, mtb, ntb, s, nk);
+    else dw_blocks<false, true>(J, T, R, lbase, w, lane, i0, j0, mtb, ntb, s, nk);
+  } else {
+    if (J.wide) dw_blocks<true, false>(J, T, R, lbase, w, lane, i0, j0, mtb, ntb, s, nk);
+    else dw_blocks<false, false>(J, T, R, lbase, w, lane, i0, j0, mtb, ntb, s, nk);
+  }
 }
 
 #ifdef IWAE_DW_TRACE

@@ -364,6 +364,7 @@ struct UpdJob {
   // `chunk` rows, split s writes its partial W_aug tile at off + s * slab_stride
   // (the Adam launch sums the slabs); the job's tiles are then split-major
   int nsplit, chunk; long long slab_stride;
+  // (apply mode 2: B = the job's slab arena, chunk = its slab count, slab_stride between slabs)
 };
 constexpr int kUpdMaxJobs = 20, kUpdMaxTiles = 384;
 struct UpdArgs {
@@ -402,13 +403,13 @@ struct DwJob {
   int M, N, mt, nt;                                  // M = fin + 1, N = fout; 16-tiles along M / N
   int mtb, ntb, nib, njb;                            // tiles per block (<= 13 x 8, or wide: <= 8 x 16), blocks along M / N
   int wide;                                          // 1: wide blocks (waves 4 x 2)
+  int scaled;                                        // dZ rows carry a scale (ks: the output layer's dpx)
   int nsplit, chunk;                                 // row chunks (chunk % 32 == 0)
   int item0;                                         // first work item of the job (chunk-major, then N, then M block)
 };
 constexpr int kDwMaxJobs = 20;
 struct DwArgs {
   DwJob job[kDwMaxJobs]; int njobs, nitems, per_xcd;
-  int ws;                                            // warp-specialized blocks (multiplying / staging waves)
 };
 hipError_t launch_dw(hipStream_t st, const DwArgs& a);
 hipError_t dw_setup_attributes();

@@ -213,8 +213,7 @@ struct iwae_handle {
   int img_rows_fwd = 0, img_rows_bwd = 0;   // image-row jobs I / I': rows per workgroup (0: auto)
   int x_direct = 1;                  // large-batch engine step: the input GEMM reads the caller's x (gemm_direct)
   int tcu = 1;                       // job I' and the fused update in one launch (tcu_kernel) where it fits
-  int dw_ws = 0;                     // dw_kernel: warp-specialized blocks (multiplying / staging waves; measured
-                                     // slower at B = 512: 0.447 vs 0.427 ms per step, so off)
+  int upd_apply = 1;                 // large batches: the update kernel sums the slabs, Adam, FX / GX (one launch)
   unsigned* tcu_ctr = nullptr;       // its in-launch counters (zero between launches; [2] spin give-ups)
   bool defer_launch = false;         // (during a step) tc_run / run_update record their launch instead
   bool pend_tc_have = false, pend_upd_have = false;
@@ -1519,7 +1518,7 @@ static bool use_update_slabs(const iwae_handle* h, const Plan& P) {
 // buffer times 1 / *scale_dev.
 static int run_update(iwae_handle* h, const Plan& P, bool adam, int bucket = 0, hipStream_t st = nullptr,
                       float gscale = 1.f, float* tail = nullptr, bool slabs = false, bool apply = false,
-                      const float* scale_dev = nullptr) {
+                      const float* scale_dev = nullptr, bool from_slabs = false) {
   if (!st) st = h->stream;
   const int L = h->L, M = P.Bimg * P.kS;
   constexpr long long UP_ROWS_ITER = 128;      // rows per reduction iteration of the update kernel
@@ -1589,6 +1588,10 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int bucket = 0, 
       J.tiles_n = (int)cdiv(d.fout, 64);
       d.splits = (int)S;
     }
+    if (apply && from_slabs) {
+      // apply from the gradient pass's slabs: B, chunk, slab_stride name them
+      J.B = h->slabs + d.slab_off; J.chunk = d.splits; J.slab_stride = d.size();
+    }
     tiles += J.tiles_m * J.tiles_n * J.nsplit;
     if (!slabs) {
       if (tiles > kUpdMaxTiles) return fail(h, IWAE_EINVAL, "fused update: too many tiles");
@@ -1607,7 +1610,7 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int bucket = 0, 
   a.fx_hi = h->fx_hi; a.fx_lo = h->fx_lo;
   a.state = &h->ds->adam; a.do_adam = (adam || apply) && !slabs ? 1 : 0;
   a.gscale = slabs ? 1.f : gscale; a.tail = (slabs || apply) ? nullptr : tail; a.tail_val = gscale;
-  a.apply = apply ? 1 : 0; a.scale_dev = scale_dev;
+  a.apply = apply ? (from_slabs ? 2 : 1) : 0; a.scale_dev = scale_dev;
   a.waves = h->upd_waves;
   if (h->defer_launch && st == h->stream && !slabs && !apply) {
     // recorded for a combined launch (tcu_kernel) with job I': the first
@@ -1716,6 +1719,7 @@ static int run_dw(iwae_handle* h, const Plan& P) {
     DwJob& J = a.job[q];
     const float* ks = dz_scale(h, w.di, w.ks);
     J.A = w.A->p; J.lda = w.A->ld; J.B = w.dZ->p; J.ldb = w.dZ->ld; J.ks = ks ? ks : h->ones;
+    J.scaled = ks ? 1 : 0;                     // (unscaled dZ: no row-scale loads)
     J.rows = w.rows;
     J.out = h->slabs + d.slab_off; J.ldo = d.ldw; J.slab_stride = d.size();
     const double ksteps = (double)cdiv(w.rows, 32);
@@ -1731,7 +1735,6 @@ static int run_dw(iwae_handle* h, const Plan& P) {
   a.njobs = (int)js.size();
   a.nitems = items;
   a.per_xcd = (int)cdiv(items, 8);
-  a.ws = h->dw_ws;
   HIPCHK(launch_dw(h->stream, a));
   return IWAE_OK;
 }
@@ -2278,8 +2281,32 @@ static int launch_pending(iwae_handle* h) {
     if (ok) {
       UpdWait w;
       w.ctr = h->tcu_ctr; w.wait_mask = h->pend_upd_mask; w.n_prod = n_tc; w.n_cons = h->pend_upd_cons;
-      HIPCHK(launch_tcu(h->stream, a, u, w, std::max(h->pend_tc_lds, upd_lds_bytes())));
+      const size_t lds = std::max(h->pend_tc_lds, upd_lds_bytes());
+      HIPCHK(launch_tcu(h->stream, a, u, w, lds));
       h->n_tcu++;
+      if (h->prof_kind == 16 && !h->prof_have && u.do_adam) {
+        // live timing (iwae_profile_replay): replays repeat this launch with the
+        // update part on scratch copies of the parameters, moments and
+        // fragment-major copies (job I' rewrites its own outputs): the model is untouched
+        const size_t pb = (size_t)h->nparam_int * sizeof(float), fb = (size_t)h->fx_elems * 2 * sizeof(__bf16);
+        if (h->prof_adam_bytes < 3 * pb + fb) {
+          if (h->prof_adam) HIPCHK(hipFree(h->prof_adam));
+          h->prof_adam = nullptr;
+          HIPCHK(hipMalloc(&h->prof_adam, 3 * pb + fb));
+          h->prof_adam_bytes = 3 * pb + fb;
+        }
+        HIPCHK(hipMemcpyAsync(h->prof_adam, h->params, pb, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(hipMemcpyAsync(h->prof_adam + h->nparam_int, h->adam_m, pb, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(hipMemcpyAsync(h->prof_adam + 2 * h->nparam_int, h->adam_v, pb, hipMemcpyDeviceToDevice, h->stream));
+        UpdArgs r = u;
+        r.param = h->prof_adam; r.m = h->prof_adam + h->nparam_int; r.v = h->prof_adam + 2 * h->nparam_int;
+        r.fx_hi = reinterpret_cast<__bf16*>(h->prof_adam + 3 * h->nparam_int);
+        r.fx_lo = r.fx_hi + h->fx_elems;
+        const TcArgs ta = a;
+        h->prof_mem = [ta, r, w, lds](hipStream_t st) { return launch_tcu(st, ta, r, w, lds); };
+        h->prof_flop1 = 0.0;
+        h->prof_have = true;
+      }
       return IWAE_OK;
     }
   }
@@ -2368,7 +2395,8 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   const bool img_bwd = img || h->engine_img_bwd;
   // job I' and the fused update as one launch (tcu_kernel): recorded here,
   // issued by launch_pending below
-  const bool tcu = img_bwd && h->tcu && use_update(h, P) && !h->dp_weighted && h->prof_kind < 0 && !h->upd_tn32;
+  const bool tcu = img_bwd && h->tcu && use_update(h, P) && !h->dp_weighted && (h->prof_kind < 0 || h->prof_kind == 16) &&
+                   !h->upd_tn32;
   struct DeferReset {
     iwae_handle* h;
     ~DeferReset() { h->defer_launch = false; h->pend_tc_have = h->pend_upd_have = false; }
@@ -2427,6 +2455,13 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
         ncclSuccess)
       return fail(h, IWAE_EHIP, "ncclAllReduce of the gradient failed");
     CHK(run_update(h, P, true, 0, nullptr, 1.f, nullptr, false, true, tail));
+    h->fx_version = h->params_version;
+    return IWAE_OK;
+  }
+  if (adam && !h->dp_weighted && h->upd && h->upd_apply && upd_tiles_ok(h) && h->slabs) {
+    // the slabs summed, Adam and the fragment-major copies in one launch (the
+    // update kernel's apply mode) in place of adam_kernel + fx_refresh_kernel
+    CHK(run_update(h, P, true, 0, nullptr, 1.f, nullptr, false, true, nullptr, true));
     h->fx_version = h->params_version;
     return IWAE_OK;
   }
@@ -3021,7 +3056,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_IMG_ROWS_BWD: h->img_rows_bwd = (int)std::max(0LL, std::min(value, 16LL)); break;
     case IWAE_KNOB_X_DIRECT: h->x_direct = on; break;
     case IWAE_KNOB_TCU: h->tcu = on; break;
-    case IWAE_KNOB_DW_WS: h->dw_ws = on; break;
+    case IWAE_KNOB_UPD_APPLY: h->upd_apply = on; break;
     case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;
@@ -3923,7 +3958,7 @@ int iwae_profile_replay(iwae_handle* h, int n, double* total_ms, double* total_f
   HIPCHK(hipEventRecord(e0, h->stream));
   for (int i = 0; i < n; ++i) {
     if (h->prof_is_tc) HIPCHK(launch_tc(h->stream, h->prof_tc, h->prof_tc_rt, h->prof_tc_lds));
-    else if (h->prof_kind >= 12) HIPCHK(h->prof_mem(h->stream));
+    else if (h->prof_kind >= 12) HIPCHK(h->prof_mem(h->stream));     // (12-16: recorded closures)
     else HIPCHK(launch_gemm(h->stream, h->prof_k, h->prof_e, h->prof_tile, h->prof_splits, h->prof_ks, h->prof_args));
   }
   HIPCHK(hipEventRecord(e1, h->stream));

@@ -380,7 +380,30 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
 
   float g[EJ];
   float wsc = a.gscale;
-  if (a.apply) {
+  if (a.apply == 2) {
+    // the large-batch step: the tile's gradient is the sum of the gradient
+    // pass's split-K slabs (dw_kernel / the grouped GEMMs), in slab order like
+    // adam_kernel's, times the launch's scale; eight slabs' loads in flight
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(J.B);
+#pragma unroll
+    for (int q = 0; q < EJ / 4; ++q) {
+      const int c = j0 + ej + 4 * q;
+      const bool ok = erow && c < J.ldw;
+      const long long e0 = (long long)(i0 + ei) * J.ldw + c;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int s0 = 0; s0 < J.chunk; s0 += 8) {
+        float4 u[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          u[k] = bld4(rs, (ok && s0 + k < J.chunk) ? (unsigned)(((s0 + k) * J.slab_stride + e0) * 4) : kOOB);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { acc.x += u[k].x; acc.y += u[k].y; acc.z += u[k].z; acc.w += u[k].w; }
+      }
+      g[4 * q] = acc.x * a.gscale; g[4 * q + 1] = acc.y * a.gscale;
+      g[4 * q + 2] = acc.z * a.gscale; g[4 * q + 3] = acc.w * a.gscale;
+    }
+    wsc = 1.f;
+  } else if (a.apply) {
     // data parallel, after the all-reduce: the summed gradient of the tile's
     // elements times 1 / (sum of the ranks' batch sizes)
     const float sc = a.scale_dev ? 1.f / *a.scale_dev : a.gscale;

@@ -395,21 +395,24 @@ def test_image_row_backward_and_update_in_one_launch_equal_two_launches(B, arch,
 
 
 @pytest.mark.parametrize("B", [100, 512])
-def test_dw_kernel_warp_specialized_equals_eight_wave_blocks(B):
-    """dw_kernel with four multiplying and four staging waves (knob dw_ws,
-    default) against the eight-wave blocks: the same products summed in the
-    same order, so losses, gradients and post-Adam weights agree bit for bit
-    over graph-replayed Philox steps and an injected-noise step."""
-    rng = np.random.default_rng(67 + B)
+def test_slab_apply_update_equals_adam_and_fx_refresh_launches(B):
+    """Large batches: the gradient pass's split-K slabs summed, Keras Adam and
+    the fragment-major copies in ONE update-kernel launch (knob upd_apply,
+    apply mode 2) against adam_kernel + fx_refresh_kernel: the slabs are summed
+    in the same order and Adam is the same arithmetic, so losses, gradients
+    and weights agree bit for bit over graph-replayed Philox steps (whose
+    forwards read the refreshed copies) and an injected-noise step."""
+    from iwae_replication_project_amd import Adam, Flexible_Model
+    rng = np.random.default_rng(71 + B)
     x = (rng.random((B, 784)) < 0.2).astype(np.float32)
     eps = [rng.standard_normal((50, B, d)).astype(np.float32) for d in ARCH2[2]]
     runs = []
     for flag in (1, 0):
-        from iwae_replication_project_amd import Adam, Flexible_Model
-        m = Flexible_Model(*ARCH2, dataset_bias=None, loss_function="IWAE", k=50, seed=13, tuning={"dw_ws": flag})
+        m = Flexible_Model(*ARCH2, dataset_bias=None, loss_function="IWAE", k=50, seed=19, tuning={"upd_apply": flag})
         m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
-        losses = [m.train_step(x)["IWAE"] for _ in range(2)]
+        losses = [m.train_step(x)["IWAE"] for _ in range(3)]
         losses.append(m.train_step(x, eps=eps)["IWAE"])
-        runs.append((np.asarray(losses, np.float32), _flat(m.get_gradients()), _flat(m.get_weights())))
+        runs.append((np.asarray(losses, np.float32), _flat(m.get_gradients()), _flat(m.get_weights()),
+                     m.get_optimizer_state()[0]))
     for a, b in zip(runs[0], runs[1]):
         np.testing.assert_array_equal(a, b)

@@ -14,11 +14,11 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from iwae_replication_project_amd import Adam, Flexible_Model  # noqa: E402
 
-alpha = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+alpha = int(sys.argv[1]) if len(sys.argv) > 1 else 150
 B = 512
 x, pi = bench.synthetic_images(2 * B, 1)
 m = Flexible_Model(bench.HE, bench.HD, bench.LE, bench.LD, dataset_bias=pi, loss_function="IWAE", k=50, seed=2,
-                   tuning={"dw_wide": 1, "dw_alpha": alpha})
+                   tuning={"dw_wide": 1, "dw_alpha": alpha} if len(sys.argv) > 1 else {"dw_wide": 1})
 m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
 xd = m._x(x)
 for i in range(4):
@@ -47,3 +47,11 @@ for d, b, item, nk, mul, stg, bar in rows[:40]:
     print(f"wg {b:3d} item {item:3d} nk {nk:3d}  start {buf[b * K + 2] - tmin:6d}  dur {d:6d}  per-k {d / max(nk, 1):7.1f}"
           f"   mul {mul:6.1f} stage {stg:6.1f} barrier {bar:6.1f}")
 print(f"... {len(rows)} workgroups; shortest {rows[-1][0]}")
+# every workgroup, compact: duration (us), k steps, per-k (us) -- the balance of the cost model
+import collections
+d = sorted(((r[0] / 100.0, r[3], r[0] / 100.0 / max(r[3], 1)) for r in rows), reverse=True)
+print("all workgroups (us, k steps, us per k step):")
+print("  ".join(f"{a:.0f}/{b}/{c:.2f}" for a, b, c in d))
+hist = collections.Counter(int(a // 10) * 10 for a, _, _ in d)
+print("duration histogram (10 us bins):", dict(sorted(hist.items())))
+print(f"mean {sum(a for a, _, _ in d) / len(d):.1f} us, max {d[0][0]:.1f} us")
