@@ -152,8 +152,10 @@ enum iwae_knob {
   IWAE_KNOB_X_DIRECT = 33,         /* 1: a large-batch engine step's input GEMM reads the caller's x (default); 0: staged copy */
   IWAE_KNOB_TCU = 34,              /* the first encoder layer's image-row backward (job I') and the fused update in one
                                       launch, its tiles of that layer waiting in-launch for job I' (1) */
-  IWAE_KNOB_UPD_APPLY = 35         /* beyond UPD_ROWS: the gradient pass's slabs summed, Adam and the FX / GX copies
+  IWAE_KNOB_UPD_APPLY = 35,        /* beyond UPD_ROWS: the gradient pass's slabs summed, Adam and the FX / GX copies
                                       in one update-kernel launch instead of the Adam and FX-refresh launches (1) */
+  IWAE_KNOB_STEPS_FIRST = 36       /* iwae_train_steps: steps in a call's first captured graph, then up to 32 per
+                                      graph (0: 32 from the start) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --
@@ -198,13 +200,13 @@ int iwae_train_step(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
  * steps with device Philox noise on the batches x + i*B*x_dim, i < nsteps
  * (x [dev] holds nsteps*B images); loss_dev [dev, may be NULL] receives
  * nsteps losses.  Same arithmetic as nsteps iwae_train_step calls; with graphs
- * on, consecutive steps replay from one captured graph of up to 32 steps (no
- * launch gap between them). */
+ * on, consecutive steps replay from captured graphs of up to 32 steps (no
+ * launch gap between them; IWAE_KNOB_STEPS_FIRST > 0 shortens the first). */
 int iwae_train_steps(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B, int nsteps,
                      float* loss_dev);
 /* Capture, without launching anything, every graph an iwae_train_steps call
- * with these arguments would capture (the step counts min(32, nsteps) and
- * nsteps % 32), so that the call itself only replays; the parameters, Adam
+ * with these arguments would capture (its chunk lengths: up to 32 steps
+ * each, the first one IWAE_KNOB_STEPS_FIRST long when that is set), so that the call itself only replays; the parameters, Adam
  * state and noise position are untouched.  Data parallelism with the library
  * communicator included (each captured step carries its all-reduces). */
 int iwae_train_steps_prepare(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B, int nsteps);

@@ -214,6 +214,7 @@ struct iwae_handle {
   int x_direct = 1;                  // large-batch engine step: the input GEMM reads the caller's x (gemm_direct)
   int tcu = 1;                       // job I' and the fused update in one launch (tcu_kernel) where it fits
   int upd_apply = 1;                 // large batches: the update kernel sums the slabs, Adam, FX / GX (one launch)
+  int steps_first = 0;               // iwae_train_steps: length of a call's first graph (0: 32 like the rest)
   unsigned* tcu_ctr = nullptr;       // its in-launch counters (zero between launches; [2] spin give-ups)
   bool defer_launch = false;         // (during a step) tc_run / run_update record their launch instead
   bool pend_tc_have = false, pend_upd_have = false;
@@ -2755,8 +2756,11 @@ static int do_train_steps(iwae_handle* h, const iwae_loss_config* lc, const floa
       h->in_train_step = false; h->out_x3 = false; h->x_user = nullptr; h->capturing = false; h->loss_out = nullptr;
     }
   } reset_flag{h};
-  for (int i0 = 0; i0 < nsteps; i0 += kGraphSteps) {
-    const int S = std::min(kGraphSteps, nsteps - i0);
+  // steps_first > 0 makes the call's first graph short, so it reaches the GPU
+  // while the host issues the rest (measured: no change in the per-call fixed
+  // cost, profiles/r05r_steps_first.txt; off by default)
+  for (int i0 = 0, S = 0; i0 < nsteps; i0 += S) {
+    S = std::min(i0 == 0 && h->steps_first > 0 ? h->steps_first : kGraphSteps, nsteps - i0);
     const float* xi = x + i0 * xstride;
     iwae_handle::GraphRec* gp = nullptr;
     CHK(steps_graph(h, lc, P, E, B, S, xi, &gp));
@@ -3057,6 +3061,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_X_DIRECT: h->x_direct = on; break;
     case IWAE_KNOB_TCU: h->tcu = on; break;
     case IWAE_KNOB_UPD_APPLY: h->upd_apply = on; break;
+    case IWAE_KNOB_STEPS_FIRST: h->steps_first = (int)std::max(0LL, std::min(value, (long long)kGraphSteps)); break;
     case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;

@@ -254,9 +254,13 @@ __device__ __forceinline__ void nr_issue(const NrCtx& C, int slot, unsigned off,
 // vmcnt(0), because hipcc cannot tell them apart from the DMA-written slots.)
 template <bool TR, int G = nr_g<TR>()>
 __device__ __forceinline__ const __bf16* nr_next(NrCtx& C) {
-  // younger than a group's pieces at its wait: the pieces of the two groups
-  // requested after it and (TR) the stores of the three groups since
-  constexpr int NV = 2 * (NR_D - 2 * G) + (TR ? 3 * G * NR_SEPI : 0);
+  // younger than a group's pieces at its wait: the pieces of the NR_D / G - 2
+  // groups requested after it and (TR) the stores of the NR_D / G - 1 groups
+  // whose phases ran since it was requested, NR_SEPI per unit (G = 2: two and
+  // three groups; G = 4: none and one -- a count of three there, 48, never
+  // waited and let a late piece be read stale, tools/determinism_stress.py)
+  constexpr int NV = 2 * (NR_D - 2 * G) + (TR ? (NR_D - G) * NR_SEPI : 0);
+  static_assert(NR_D % G == 0 && NV >= 0 && NV < 64, "vmcnt");
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
   NR_TR(C.u, 0)
   if ((C.u & (G - 1)) == 0) {
@@ -383,11 +387,17 @@ __device__ __forceinline__ void nr_st2r(__amdgpu_buffer_rsrc_t r, unsigned off, 
   const u32x2 u = {__float_as_uint(a), __float_as_uint(b)};
   __builtin_amdgcn_raw_buffer_store_b64(u, r, off, 0, 0);
 }
-// n out-of-range stores: they count in vmcnt like the real ones
+// n out-of-range stores: they count in vmcnt like the real ones.  Inline asm:
+// as intrinsics (the same zero to the same dropped address) hipcc kept one of
+// every run of them, so a group issued 5-12 of its 16 (nre_kernel: 4 of 8)
+// and the counted waits let a late DMA piece be read stale (run-to-run
+// differences at B = 512; tests/test_nring_counts.py checks the issued counts)
 template <int NPAD>
-__device__ __forceinline__ void nr_st_pad(const NrRow& R) {
+__device__ __forceinline__ void nr_st_pad(const NrRow&) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const i32x4 rz = {0, 0, 0, 0x00020000};      // num_records 0: every store dropped
 #pragma unroll
-  for (int i = 0; i < NPAD; ++i) __builtin_amdgcn_raw_buffer_store_b32(0u, R.nul, kOOB, 0, 0);
+  for (int i = 0; i < NPAD; ++i) asm volatile("buffer_store_dword %0, off, %1, 0" ::"v"(0), "s"(rz));
 }
 
 // tanh Dense layer: OUT = [tanh(IN . W) | 1 | 0 ...] as the next layer's B

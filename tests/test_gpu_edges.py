@@ -262,10 +262,11 @@ def test_train_steps_equal_single_step_calls(B, n):
         assert runs[0][3] == r[3] == 2 * n
 
 
-@pytest.mark.parametrize("B,n", [(20, 20), (20, 45), (512, 3)])
-def test_prepared_train_steps_capture_nothing_more_and_equal_unprepared(B, n):
+@pytest.mark.parametrize("B,n,first", [(20, 20, 0), (20, 45, 0), (512, 3, 0), (20, 45, 2), (512, 3, 2)])
+def test_prepared_train_steps_capture_nothing_more_and_equal_unprepared(B, n, first):
     """iwae_train_steps_prepare captures the graphs of a later train_steps call
-    (one per step count: 45 = 32 + 13 gives two) without running anything:
+    (one per chunk length: 45 = 32 + 13 gives two; with a first graph of 2
+    steps, knob steps_first, 45 = 2 + 32 + 11 gives three) without running anything:
     weights, Adam step and an evaluation on injected noise are those of an
     unprepared model; the call then captures nothing (capture counter, id 7)
     and its losses, weights and Adam state equal the unprepared run bit for
@@ -277,13 +278,15 @@ def test_prepared_train_steps_capture_nothing_more_and_equal_unprepared(B, n):
     eps = [rng.standard_normal((5, 4, d)).astype(np.float32) for d in ARCH2[2]]
     runs = []
     for prep in (False, True):
-        m = _model(ARCH2, "IWAE", 50)
+        m = _model(ARCH2, "IWAE", 50, tuning={"steps_first": first})
         X = torch.from_numpy(xs).to(m.device)
         w0 = _flat(m.get_weights())
         if prep:
             c0 = m.graph_captures()
             m.prepare_train_steps(X, B)
-            assert m.graph_captures() - c0 == (2 if n > 32 and n % 32 else 1)
+            r = n - min(first, n)
+            lens = ({min(first, n)} if first else set()) | ({32} if r >= 32 else set()) | ({r % 32} if r % 32 else set())
+            assert m.graph_captures() - c0 == len(lens), (lens, m.graph_captures() - c0)
             np.testing.assert_array_equal(_flat(m.get_weights()), w0)
             assert m.get_optimizer_state()[2] == 0
         lw = m.get_log_weights(xe, 5, eps=eps).cpu().numpy()

@@ -416,3 +416,37 @@ def test_slab_apply_update_equals_adam_and_fx_refresh_launches(B):
                      m.get_optimizer_state()[0]))
     for a, b in zip(runs[0], runs[1]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("B", [512, 1000])
+def test_large_batch_training_is_run_to_run_bitwise_reproducible(B):
+    """Every launch of a train step is deterministic (fixed reduction orders,
+    no float atomics), so fresh models trained on the same batches and noise
+    agree bit for bit, step after step.  Run to run, a read that races its
+    producer sees whatever the buffer held before, which differs from step to
+    step: this caught the weight-ring train forward's counted wait allowing
+    one group's stores too many per group (no wait at all at 4 units per group,
+    a late LDS-DMA piece read stale; about 1 run in 10 at B = 512, 6 steps,
+    tools/determinism_stress.py).  Replaying one step from a fixed state does
+    not show such races: the stale bytes are that step's own."""
+    import torch
+    from iwae_replication_project_amd import Adam, Flexible_Model
+    steps = 6 if B == 512 else 4
+    rng = np.random.default_rng(7 + B)
+    xs = torch.from_numpy((rng.random((steps * B, 784)) < 0.3).astype(np.float32)).cuda()
+    base = None
+    for r in range(24 if B == 512 else 10):
+        m = Flexible_Model(*ARCH2, dataset_bias=None, loss_function="IWAE", k=50, seed=3)
+        m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+        out = []
+        for i in range(steps):
+            out.append(np.float32(m.train_step(xs[i * B:(i + 1) * B])["IWAE"]))
+            out.append(_flat(m.get_gradients()))
+        out.append(_flat(m.get_weights()))
+        del m
+        if base is None:
+            base = out
+            assert np.isfinite(np.asarray(out[0::2][:steps])).all()
+            continue
+        for j, (a, b) in enumerate(zip(base, out)):
+            np.testing.assert_array_equal(a, b, err_msg=f"run {r}, item {j} (step {j // 2})")

@@ -1,0 +1,134 @@
+"""The weight-ring kernels' counted waits, checked on the compiled code (CPU:
+hipcc cross-compiles iwae_nring.hip for gfx950 to assembly, nothing runs).
+
+nring_kernel and nre_kernel wait for a group's LDS-DMA pieces with a constant
+`s_waitcnt vmcnt(N)`, N = the vector memory operations the wave issues after
+those pieces (iwae_nring.hip nr_next); nrb_kernel does the same with its own
+per-group counts (NrbCount).  The count is only right if the compiled code
+issues exactly the operations the source does, on every path:
+
+* every group issues 2 pieces per unit and, in train mode, NR_SEPI stores per
+  unit, real or out-of-range padding.  hipcc once kept one of every run of
+  identical padding stores (same zero, same dropped address), so groups issued
+  5-12 of their 16 stores and the waits let a late piece be read stale: about 1
+  run in 10 of a B = 512 training run differed from the others
+  (tests/test_gpu_state.py::test_large_batch_training_is_run_to_run_bitwise_reproducible);
+* no vector memory operation issued while a piece is in flight sits in a
+  block that an `s_cbranch_execz` can skip (a wave with no active lanes there
+  would issue fewer).
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "iwae_replication_project_amd", "csrc", "iwae_nring.hip")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+NR_SEPI = 4
+# (kernel symbol prefix, DMA pieces per group, stores per group at least)
+TRAIN_RING = [
+    ("_ZN4iwae12nring_kernelILi0ELb0ELb1E", 8, 4 * NR_SEPI),   # 2L, Philox, train: 4 units per group
+    ("_ZN4iwae12nring_kernelILi0ELb1ELb1E", 8, 4 * NR_SEPI),   # 2L, injected noise, train
+    ("_ZN4iwae12nring_kernelILi1ELb0ELb1E", 8, 4 * NR_SEPI),   # 1L, Philox, train
+    ("_ZN4iwae12nring_kernelILi1ELb1ELb1E", 8, 4 * NR_SEPI),   # 1L, injected noise, train
+    ("_ZN4iwae10nre_kernel", 4, 2 * NR_SEPI),                   # encoder / prior backward: 2 units per group
+]
+VMEM = re.compile(r"^(buffer_|global_|scratch_|flat_)")
+
+
+@pytest.fixture(scope="module")
+def asm(tmp_path_factory):
+    if not os.path.exists(HIPCC) and not shutil.which("hipcc"):
+        pytest.skip("hipcc not available")
+    out = tmp_path_factory.mktemp("nring") / "nring.s"
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S", "-o", str(out),
+                    SRC], check=True, capture_output=True, timeout=600)
+    return out.read_text().split("\n")
+
+
+def _body(lines, prefix):
+    start = next(i for i, l in enumerate(lines) if l.split(":")[0] == prefix and ":" in l)
+    end = next(i for i in range(start + 1, len(lines)) if lines[i].strip().startswith(".Lfunc_end"))
+    return [l.split(";")[0].strip() for l in lines[start + 1:end]]
+
+
+def _labels(body):
+    return {l[:-1]: i for i, l in enumerate(body) if re.match(r"^\.LBB\w+:$", l)}
+
+
+def _group_segments(body):
+    """(wait index, vmcnt, ops between the previous group wait and this one)."""
+    segs, cur = [], []
+    for i, l in enumerate(body):
+        if VMEM.match(l):
+            cur.append((i, l))
+        m = re.match(r"s_waitcnt vmcnt\((\d+)\)$", l)
+        if m and body[i + 1].startswith("s_waitcnt lgkmcnt(0)") and body[i + 2].startswith("s_barrier"):
+            segs.append((i, int(m.group(1)), cur))
+            cur = []
+    return segs
+
+
+def _kernels(lines):
+    return sorted({m.group(1) for l in lines for m in [re.match(r"^(_ZN4iwae(?:12nring_kernel|10nre_kernel|10nrb_kernel)\w*):", l)]
+                   if m})
+
+
+def test_all_ring_kernels_found(asm):
+    names = _kernels(asm)
+    for prefix, _, _ in TRAIN_RING:
+        assert any(n.startswith(prefix) for n in names), (prefix, names)
+    assert any(n.startswith("_ZN4iwae10nrb_kernel") for n in names)
+
+
+def test_no_vector_memory_operation_in_an_execz_skippable_block(asm):
+    """(one that a counted wait relies on: issued while a DMA piece is in
+    flight, i.e. after a piece and no full drain, vmcnt(0), since)"""
+    for name in _kernels(asm):
+        body = _body(asm, name)
+        labels = _labels(body)
+        inflight, dma = [], False
+        for l in body:
+            if l.startswith("s_waitcnt vmcnt(0)"):
+                dma = False
+            inflight.append(dma)
+            if VMEM.match(l) and l.endswith(" lds"):
+                dma = True
+        for i, l in enumerate(body):
+            m = re.match(r"s_cbranch_execz (\.LBB\w+)$", l)
+            if not m or labels[m.group(1)] < i:
+                continue
+            skipped = [(j, x) for j, x in enumerate(body[i + 1:labels[m.group(1)]], i + 1) if VMEM.match(x) and inflight[j]]
+            assert not skipped, f"{name}: {l} at {i} can skip {skipped[:3]}"
+
+
+@pytest.mark.parametrize("prefix,pieces,stores", TRAIN_RING, ids=[p[0][6:30] for p in TRAIN_RING])
+def test_every_group_issues_its_pieces_and_stores(asm, prefix, pieces, stores):
+    name = next(n for n in _kernels(asm) if n.startswith(prefix))
+    body = _body(asm, name)
+    labels = _labels(body)
+    # loops (a branch back to an earlier label): the per-unit code of a stage
+    # not unrolled; its segments mix iterations, so only straight code is counted
+    back = [(labels[m.group(1)], i) for i, l in enumerate(body)
+            for m in [re.match(r"s_c?branch\w* (\.LBB\w+)$", l)] if m and labels[m.group(1)] < i]
+    segs = _group_segments(body)
+    assert len(segs) >= 8, f"{name}: {len(segs)} group waits"
+    counted = 0
+    prev = 0
+    for k, (i, vm, ops) in enumerate(segs):
+        lo = prev
+        prev = i
+        if k == 0 or segs[k - 1][1] == 0 or any(lo <= a <= i or lo <= b <= i for a, b in back):
+            continue      # a prologue (after the start or a full drain: its own pieces), or loop code
+        n_lds = sum(1 for _, l in ops if l.endswith(" lds"))
+        n_st = sum(1 for _, l in ops if "store" in l.split()[0])
+        n_other = len(ops) - n_lds - n_st
+        assert n_lds == pieces, f"{name}: group wait at {i}: {n_lds} DMA pieces, expected {pieces}"
+        assert n_st >= stores, f"{name}: group wait at {i} (vmcnt {vm}): {n_st} stores, expected {stores}"
+        assert n_other == 0, f"{name}: group wait at {i}: {n_other} other vector memory operations"
+        counted += 1
+    assert counted >= len(segs) // 2, (name, counted, len(segs))

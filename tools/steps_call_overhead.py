@@ -3,7 +3,7 @@ for n steps, the host time until the call returns and the time until its
 stream drained, graphs captured beforehand (iwae_train_steps_prepare).  The
 intercept of wall time over n is the per-call latency that a short timed
 region (the driver's --steps 20) pays once.
-    python tools/steps_call_overhead.py"""
+    python tools/steps_call_overhead.py [steps_first]"""
 import os
 import sys
 import time
@@ -16,7 +16,8 @@ from iwae_replication_project_amd import Adam, Flexible_Model
 rng = np.random.default_rng(0)
 pi = rng.uniform(0.02, 0.4, 784)
 m = Flexible_Model([200, 100], [100, 200], [100, 50], [100, 784], dataset_bias=pi, loss_function="IWAE", k=50,
-                   seed=2, use_graphs=True)
+                   seed=2, use_graphs=True,
+                   tuning={"steps_first": int(sys.argv[1])} if len(sys.argv) > 1 else {})
 m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
 X = m._x((rng.random((64 * 20, 784)) < pi).astype(np.float32))
 ns = [1, 2, 4, 8, 16, 20, 32, 64]
