@@ -106,24 +106,35 @@ def test_no_vector_memory_operation_in_an_execz_skippable_block(asm):
             assert not skipped, f"{name}: {l} at {i} can skip {skipped[:3]}"
 
 
+# (kernel symbol prefix, groups in the ring D): the requests issued after
+# group wait Y are those of group Y + D - 1 (the NLL forward waits with
+# vmcnt(0): nothing to check)
+RINGS = [(p, 2) for p, _, _ in TRAIN_RING[:4]] + [
+    ("_ZN4iwae10nre_kernel", 4),                   # 8 slots, 2 units per group
+    ("_ZN4iwae10nrb_kernelILi0E", 3),              # 6 slots, 2 units per group (NrbCount)
+    ("_ZN4iwae10nrb_kernelILi1E", 3),
+]
+
+
+def _straight(body):
+    labels = _labels(body)
+    back = [(labels[m.group(1)], i) for i, l in enumerate(body)
+            for m in [re.match(r"s_c?branch\w* (\.LBB\w+)$", l)] if m and labels[m.group(1)] < i]
+    return lambda lo, hi: not any(lo <= a <= hi or lo <= b <= hi for a, b in back)
+
+
 @pytest.mark.parametrize("prefix,pieces,stores", TRAIN_RING, ids=[p[0][6:30] for p in TRAIN_RING])
 def test_every_group_issues_its_pieces_and_stores(asm, prefix, pieces, stores):
     name = next(n for n in _kernels(asm) if n.startswith(prefix))
     body = _body(asm, name)
-    labels = _labels(body)
-    # loops (a branch back to an earlier label): the per-unit code of a stage
-    # not unrolled; its segments mix iterations, so only straight code is counted
-    back = [(labels[m.group(1)], i) for i, l in enumerate(body)
-            for m in [re.match(r"s_c?branch\w* (\.LBB\w+)$", l)] if m and labels[m.group(1)] < i]
+    straight = _straight(body)
     segs = _group_segments(body)
     assert len(segs) >= 8, f"{name}: {len(segs)} group waits"
     counted = 0
-    prev = 0
-    for k, (i, vm, ops) in enumerate(segs):
-        lo = prev
-        prev = i
-        if k == 0 or segs[k - 1][1] == 0 or any(lo <= a <= i or lo <= b <= i for a, b in back):
-            continue      # a prologue (after the start or a full drain: its own pieces), or loop code
+    for k in range(1, len(segs)):
+        i, vm, ops = segs[k]
+        if segs[k - 1][1] == 0 or not straight(segs[k - 1][0], i):
+            continue      # a prologue (after a full drain: its own pieces), or loop code
         n_lds = sum(1 for _, l in ops if l.endswith(" lds"))
         n_st = sum(1 for _, l in ops if "store" in l.split()[0])
         n_other = len(ops) - n_lds - n_st
@@ -132,3 +143,24 @@ def test_every_group_issues_its_pieces_and_stores(asm, prefix, pieces, stores):
         assert n_other == 0, f"{name}: group wait at {i}: {n_other} other vector memory operations"
         counted += 1
     assert counted >= len(segs) // 2, (name, counted, len(segs))
+
+
+@pytest.mark.parametrize("prefix,D", RINGS, ids=[p[0][6:30] for p in RINGS])
+def test_every_counted_wait_covers_its_groups_pieces(asm, prefix, D):
+    """At group wait X the wave's pieces of group X were requested right after
+    wait X - D + 1; everything it issued since is younger.  vmcnt(N) covers
+    the pieces iff N <= that count (in-order completion)."""
+    name = next(n for n in _kernels(asm) if n.startswith(prefix))
+    body = _body(asm, name)
+    straight = _straight(body)
+    segs = _group_segments(body)
+    checked = 0
+    for x in range(len(segs)):
+        first = x - D + 2                      # the segment that starts with group x's requests
+        if first < 1 or any(segs[j][1] == 0 for j in range(first - 1, x)) or not straight(segs[first - 1][0], segs[x][0]):
+            continue                           # prologue, a restart after a full drain, or loop code
+        ops = segs[first][2]
+        younger = sum(1 for _, l in ops if not l.endswith(" lds")) + sum(len(segs[j][2]) for j in range(first + 1, x + 1))
+        assert segs[x][1] <= younger, f"{name}: group wait at {segs[x][0]}: vmcnt({segs[x][1]}) > {younger} younger"
+        checked += 1
+    assert checked >= 4, (name, checked, len(segs))
