@@ -5,7 +5,8 @@ step where it does and which outputs differ there (the loss, each parameter
 tensor's gradient, its updated value).  Every path is meant to be bitwise
 reproducible, so a difference names a race (or a read of memory nothing
 wrote).
-    python tools/determinism_stress.py [B] [repeats] [steps] [knob=v,knob=v ...]"""
+    python tools/determinism_stress.py [B] [repeats] [steps] [knob=v,knob=v ...]
+NLL=1: instead, the k=5000 NLL of B images (device Philox) per fresh model."""
 import os
 import sys
 
@@ -28,7 +29,20 @@ rng = np.random.default_rng(7)
 xs = (rng.random((S * B, 784)) < 0.3).astype(np.float32)
 
 
+def run_nll(cfg):
+    m = Flexible_Model([200, 100], [100, 200], [100, 50], [100, 784], dataset_bias=None, loss_function="IWAE", k=50,
+                       seed=3, use_graphs=True, tuning=cfg)
+    m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
+    X = torch.from_numpy(xs[:B]).to(m.device)
+    m.set_seed(5)
+    v = np.float32(m.get_NLL(X, k=5000))
+    del m
+    return [(v, [], [])], [0, 0, 0]
+
+
 def run(cfg):
+    if os.environ.get("NLL") == "1":
+        return run_nll(cfg)
     m = Flexible_Model([200, 100], [100, 200], [100, 50], [100, 784], dataset_bias=None, loss_function="IWAE", k=50,
                        seed=3, use_graphs=True, tuning=cfg)
     m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
