@@ -154,8 +154,11 @@ enum iwae_knob {
                                       launch, its tiles of that layer waiting in-launch for job I' (1) */
   IWAE_KNOB_UPD_APPLY = 35,        /* beyond UPD_ROWS: the gradient pass's slabs summed, Adam and the FX / GX copies
                                       in one update-kernel launch instead of the Adam and FX-refresh launches (1) */
-  IWAE_KNOB_STEPS_FIRST = 36       /* iwae_train_steps: steps in a call's first captured graph, then up to 32 per
+  IWAE_KNOB_STEPS_FIRST = 36,     /* iwae_train_steps: steps in a call's first captured graph, then up to 32 per
                                       graph (0: 32 from the start) */
+  IWAE_KNOB_SM_CHAIN = 37          /* up to SMALLM_ROWS images: the first encoder layer's three few-row launches as
+                                      one launch, each layer waiting in-launch for the one before (0: measured
+                                      slower) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --
@@ -321,7 +324,9 @@ double iwae_workspace_bytes(const iwae_handle* h);
  * across its timed region), 8 in-launch waits of the combined image-row
  * backward + update launch that gave up (synchronous; 0 unless the GPU was
  * shared with a kernel that held CUs for ~1 s), 9 such combined launches
- * issued (a captured step counts once, at capture); -1 for an unknown id. */
+ * issued (a captured step counts once, at capture), 10 in-launch waits of the
+ * chained first-encoder-layer launch (smchain_kernel) that gave up
+ * (synchronous), 11 such chained launches issued; -1 for an unknown id. */
 long long iwae_debug_count(const iwae_handle* h, int what);
 /* Live kernel timing: bracket every launch of one kernel class with HIP events
  * on the handle's stream -- a GEMM class (kind: 0 forward, 1 backward-data,

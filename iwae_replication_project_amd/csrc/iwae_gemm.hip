@@ -26,6 +26,8 @@
 //                  backward pass; the [rows][784] probabilities never hit HBM.
 #include "iwae_kernels.h"
 
+#include <algorithm>
+
 namespace iwae {
 
 #ifdef IWAE_GEMM_TRACE
@@ -653,12 +655,55 @@ constexpr int SM_MAX_ASLABS = 4;    // partial slabs a reader sums while staging
 // activation rows in batches of SM_STAGE quads per thread.
 constexpr int SM_STAGE = 4;
 
+// In-launch chaining of the few-row layers (smchain_kernel): a later stage's
+// workgroups request their weights first, then wait for every workgroup of the
+// stage before it (agent scope: each producer drains its stores, barrier,
+// release fence, counter add; one consumer thread polls relaxed, then acquire
+// fence; the stages' workgroups are dispatched in stage order, so a waiting
+// workgroup never holds back one it waits for).  Bounded spins, give-ups
+// counted in ctr[3]; the last workgroup of the last stage through its wait
+// resets ctr[0..2] (every wait of the launch has passed by then).
+__device__ __forceinline__ void sm_wait(const SmChainArgs& c, int stage) {
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(c.ctr + stage - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+           (unsigned)c.nb[stage - 1]) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 24)) {
+        __hip_atomic_fetch_add(c.ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (stage == c.nstage - 1) {
+      const unsigned k = __hip_atomic_fetch_add(c.ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (k + 1 == (unsigned)c.nb[stage]) {
+        __hip_atomic_store(c.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(c.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(c.ctr + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ void sm_publish(const SmChainArgs& c, int stage) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(c.ctr + stage, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// one workgroup (column tile t, K slab ks) of a few-row Dense; ch: the chain it
+// is stage `stage` of (nullptr: a plain smallm_kernel launch)
 template <bool BT>
-__global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm_lds[];
+__device__ __forceinline__ void smallm_body(const SmArgs& a, int t, int ks, float* sm_lds, const SmChainArgs* ch,
+                                            int stage) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int t = blockIdx.x, ks = blockIdx.y;
   const int n = t * 16 + r;
   // this workgroup's K range [kb0, kb0 + Kb)
   const int KC = a.kslabs > 1 ? (((a.K + a.kslabs - 1) / a.kslabs) + 15) & ~15 : a.K;
@@ -688,11 +733,13 @@ __global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
       bq[u] = make_float4(e[0], e[1], e[2], e[3]);
     }
   }
+  // (chained: the activations are the previous stage's output)
+  if (ch && stage > 0) sm_wait(*ch, stage);
   // activations -> LDS (rows >= M and k >= K zero)
   const __amdgpu_buffer_rsrc_t rA = a.a_bytes ? buf_rsrc(a.A, a.a_bytes) : buf_rsrc(a.A);
   const int q4 = Kp >> 2;
   const int nq = 32 * q4;
-  const bool write_a = a.a_out != nullptr && blockIdx.x == 0 && ks == 0;
+  const bool write_a = a.a_out != nullptr && t == 0 && ks == 0;
   const int nsl = a.a_slabs;
   for (int e0 = threadIdx.x; e0 < nq; e0 += SM_STAGE * blockDim.x) {
     // the batch's loads (every slab of every quad) first
@@ -747,7 +794,7 @@ __global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
           if (k + 2 >= Kb) v.z = 0.f;
           if (k + 3 >= Kb) v.w = 0.f;
         }
-        if (a.a_copy && blockIdx.x == 0 && row < a.M && k < Kb) {
+        if (a.a_copy && t == 0 && row < a.M && k < Kb) {
           float* dst = a.a_copy + (size_t)row * a.a_copy_ld + gk;
           const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -794,15 +841,30 @@ __global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
   if (row < a.M && col < a.N) {
     if (a.kslabs > 1) {
       a.C[(size_t)ks * a.c_slab + (size_t)row * a.ldc + col] = v;
-      return;
+    } else {
+      if (a.act == 1) v = ftanh(v);
+      else if (a.act == 2) {
+        const float y = a.Y[(size_t)row * a.ldy + col];
+        v = v * (1.f - y * y);
+      }
+      a.C[(size_t)row * a.ldc + col] = v;
     }
-    if (a.act == 1) v = ftanh(v);
-    else if (a.act == 2) {
-      const float y = a.Y[(size_t)row * a.ldy + col];
-      v = v * (1.f - y * y);
-    }
-    a.C[(size_t)row * a.ldc + col] = v;
   }
+  if (ch && stage < ch->nstage - 1) sm_publish(*ch, stage);
+}
+
+template <bool BT>
+__global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm_lds[];
+  smallm_body<BT>(a, blockIdx.x, blockIdx.y, sm_lds, nullptr, 0);
+}
+
+// the first encoder layer's forward (input Dense, l2, head) as one launch
+__global__ __launch_bounds__(SM_WAVES * 64) void smchain_kernel(SmChainArgs c) {
+  extern __shared__ __attribute__((aligned(16))) float sm_lds[];
+  int b = blockIdx.x, stage = 0;
+  while (stage < c.nstage - 1 && b >= c.nb[stage]) b -= c.nb[stage++];
+  smallm_body<false>(c.s[stage], b % c.gx[stage], b / c.gx[stage], sm_lds, &c, stage);
 }
 
 hipError_t launch_smallm(hipStream_t st, const SmArgs& a) {
@@ -819,7 +881,37 @@ hipError_t launch_smallm(hipStream_t st, const SmArgs& a) {
   return hipGetLastError();
 }
 
+static size_t smallm_lds(const SmArgs& a) {
+  const int ksl = a.kslabs > 1 ? a.kslabs : 1;
+  const int KC = ksl > 1 ? (((a.K + ksl - 1) / ksl) + 15) & ~15 : a.K;
+  const int Kp = (KC + 15) & ~15;
+  return (size_t)(32 * (Kp + 4) + SM_WAVES * 2 * 4 * 64) * sizeof(float);
+}
+
+hipError_t launch_smchain(hipStream_t st, SmChainArgs& c) {
+  size_t lds = 0;
+  int nb = 0;
+  for (int j = 0; j < c.nstage; ++j) {
+    const SmArgs& a = c.s[j];
+    const int ksl = a.kslabs > 1 ? a.kslabs : 1;
+    const int KC = ksl > 1 ? (((a.K + ksl - 1) / ksl) + 15) & ~15 : a.K;
+    if (a.bt || a.M <= 0 || a.M > 32 || a.N <= 0 || KC > SM_WAVES * 16 * SM_MAXU || a.a_slabs > SM_MAX_ASLABS)
+      return hipErrorInvalidValue;
+    c.gx[j] = (a.N + 15) / 16;
+    c.nb[j] = c.gx[j] * ksl;
+    nb += c.nb[j];
+    lds = std::max(lds, smallm_lds(a));
+  }
+  // every workgroup resident at once (one per CU at most), so no wait outlives its producer's dispatch
+  if (c.nstage < 2 || c.nstage > 3 || nb > 256 || !c.ctr) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(smchain_kernel, dim3(nb), dim3(SM_WAVES * 64), lds, st, c);
+  return hipGetLastError();
+}
+
 hipError_t smallm_setup_attributes() {
+  hipError_t e0 = hipFuncSetAttribute((const void*)smchain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024);
+  if (e0 != hipSuccess) return e0;
   hipError_t e = hipFuncSetAttribute((const void*)smallm_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      160 * 1024);
   if (e != hipSuccess) return e;

@@ -193,6 +193,18 @@ struct SmArgs {
 };
 hipError_t launch_smallm(hipStream_t st, const SmArgs& a);
 hipError_t smallm_setup_attributes();
+// two or three forward few-row layers (bt 0) in one launch, stage j reading
+// stage j - 1's output after an in-launch wait (iwae_gemm.hip smchain_kernel);
+// gx / nb are filled in place by launch_smchain (a graph node re-pointed
+// later takes the filled struct); ctr: 4 zeroed words [stage 0 done, stage 1
+// done, last stage through, spin give-ups]
+struct SmChainArgs {
+  SmArgs s[3];
+  int nstage;
+  int gx[3], nb[3];
+  unsigned* ctr;
+};
+hipError_t launch_smchain(hipStream_t st, SmChainArgs& c);
 
 // grouped backward-weight GEMMs (64x64 tiles, split over K = rows)
 constexpr int kMaxGroup = 16;

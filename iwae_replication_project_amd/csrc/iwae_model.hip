@@ -215,7 +215,11 @@ struct iwae_handle {
   int tcu = 1;                       // job I' and the fused update in one launch (tcu_kernel) where it fits
   int upd_apply = 1;                 // large batches: the update kernel sums the slabs, Adam, FX / GX (one launch)
   int steps_first = 0;               // iwae_train_steps: length of a call's first graph (0: 32 like the rest)
-  unsigned* tcu_ctr = nullptr;       // its in-launch counters (zero between launches; [2] spin give-ups)
+  unsigned* tcu_ctr = nullptr;       // its in-launch counters (zero between launches; [2] spin give-ups);
+                                     // [4..7]: smchain_kernel's ([7] spin give-ups)
+  int sm_chain = 0;                  // the first encoder layer's three few-row launches as one (smchain_kernel;
+                                     // measured slower: B = 20 step 0.136-0.137 vs 0.114 ms, r05x)
+  long long n_smchain = 0;           // smchain_kernel launches, iwae_debug_count(h, 11)
   bool defer_launch = false;         // (during a step) tc_run / run_update record their launch instead
   bool pend_tc_have = false, pend_upd_have = false;
   TcArgs pend_tc{};
@@ -235,9 +239,10 @@ struct iwae_handle {
   // (x_node: that launch, re-pointed with hipGraphExecKernelNodeSetParams)
   // the input-layer launch of a captured train step, re-pointed at each call's x
   struct XLaunch {
-    int kind = 0;                      // 0: smallm_kernel (SmArgs), 1: gemm_kernel (GemmArgs)
+    int kind = 0;                      // 0: smallm_kernel (SmArgs), 1: gemm_kernel (GemmArgs), 2: smchain_kernel
     SmArgs sm{};
     GemmArgs gm{};
+    SmChainArgs sc{};
   };
   struct GraphRec {
     hipGraphExec_t exec = nullptr;
@@ -1063,7 +1068,8 @@ static RbNoise rb_noise(iwae_handle* h, const Plan& P, const EpsSet& E, int laye
 }
 
 // few-row Dense layer (per-image first encoder layer of a small batch)
-static int smallm(iwae_handle* h, const Mat& A, int rows, const DenseL& d, bool bwd, int act, const Mat* Y, Mat& C) {
+static SmArgs smallm_args(iwae_handle* h, const Mat& A, int rows, const DenseL& d, bool bwd, int act, const Mat* Y,
+                          Mat& C) {
   SmArgs a{};
   a.A = A.p; a.lda = A.ld;
   a.W = h->params + d.off; a.ldw = d.ldw; a.bt = bwd ? 1 : 0;
@@ -1071,7 +1077,10 @@ static int smallm(iwae_handle* h, const Mat& A, int rows, const DenseL& d, bool 
   a.M = rows; a.N = bwd ? d.fin : d.fout; a.K = bwd ? d.fout : d.fin + 1;
   a.act = act;
   if (Y) { a.Y = Y->p; a.ldy = Y->ld; }
-  HIPCHK(launch_smallm(h->stream, a));
+  return a;
+}
+static int smallm(iwae_handle* h, const Mat& A, int rows, const DenseL& d, bool bwd, int act, const Mat* Y, Mat& C) {
+  HIPCHK(launch_smallm(h->stream, smallm_args(h, A, rows, d, bwd, act, Y, C)));
   return IWAE_OK;
 }
 static bool smallm_ok(const iwae_handle* h, int rows) {
@@ -1121,9 +1130,9 @@ static int enc0_forward(iwae_handle* h, const Plan& P, bool l1_only = false) {
       a.C = h->eb[0].y1.p; a.ldc = h->eb[0].y1.ld;
       a.act = 1;
     }
-    HIPCHK(launch_smallm(h->stream, a));
-    if (h->capturing && h->x_user) {
-      // remember this launch: replays re-point it at the caller's next x
+    // remember the launch that reads x: replays re-point it at the caller's next x
+    auto note_x = [&](int kind, const SmChainArgs* c) -> int {
+      if (!(h->capturing && h->x_user)) return IWAE_OK;
       hipStreamCaptureStatus cs;
       unsigned long long cid;
       hipGraph_t cg;
@@ -1131,9 +1140,42 @@ static int enc0_forward(iwae_handle* h, const Plan& P, bool l1_only = false) {
       size_t nd = 0;
       HIPCHK(hipStreamGetCaptureInfo_v2(h->stream, &cs, &cid, &cg, &deps, &nd));
       h->cap_x_node = nd == 1 ? deps[0] : nullptr;
-      h->cap_x_args.kind = 0;
+      h->cap_x_args.kind = kind;
       h->cap_x_args.sm = a;
+      if (c) h->cap_x_args.sc = *c;
+      return IWAE_OK;
+    };
+    if (!l1_only && h->sm_chain && h->prof_kind < 0) {
+      // the three layers as ONE launch (smchain_kernel): the l2 and head
+      // workgroups request their weights at the launch's start and wait in-launch
+      // for the layer before (three launches: 6.3 + 6.9 + 5.4 us at B = 20).
+      // Off by default: the step measured 0.136-0.137 against 0.114 ms -- the
+      // agent-scope handoffs (every producer's L2 write-back, every consumer's
+      // L2 invalidate across 8 XCDs) cost more than the two launch boundaries
+      // (profiles/r05x_sm_chain_ab.txt)
+      SmChainArgs c{};
+      c.s[0] = a;
+      const DenseL& d2 = h->dense[S0.l2];
+      if (ksl > 1) {
+        SmArgs& b = c.s[1];
+        b.A = h->fslab; b.lda = a.ldc;
+        b.a_slabs = ksl; b.a_slab = a.c_slab; b.a_act = 1; b.a_out = h->eb[0].y1.p; b.a_ldo = h->eb[0].y1.ld;
+        b.W = h->params + d2.off; b.ldw = d2.ldw;
+        b.C = h->eb[0].y2.p; b.ldc = h->eb[0].y2.ld;
+        b.M = P.Bimg; b.N = d2.fout; b.K = d2.fin + 1;
+        b.act = 1;
+      } else {
+        c.s[1] = smallm_args(h, h->eb[0].y1, P.Bimg, d2, false, 1, nullptr, h->eb[0].y2);
+      }
+      c.s[2] = smallm_args(h, h->eb[0].y2, P.Bimg, h->dense[S0.head], false, 0, nullptr, h->eb[0].P);
+      c.nstage = 3;
+      c.ctr = h->tcu_ctr + 4;
+      HIPCHK(launch_smchain(h->stream, c));
+      h->n_smchain++;
+      return note_x(2, &c);
     }
+    HIPCHK(launch_smallm(h->stream, a));
+    CHK(note_x(0, nullptr));
     if (l1_only) return IWAE_OK;
     if (ksl > 1) {
       const DenseL& d2 = h->dense[S0.l2];
@@ -2527,9 +2569,11 @@ static hipError_t repoint_x(hipGraphExec_t exec, hipGraphNode_t node, const iwae
   if (e != hipSuccess) return e;
   SmArgs sa = xa.sm;
   GemmArgs ga = xa.gm;
+  SmChainArgs ca = xa.sc;
   sa.A = x;
   ga.A = x;
-  void* args[] = {xa.kind == 1 ? (void*)&ga : (void*)&sa};
+  ca.s[0].A = x;
+  void* args[] = {xa.kind == 1 ? (void*)&ga : xa.kind == 2 ? (void*)&ca : (void*)&sa};
   kp.kernelParams = args;
   kp.extra = nullptr;
   return hipGraphExecKernelNodeSetParams(exec, node, &kp);
@@ -2861,8 +2905,8 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (e == hipSuccess) e = hipMalloc(&h->adam_v, pb);
   if (e == hipSuccess) e = hipMalloc(&h->grad_own, pb + 4 * sizeof(float));   // + the DP batch-size tail
   if (e == hipSuccess) e = hipMalloc(&h->ds, sizeof(DevState));
-  if (e == hipSuccess) e = hipMalloc(&h->tcu_ctr, 4 * sizeof(unsigned));
-  if (e == hipSuccess) e = hipMemset(h->tcu_ctr, 0, 4 * sizeof(unsigned));
+  if (e == hipSuccess) e = hipMalloc(&h->tcu_ctr, 8 * sizeof(unsigned));
+  if (e == hipSuccess) e = hipMemset(h->tcu_ctr, 0, 8 * sizeof(unsigned));
   if (e == hipSuccess) e = hipMalloc(&h->wsplit_hi, (size_t)(2 * h->wsplit_elems) * sizeof(__bf16));
   if (e == hipSuccess) e = hipMalloc(&h->fx_hi, (size_t)(2 * h->fx_elems) * sizeof(__bf16));
   if (e == hipSuccess) e = hipMemset(h->fx_hi, 0, (size_t)(2 * h->fx_elems) * sizeof(__bf16));
@@ -3062,6 +3106,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_TCU: h->tcu = on; break;
     case IWAE_KNOB_UPD_APPLY: h->upd_apply = on; break;
     case IWAE_KNOB_STEPS_FIRST: h->steps_first = (int)std::max(0LL, std::min(value, (long long)kGraphSteps)); break;
+    case IWAE_KNOB_SM_CHAIN: h->sm_chain = value ? 1 : 0; break;
     case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;
@@ -3936,6 +3981,13 @@ long long iwae_debug_count(const iwae_handle* h, int what) {
       return v[2];
     }
     case 9: return h->n_tcu;
+    case 10: {                          // smchain_kernel spin give-ups so far (synchronous read)
+      unsigned v[8] = {};
+      if (hipStreamSynchronize(h->stream) != hipSuccess ||
+          hipMemcpy(v, h->tcu_ctr, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+      return v[7];
+    }
+    case 11: return h->n_smchain;
     default: return -1;
   }
 }

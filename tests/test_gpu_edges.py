@@ -324,3 +324,33 @@ def test_input_gemm_on_the_callers_x_equals_the_staged_copy(B):
     for r in runs[1:]:
         for u, v in zip(runs[0], r):
             np.testing.assert_array_equal(u, v)
+
+
+@pytest.mark.parametrize("B", [20, 7, 32])
+def test_first_encoder_layer_chain_equals_three_launches(B):
+    """Up to 32 images the first encoder layer (input Dense split over K, l2,
+    head) runs as ONE launch, smchain_kernel: the l2 and head workgroups
+    request their weights first and wait in-launch for the layer before
+    (agent-scope release / counter / acquire).  Same arithmetic and summation
+    order as the three launches (knob sm_chain 0): losses, weights and Adam
+    state equal bit for bit over graph replays with a moving batch (the chained
+    launch re-pointed at each call's x), a multi-step train_steps call and
+    eager steps; no wait gave up (iwae_debug_count 10)."""
+    import torch
+    rng = np.random.default_rng(91 + B)
+    xs = (rng.random((6 * B + 5, 784)) < 0.3).astype(np.float32)
+    runs = []
+    for chain in (1, 0):
+        for graphs in (True, False):
+            m = _model(ARCH2, "IWAE", 50, use_graphs=graphs, tuning={"sm_chain": chain})
+            X = torch.from_numpy(xs).to(m.device)
+            losses = [m.train_step(X[i * B + i:(i + 1) * B + i])["IWAE"] for i in range(3)]
+            losses += list(m.train_steps(X[3 * B + 3:6 * B + 3], B))
+            mm, vv, st = m.get_optimizer_state()
+            n_chain = m._lib.iwae_debug_count(m._h, 11)
+            assert (n_chain > 0) == bool(chain), (chain, n_chain)
+            assert m._lib.iwae_debug_count(m._h, 10) == 0
+            runs.append((np.asarray(losses, np.float32), _flat(m.get_weights()), mm, vv))
+    for r in runs[1:]:
+        for u, v in zip(runs[0], r):
+            np.testing.assert_array_equal(u, v)
