@@ -254,6 +254,8 @@ struct iwae_handle {
     std::vector<hipGraphNode_t> xs_node;
     std::vector<XLaunch> xs_args;
     std::vector<const float*> xs_cap;
+    hipGraphNode_t loss_node = nullptr;  // its last node: the losses' copy, re-pointed at each call's loss_dev
+    float* loss_cap = nullptr;
   };
   std::map<std::vector<long long>, GraphRec> graphs;
   const float* x_user = nullptr;       // train step: caller's x read directly by the first kernel
@@ -262,7 +264,9 @@ struct iwae_handle {
   XLaunch cap_x_args{};
   // live kernel timing (HIP events around every launch of one GEMM class)
   float* loss_out = nullptr;           // train-step loss destination (part of the graph key)
-  float* loss_slots = nullptr;         // multi-step graphs: step j's loss (kGraphSteps floats)
+  float* loss_slots = nullptr;         // multi-step graphs: step j's loss (kGraphSteps floats), then
+                                       // [kGraphSteps, 2 kGraphSteps): where a graph's copy node writes
+                                       // when the call wants no losses
   int prof_kind = -1, prof_epi = -1;
   std::vector<hipEvent_t> prof_ev;
   size_t prof_used = 0;
@@ -2681,7 +2685,7 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
 // E:82): graphs of up to kGraphSteps captured steps, so consecutive steps run
 // without the per-graph launch gap; step j of a graph reads its own batch (its
 // input-layer launch re-pointed when the batch moves) and writes its loss to
-// loss_slots[j], copied to loss_dev + i after the graph.  Anything the
+// loss_slots[j], copied to loss_dev + i by the graph's last node.  Anything the
 // multi-step graph does not cover (no graphs, staged x, data parallel, live
 // profiling) runs as nsteps single steps.
 static constexpr int kGraphSteps = 32;
@@ -2714,6 +2718,21 @@ static int steps_graph(iwae_handle* h, const iwae_loss_config* lc, const Plan& P
       g.xs_args.push_back(h->cap_x_args);
       g.xs_cap.push_back(h->x_user);
     }
+    if (rc == IWAE_OK) {
+      // the losses' copy as the graph's last node (a copy after the graph was a
+      // launch of its own: +9 us gap and 4 us per call, profiles/r05q_train_step_timeline.txt);
+      // captured into the no-losses sink, re-pointed per call
+      g.loss_cap = h->loss_slots + kGraphSteps;
+      hipError_t em = hipMemcpyAsync(g.loss_cap, h->loss_slots, S * sizeof(float), hipMemcpyDeviceToDevice, h->stream);
+      hipStreamCaptureStatus cs;
+      unsigned long long cid;
+      hipGraph_t cg;
+      const hipGraphNode_t* deps = nullptr;
+      size_t nd = 0;
+      if (em == hipSuccess) em = hipStreamGetCaptureInfo_v2(h->stream, &cs, &cid, &cg, &deps, &nd);
+      if (em != hipSuccess) rc = fail(h, IWAE_EHIP, "multi-step capture: the losses' copy");
+      else g.loss_node = nd == 1 ? deps[0] : nullptr;
+    }
     const hipError_t ec = hipStreamEndCapture(h->stream, &graph);
     h->capturing = false;
     if (rc != IWAE_OK || ec != hipSuccess) {
@@ -2733,6 +2752,10 @@ static int steps_graph(iwae_handle* h, const iwae_loss_config* lc, const Plan& P
         destroy_graph(g);
         return fail(h, IWAE_EHIP, "multi-step capture: input-layer launch not found");
       }
+    if (!g.loss_node) {
+      destroy_graph(g);
+      return fail(h, IWAE_EHIP, "multi-step capture: the losses' copy node not found");
+    }
     h->n_captures++;
     it = h->graphs.emplace(key, g).first;
   }
@@ -2791,7 +2814,7 @@ static int do_train_steps(iwae_handle* h, const iwae_loss_config* lc, const floa
       (void)nre_plan(h, ne);
     }
   }
-  if (!h->loss_slots) HIPCHK(hipMalloc(&h->loss_slots, kGraphSteps * sizeof(float)));
+  if (!h->loss_slots) HIPCHK(hipMalloc(&h->loss_slots, 2 * kGraphSteps * sizeof(float)));
   h->in_train_step = true;
   const long long pv = h->params_version, wv = h->wsplit_version, fv = h->fx_version;
   struct Reset {
@@ -2822,9 +2845,13 @@ static int do_train_steps(iwae_handle* h, const iwae_loss_config* lc, const floa
       HIPCHK(repoint_x(g.exec, g.xs_node[j], g.xs_args[j], xj));
       g.xs_cap[j] = xj;
     }
+    float* ldst = loss_dev ? loss_dev + i0 : h->loss_slots + kGraphSteps;
+    if (g.loss_cap != ldst) {
+      HIPCHK(hipGraphExecMemcpyNodeSetParams1D(g.exec, g.loss_node, ldst, h->loss_slots, S * sizeof(float),
+                                               hipMemcpyDeviceToDevice));
+      g.loss_cap = ldst;
+    }
     HIPCHK(hipGraphLaunch(g.exec, h->stream));
-    if (loss_dev)
-      HIPCHK(hipMemcpyAsync(loss_dev + i0, h->loss_slots, S * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
     h->params_version++;
     h->fx_version = h->params_version;   // every replayed step refreshed the fragment-major copies
   }
