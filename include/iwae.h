@@ -156,9 +156,12 @@ enum iwae_knob {
                                       in one update-kernel launch instead of the Adam and FX-refresh launches (1) */
   IWAE_KNOB_STEPS_FIRST = 36,     /* iwae_train_steps: steps in a call's first captured graph, then up to 32 per
                                       graph (0: 32 from the start) */
-  IWAE_KNOB_SM_CHAIN = 37          /* up to SMALLM_ROWS images: the first encoder layer's three few-row launches as
+  IWAE_KNOB_SM_CHAIN = 37,        /* up to SMALLM_ROWS images: the first encoder layer's three few-row launches as
                                       one launch, each layer waiting in-launch for the one before (0: measured
                                       slower) */
+  IWAE_KNOB_DW_SCALE_COST = 38,   /* weight-gradient pass (dw_kernel) cost model: extra tile units per k step of a
+                                      row-scaled dZ (0) */
+  IWAE_KNOB_DW_WIDE_COST = 39      /* ... and of a wide block (0) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --

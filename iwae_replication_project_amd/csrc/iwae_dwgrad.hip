@@ -360,9 +360,6 @@ __global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
   const int bx = blockIdx.x, x = bx & 7, sl = bx >> 3;
   const int item = x * a.per_xcd + sl;
   if (sl >= a.per_xcd || item >= a.nitems) return;
-#ifdef IWAE_DW_TRACE
-  if (threadIdx.x == 0 && bx < 256) g_dw_trace[bx * kDwTr] = item;
-#endif
   int jb = 0;
   while (jb + 1 < a.njobs && item >= a.job[jb + 1].item0) ++jb;
   const DwJob& J = a.job[jb];
@@ -372,6 +369,13 @@ __global__ __launch_bounds__(DW_NT) void dw_kernel(DwArgs a) {
   const int jbk = li % J.njb, s = li / J.njb;
   const int i0 = 16 * J.mtb * ib, j0 = 16 * J.ntb * jbk;
   const int mtb = min(J.mtb, J.mt - J.mtb * ib), ntb = min(J.ntb, J.nt - J.ntb * jbk);
+#ifdef IWAE_DW_TRACE
+  // item | job << 16 | tiles of the block (rows << 24, columns << 32) | wide << 40
+  if (threadIdx.x == 0 && bx < 256)
+    g_dw_trace[bx * kDwTr] = (unsigned long long)item | ((unsigned long long)jb << 16) |
+                             ((unsigned long long)mtb << 24) | ((unsigned long long)ntb << 32) |
+                             ((unsigned long long)J.wide << 40);
+#endif
   const int rbase = s * J.chunk, rend = min(J.rows, rbase + J.chunk);
   const int nk = (rend - rbase + DW_KR - 1) / DW_KR;
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);

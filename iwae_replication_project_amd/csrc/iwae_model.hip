@@ -210,6 +210,8 @@ struct iwae_handle {
   int dw_wg = 256;                   // large-batch weight-gradient pass: workgroups its row chunks aim at
   int dw_alpha = 150;                // ... its cost model: a k step's fixed cost in MFMA tiles (measured: a
                                      // k step costs ~2 us whatever its tiles; alpha 0 / 45 / 90 / 200: 174 / 127 / 108 / 106 us)
+  int dw_scale_cost = 0;             // ... the extra cost of a row-scaled dZ's k step (tile units)
+  int dw_wide_cost = 0;              // ... and of a wide block's
   int img_rows_fwd = 0, img_rows_bwd = 0;   // image-row jobs I / I': rows per workgroup (0: auto)
   int x_direct = 1;                  // large-batch engine step: the input GEMM reads the caller's x (gemm_direct)
   int tcu = 1;                       // job I' and the fused update in one launch (tcu_kernel) where it fits
@@ -1741,7 +1743,9 @@ static int run_dw(iwae_handle* h, const Plan& P) {
     J.wide = J.mt <= 8 && J.nt > 8 ? 1 : 0;
     J.nib = (int)cdiv(J.mt, J.wide ? 8 : 13); J.mtb = (int)cdiv(J.mt, J.nib);
     J.njb = (int)cdiv(J.nt, J.wide ? 16 : 8); J.ntb = (int)cdiv(J.nt, J.njb);
-    cost[q] = (double)J.mtb * J.ntb + (double)h->dw_alpha;   // + a k step's fixed cost in tile units
+    // a k step's fixed cost in tile units, + a row-scaled dZ's and a wide block's
+    cost[q] = (double)J.mtb * J.ntb + (double)h->dw_alpha + (dz_scale(h, js[q].di, js[q].ks) ? h->dw_scale_cost : 0) +
+              (J.wide ? h->dw_wide_cost : 0);
     W += cost[q] * J.nib * J.njb * (double)cdiv(js[q].rows, 32);
   }
   // block-k-steps of tiles per workgroup; the grid must not exceed one workgroup
@@ -3134,6 +3138,8 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_UPD_APPLY: h->upd_apply = on; break;
     case IWAE_KNOB_STEPS_FIRST: h->steps_first = (int)std::max(0LL, std::min(value, (long long)kGraphSteps)); break;
     case IWAE_KNOB_SM_CHAIN: h->sm_chain = value ? 1 : 0; break;
+    case IWAE_KNOB_DW_SCALE_COST: h->dw_scale_cost = (int)std::max(0LL, std::min(value, 1000LL)); break;
+    case IWAE_KNOB_DW_WIDE_COST: h->dw_wide_cost = (int)std::max(0LL, std::min(value, 1000LL)); break;
     case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;

@@ -32,7 +32,7 @@ n = dump(buf, 256 * K)
 rows = []
 for b in range(256):
     r = buf[b * K:(b + 1) * K]
-    item, nk, t0, t1 = r[0], r[1], r[2], r[K - 1]
+    item, nk, t0, t1 = r[0] & 0xFFFF, r[1], r[2], r[K - 1]
     if nk == 0 or t1 <= t0:
         continue
     ks = min(nk + (nk & 1), 80)
@@ -55,3 +55,17 @@ print("  ".join(f"{a:.0f}/{b}/{c:.2f}" for a, b, c in d))
 hist = collections.Counter(int(a // 10) * 10 for a, _, _ in d)
 print("duration histogram (10 us bins):", dict(sorted(hist.items())))
 print(f"mean {sum(a for a, _, _ in d) / len(d):.1f} us, max {d[0][0]:.1f} us")
+# per job: block shape, items, k steps, duration, time per k step (the cost model's unit)
+per = collections.defaultdict(list)
+for b in range(256):
+    r = buf[b * K:(b + 1) * K]
+    if r[1] == 0 or r[K - 1] <= r[2]:
+        continue
+    w = r[0]
+    per[((w >> 16) & 0xFF, (w >> 24) & 0xFF, (w >> 32) & 0xFF, (w >> 40) & 1)].append((r[1], (r[K - 1] - r[2]) / 100.0))
+print("job mtb ntb wide | items  k steps  dur us (mean / max)  us per k step  tiles")
+for (jb, mtb, ntb, wide), v in sorted(per.items()):
+    nk = sum(a for a, _ in v) / len(v)
+    du = [b for _, b in v]
+    print(f"{jb:3d} {mtb:3d} {ntb:3d} {wide:4d} | {len(v):5d}  {nk:7.1f}  {sum(du) / len(du):7.1f} / {max(du):6.1f}"
+          f"  {sum(b / a for a, b in v) / len(v):8.3f}  {mtb * ntb:5d}")
