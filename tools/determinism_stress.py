@@ -6,7 +6,8 @@ tensor's gradient, its updated value).  Every path is meant to be bitwise
 reproducible, so a difference names a race (or a read of memory nothing
 wrote).
     python tools/determinism_stress.py [B] [repeats] [steps] [knob=v,knob=v ...]
-NLL=1: instead, the k=5000 NLL of B images (device Philox) per fresh model."""
+NLL=1: instead, the k=5000 NLL of B images (device Philox) per fresh model.
+LOSS=<name> [K=<k>]: another loss function (default IWAE, k=50)."""
 import os
 import sys
 
@@ -40,11 +41,17 @@ def run_nll(cfg):
     return [(v, [], [])], [0, 0, 0]
 
 
+LOSS = os.environ.get("LOSS", "IWAE")
+KS = int(os.environ.get("K", "50"))
+LOSS_KW = {"CIWAE": {"beta": 0.5}, "L_alpha": {"alpha": 0.5}, "L_power_p": {"p": 2.0},
+           "MIWAE": {"k1": 8, "k2": 8}, "PIWAE": {"k1": 8, "k2": 8}}.get(LOSS, {})
+
+
 def run(cfg):
     if os.environ.get("NLL") == "1":
         return run_nll(cfg)
-    m = Flexible_Model([200, 100], [100, 200], [100, 50], [100, 784], dataset_bias=None, loss_function="IWAE", k=50,
-                       seed=3, use_graphs=True, tuning=cfg)
+    m = Flexible_Model([200, 100], [100, 200], [100, 50], [100, 784], dataset_bias=None, loss_function=LOSS, k=KS,
+                       seed=3, use_graphs=True, tuning=cfg, **LOSS_KW)
     m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
     X = torch.from_numpy(xs).to(m.device)
     if SETTLE:
@@ -53,7 +60,7 @@ def run(cfg):
         time.sleep(0.05)
     steps = []
     for i in range(S):
-        loss = np.float32(m.train_step(X[i * B:(i + 1) * B])["IWAE"])
+        loss = np.float32(m.train_step(X[i * B:(i + 1) * B])[LOSS])
         g = [np.asarray(t, np.float32).copy() for t in m.get_gradients()]
         w = [np.asarray(t, np.float32).copy() for t in m.get_weights()]
         steps.append((loss, g, w))
