@@ -354,3 +354,38 @@ def test_first_encoder_layer_chain_equals_three_launches(B):
     for r in runs[1:]:
         for u, v in zip(runs[0], r):
             np.testing.assert_array_equal(u, v)
+
+
+def test_train_steps_losses_copy_node_repointed_and_null():
+    """A multi-step graph's last node copies its losses to the caller's array,
+    re-pointed per call (hipGraphExecMemcpyNodeSetParams1D).  Calls with no
+    loss array (NULL: the copy goes to a sink), with one array and with
+    another array replay the same graphs (45 steps: 32 + 13) and leave the
+    same weights as a model whose every call passed one array; each array
+    receives exactly its call's losses."""
+    import ctypes
+    import torch
+    from iwae_replication_project_amd import _lib
+    rng = np.random.default_rng(77)
+    B, n = 20, 45
+    xs = (rng.random((3 * n * B, 784)) < 0.3).astype(np.float32)
+    res = []
+    for mode in ("arrays", "mixed"):
+        m = _model(ARCH2, "IWAE", 50)
+        X = torch.from_numpy(xs).to(m.device)
+        outs = []
+        for c in range(3):
+            xc = X[c * n * B:(c + 1) * n * B]
+            if mode == "mixed" and c == 0:
+                m._call(m._lib.iwae_train_steps(m._h, m._lc(), _lib.fptr(xc), B, n,
+                                                ctypes.cast(None, _lib.FP)))
+                m._stream.synchronize()
+                outs.append(None)
+            else:
+                outs.append(np.asarray(m.train_steps(xc, B), np.float32))
+        res.append((outs, _flat(m.get_weights())))
+    (a_outs, a_w), (b_outs, b_w) = res
+    np.testing.assert_array_equal(a_w, b_w)
+    for c in (1, 2):
+        np.testing.assert_array_equal(a_outs[c], b_outs[c])
+    assert np.isfinite(a_outs[0]).all() and not np.array_equal(a_outs[1], a_outs[2])
