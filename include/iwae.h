@@ -161,7 +161,10 @@ enum iwae_knob {
                                       slower) */
   IWAE_KNOB_DW_SCALE_COST = 38,   /* weight-gradient pass (dw_kernel) cost model: extra tile units per k step of a
                                       row-scaled dZ (0) */
-  IWAE_KNOB_DW_WIDE_COST = 39      /* ... and of a wide block (0) */
+  IWAE_KNOB_DW_WIDE_COST = 39,     /* ... and of a wide block (0) */
+  IWAE_KNOB_SM_PAIR = 40           /* up to SMALLM_ROWS images: the first encoder layer's l2 and head as one launch,
+                                      every workgroup computing the whole l2 into its LDS: 1 exact f32 (bitwise the
+                                      two launches), 2 l2's products bf16x3 (0) */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --
@@ -329,7 +332,8 @@ double iwae_workspace_bytes(const iwae_handle* h);
  * shared with a kernel that held CUs for ~1 s), 9 such combined launches
  * issued (a captured step counts once, at capture), 10 in-launch waits of the
  * chained first-encoder-layer launch (smchain_kernel) that gave up
- * (synchronous), 11 such chained launches issued; -1 for an unknown id. */
+ * (synchronous), 11 such chained launches issued, 12 first-encoder-layer l2 +
+ * head launches (smpair_kernel) issued; -1 for an unknown id. */
 long long iwae_debug_count(const iwae_handle* h, int what);
 /* Live kernel timing: bracket every launch of one kernel class with HIP events
  * on the handle's stream -- a GEMM class (kind: 0 forward, 1 backward-data,

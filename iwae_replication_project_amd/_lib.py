@@ -22,7 +22,7 @@ KNOBS = {
     "nring": 21, "nring_train": 22, "nring_train_rows": 23, "nring_bwd": 24, "wide_rt": 25, "upd_waves": 26,
     "nll_imgs": 27, "dw_wg": 28, "piwae_one": 29, "dw_alpha": 30,
     "img_rows_fwd": 31, "img_rows_bwd": 32, "x_direct": 33, "tcu": 34, "upd_apply": 35, "steps_first": 36,
-    "sm_chain": 37, "dw_scale_cost": 38, "dw_wide_cost": 39,
+    "sm_chain": 37, "dw_scale_cost": 38, "dw_wide_cost": 39, "sm_pair": 40,
 }
 LOSS_IDS = {
     "VAE": 0, "IWAE": 1, "VAE_V1": 2, "L_alpha": 3, "L_power_p": 4,

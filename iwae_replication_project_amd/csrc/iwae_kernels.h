@@ -192,6 +192,12 @@ struct SmArgs {
   int a_ones; unsigned a_bytes; float* a_copy; int a_copy_ld;
 };
 hipError_t launch_smallm(hipStream_t st, const SmArgs& a);
+// l2 (bt 0, tanh) and the head (act 0, K = l2.N + 1) of the first encoder
+// layer in one launch, one workgroup per head column tile, each computing the
+// whole l2 into LDS first (iwae_gemm.hip smpair_kernel): x3 0 exact f32 (bitwise
+// the two smallm launches), 1 l2's products bf16x3; smpair_fits: the shapes it takes
+bool smpair_fits(const SmArgs& l2, const SmArgs& hd, bool x3);
+hipError_t launch_smpair(hipStream_t st, const SmArgs& l2, const SmArgs& hd, bool x3);
 hipError_t smallm_setup_attributes();
 // two or three forward few-row layers (bt 0) in one launch, stage j reading
 // stage j - 1's output after an in-launch wait (iwae_gemm.hip smchain_kernel);

@@ -222,6 +222,8 @@ struct iwae_handle {
   int sm_chain = 0;                  // the first encoder layer's three few-row launches as one (smchain_kernel;
                                      // measured slower: B = 20 step 0.136-0.137 vs 0.114 ms, r05x)
   long long n_smchain = 0;           // smchain_kernel launches, iwae_debug_count(h, 11)
+  int sm_pair = 0;                   // the first encoder layer's l2 and head as one launch (smpair_kernel: 1 exact f32, 2 bf16x3 l2)
+  long long n_smpair = 0;            // smpair_kernel launches, iwae_debug_count(h, 12)
   bool defer_launch = false;         // (during a step) tc_run / run_update record their launch instead
   bool pend_tc_have = false, pend_upd_have = false;
   TcArgs pend_tc{};
@@ -1183,20 +1185,29 @@ static int enc0_forward(iwae_handle* h, const Plan& P, bool l1_only = false) {
     HIPCHK(launch_smallm(h->stream, a));
     CHK(note_x(0, nullptr));
     if (l1_only) return IWAE_OK;
+    const DenseL& d2 = h->dense[S0.l2];
+    SmArgs b{};
     if (ksl > 1) {
-      const DenseL& d2 = h->dense[S0.l2];
-      SmArgs b{};
       b.A = h->fslab; b.lda = a.ldc;
       b.a_slabs = ksl; b.a_slab = a.c_slab; b.a_act = 1; b.a_out = h->eb[0].y1.p; b.a_ldo = h->eb[0].y1.ld;
       b.W = h->params + d2.off; b.ldw = d2.ldw;
       b.C = h->eb[0].y2.p; b.ldc = h->eb[0].y2.ld;
       b.M = P.Bimg; b.N = d2.fout; b.K = d2.fin + 1;
       b.act = 1;
-      HIPCHK(launch_smallm(h->stream, b));
     } else {
-      CHK(smallm(h, h->eb[0].y1, P.Bimg, h->dense[S0.l2], false, 1, nullptr, h->eb[0].y2));
+      b = smallm_args(h, h->eb[0].y1, P.Bimg, d2, false, 1, nullptr, h->eb[0].y2);
     }
-    CHK(smallm(h, h->eb[0].y2, P.Bimg, h->dense[S0.head], false, 0, nullptr, h->eb[0].P));
+    const SmArgs hd = smallm_args(h, h->eb[0].y2, P.Bimg, h->dense[S0.head], false, 0, nullptr, h->eb[0].P);
+    if (h->sm_pair && smpair_fits(b, hd, h->sm_pair == 2)) {
+      // l2 and head in one launch: every workgroup computes the whole l2 into
+      // its LDS, then its head column tile (no in-launch handoff); bitwise the
+      // two launches below
+      HIPCHK(launch_smpair(h->stream, b, hd, h->sm_pair == 2));
+      h->n_smpair++;
+      return IWAE_OK;
+    }
+    HIPCHK(launch_smallm(h->stream, b));
+    HIPCHK(launch_smallm(h->stream, hd));
   } else
   // (1) first encoder Dense (K = 785) as a split-K GEMM into partial slabs
   {
@@ -3138,6 +3149,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_UPD_APPLY: h->upd_apply = on; break;
     case IWAE_KNOB_STEPS_FIRST: h->steps_first = (int)std::max(0LL, std::min(value, (long long)kGraphSteps)); break;
     case IWAE_KNOB_SM_CHAIN: h->sm_chain = value ? 1 : 0; break;
+    case IWAE_KNOB_SM_PAIR: h->sm_pair = (int)std::max(0LL, std::min(value, 2LL)); break;
     case IWAE_KNOB_DW_SCALE_COST: h->dw_scale_cost = (int)std::max(0LL, std::min(value, 1000LL)); break;
     case IWAE_KNOB_DW_WIDE_COST: h->dw_wide_cost = (int)std::max(0LL, std::min(value, 1000LL)); break;
     case IWAE_KNOB_NRING: h->nring = on; break;
@@ -4021,6 +4033,7 @@ long long iwae_debug_count(const iwae_handle* h, int what) {
       return v[7];
     }
     case 11: return h->n_smchain;
+    case 12: return h->n_smpair;
     default: return -1;
   }
 }

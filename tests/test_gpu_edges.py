@@ -326,34 +326,48 @@ def test_input_gemm_on_the_callers_x_equals_the_staged_copy(B):
             np.testing.assert_array_equal(u, v)
 
 
-@pytest.mark.parametrize("B", [20, 7, 32])
-def test_first_encoder_layer_chain_equals_three_launches(B):
+@pytest.mark.parametrize("B", [20, 7, 32, 16, 17])
+def test_first_encoder_layer_chain_and_pair_equal_three_launches(B):
     """Up to 32 images the first encoder layer (input Dense split over K, l2,
-    head) runs as ONE launch, smchain_kernel: the l2 and head workgroups
-    request their weights first and wait in-launch for the layer before
-    (agent-scope release / counter / acquire).  Same arithmetic and summation
-    order as the three launches (knob sm_chain 0): losses, weights and Adam
-    state equal bit for bit over graph replays with a moving batch (the chained
-    launch re-pointed at each call's x), a multi-step train_steps call and
-    eager steps; no wait gave up (iwae_debug_count 10)."""
+    head) runs on few-row launches.  Two fused forms: smchain_kernel (knob
+    sm_chain: all three layers in ONE launch, the l2 and head workgroups
+    waiting in-launch for the layer before, agent-scope release / counter /
+    acquire) and smpair_kernel (knob sm_pair, the default: l2 and head in one
+    launch, every workgroup computing the whole l2 into its LDS, no handoff).
+    Same arithmetic and summation order as the three launches (both knobs 0):
+    losses, weights and Adam state equal bit for bit over graph replays with a
+    moving batch (the launch that reads x re-pointed at each call's x), a
+    multi-step train_steps call and eager steps; no wait gave up
+    (iwae_debug_count 10); the launch counters (11, 12) show which form ran."""
     import torch
     rng = np.random.default_rng(91 + B)
     xs = (rng.random((6 * B + 5, 784)) < 0.3).astype(np.float32)
     runs = []
-    for chain in (1, 0):
+    for chain, pair in ((1, 0), (0, 1), (0, 0)):
         for graphs in (True, False):
-            m = _model(ARCH2, "IWAE", 50, use_graphs=graphs, tuning={"sm_chain": chain})
+            m = _model(ARCH2, "IWAE", 50, use_graphs=graphs, tuning={"sm_chain": chain, "sm_pair": pair})
             X = torch.from_numpy(xs).to(m.device)
             losses = [m.train_step(X[i * B + i:(i + 1) * B + i])["IWAE"] for i in range(3)]
             losses += list(m.train_steps(X[3 * B + 3:6 * B + 3], B))
             mm, vv, st = m.get_optimizer_state()
             n_chain = m._lib.iwae_debug_count(m._h, 11)
+            n_pair = m._lib.iwae_debug_count(m._h, 12)
             assert (n_chain > 0) == bool(chain), (chain, n_chain)
+            assert (n_pair > 0) == bool(pair), (pair, n_pair)
             assert m._lib.iwae_debug_count(m._h, 10) == 0
             runs.append((np.asarray(losses, np.float32), _flat(m.get_weights()), mm, vv))
     for r in runs[1:]:
         for u, v in zip(runs[0], r):
             np.testing.assert_array_equal(u, v)
+    # sm_pair 2: the pair launch with l2's products in bf16x3 (the engine's
+    # arithmetic): close to the exact-f32 runs, not bitwise
+    m = _model(ARCH2, "IWAE", 50, tuning={"sm_chain": 0, "sm_pair": 2})
+    X = torch.from_numpy(xs).to(m.device)
+    losses = [m.train_step(X[i * B + i:(i + 1) * B + i])["IWAE"] for i in range(3)]
+    losses += list(m.train_steps(X[3 * B + 3:6 * B + 3], B))
+    assert m._lib.iwae_debug_count(m._h, 12) > 0
+    np.testing.assert_allclose(np.asarray(losses, np.float32), runs[0][0], rtol=2e-5)
+    np.testing.assert_allclose(_flat(m.get_weights()), runs[0][1], rtol=0, atol=2e-5)
 
 
 def test_train_steps_losses_copy_node_repointed_and_null():
