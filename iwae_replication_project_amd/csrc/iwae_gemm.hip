@@ -648,6 +648,9 @@ static hipError_t dispatch_tile(hipStream_t st, GemmKind kind, GemmEpi epi, int 
 // 16-byte LDS read feeds 4 MFMAs and, for bt = 1, one 16-byte weight load does.
 constexpr int SM_WAVES = 8;
 constexpr int SM_MAXU = 8;          // 16-deep k groups per wave (K <= 8 * 16 * 8 = 1024)
+#ifndef IWAE_SM_NARROW
+#define IWAE_SM_NARROW 1            // launches with K <= 256 per workgroup on the MU = 2 instantiation
+#endif
 constexpr int SM_MAX_ASLABS = 4;    // partial slabs a reader sums while staging A
 
 // Every load of a phase is issued before the first wait: the weight fragments
@@ -700,13 +703,16 @@ __device__ __forceinline__ void sm_publish(const SmChainArgs& c, int stage) {
 // A's rows -> LDS As[32][lds_ld] (rows >= M and k >= K zero; partial slabs summed,
 // activation and ones column applied when a_slabs > 0): one workgroup's K range
 // [kb0, kb0 + Kb) of column tile t, slab ks (t == 0 && ks == 0 write a_out / a_copy)
+template <int SL = 0>
 __device__ __forceinline__ void sm_stage(const SmArgs& a, int t, int ks, float* As, int kb0, int Kb, int Kp,
                                          int lds_ld) {
   const __amdgpu_buffer_rsrc_t rA = a.a_bytes ? buf_rsrc(a.A, a.a_bytes) : buf_rsrc(a.A);
   const int q4 = Kp >> 2;
   const int nq = 32 * q4;
   const bool write_a = a.a_out != nullptr && t == 0 && ks == 0;
-  const int nsl = a.a_slabs;
+  // (SL 1 / 2: the launch's A is known to be direct rows / partial slabs)
+  const int nsl = SL == 1 ? 0 : a.a_slabs;
+  constexpr int NSL = SL == 1 ? 1 : SM_MAX_ASLABS;
   for (int e0 = threadIdx.x; e0 < nq; e0 += SM_STAGE * blockDim.x) {
     // the batch's loads (every slab of every quad) first
     float4 w[SM_STAGE][SM_MAX_ASLABS];
@@ -717,7 +723,7 @@ __device__ __forceinline__ void sm_stage(const SmArgs& a, int t, int ks, float* 
       const int k = 4 * kq, gk = kb0 + k;
       const bool in = e < nq && row < a.M && k < Kb;
 #pragma unroll
-      for (int sl = 0; sl < SM_MAX_ASLABS; ++sl) {
+      for (int sl = 0; sl < NSL; ++sl) {
         const bool used = nsl > 0 ? sl < nsl : sl == 0;
         w[i][sl] = bld4(rA, (used && in) ? (unsigned)(sl * a.a_slab + row * a.lda + gk) * 4u : kOOB);
       }
@@ -729,11 +735,11 @@ __device__ __forceinline__ void sm_stage(const SmArgs& a, int t, int ks, float* 
       const int row = e / q4, kq = e - row * q4;
       const int k = 4 * kq, gk = kb0 + k;
       float4 v;
-      if (nsl > 0) {
+      if (SL != 1 && (SL == 2 || nsl > 0)) {
         // sum of the producer's partial slabs, activation, ones column at K - 1
         float4 sacc = w[i][0];
 #pragma unroll
-        for (int sl = 1; sl < SM_MAX_ASLABS; ++sl) {
+        for (int sl = 1; sl < NSL; ++sl) {
           sacc.x += w[i][sl].x; sacc.y += w[i][sl].y; sacc.z += w[i][sl].z; sacc.w += w[i][sl].w;
         }
         float vv[4] = {sacc.x, sacc.y, sacc.z, sacc.w};
@@ -775,7 +781,7 @@ __device__ __forceinline__ void sm_stage(const SmArgs& a, int t, int ks, float* 
 
 // one workgroup (column tile t, K slab ks) of a few-row Dense; ch: the chain it
 // is stage `stage` of (nullptr: a plain smallm_kernel launch)
-template <bool BT>
+template <bool BT, int MU = SM_MAXU, int SL = 0>
 __device__ __forceinline__ void smallm_body(const SmArgs& a, int t, int ks, float* sm_lds, const SmChainArgs* ch,
                                             int stage) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -790,12 +796,12 @@ __device__ __forceinline__ void smallm_body(const SmArgs& a, int t, int ks, floa
   float* part = sm_lds + 32 * lds_ld;                  // [wave][rt][i][lane]
   const int kc = (((Kb + SM_WAVES - 1) / SM_WAVES) + 15) & ~15;
   const int kb = wave * kc;
-  const int nu = min(SM_MAXU, max(0, (min(kc, Kp - kb) + 15) >> 4));
+  const int nu = min(MU, max(0, (min(kc, Kp - kb) + 15) >> 4));
   // weights of this wave's k range, requested first (they do not depend on A)
   const __amdgpu_buffer_rsrc_t rW = buf_rsrc(a.W);
-  float4 bq[SM_MAXU];
+  float4 bq[MU];
 #pragma unroll
-  for (int u = 0; u < SM_MAXU; ++u) {
+  for (int u = 0; u < MU; ++u) {
     const int k0 = kb + 16 * u + 4 * g;
     const bool ok = u < nu && n < a.N;
     if (BT) {
@@ -812,13 +818,13 @@ __device__ __forceinline__ void smallm_body(const SmArgs& a, int t, int ks, floa
   // (chained: the activations are the previous stage's output)
   if (ch && stage > 0) sm_wait(*ch, stage);
   // activations -> LDS (rows >= M and k >= K zero)
-  sm_stage(a, t, ks, As, kb0, Kb, Kp, lds_ld);
+  sm_stage<SL>(a, t, ks, As, kb0, Kb, Kp, lds_ld);
   __syncthreads();
   typedef float f4v __attribute__((ext_vector_type(4)));
   f4v c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
   const bool two = a.M > 16;
 #pragma unroll
-  for (int u = 0; u < SM_MAXU; ++u) {
+  for (int u = 0; u < MU; ++u) {
     if (u >= nu) break;
     const int k0 = kb + 16 * u + 4 * g;
     const float4 a0 = *reinterpret_cast<const float4*>(&As[r * lds_ld + k0]);
@@ -861,10 +867,13 @@ __device__ __forceinline__ void smallm_body(const SmArgs& a, int t, int ks, floa
   if (ch && stage < ch->nstage - 1) sm_publish(*ch, stage);
 }
 
-template <bool BT>
+// MU: 16-deep k groups per wave the instantiation unrolls (2: K <= 256 per
+// workgroup, every few-row launch of the paper's shapes; a third of the code of
+// the MU = 8 form)
+template <bool BT, int MU, int SL>
 __global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm_lds[];
-  smallm_body<BT>(a, blockIdx.x, blockIdx.y, sm_lds, nullptr, 0);
+  smallm_body<BT, MU, SL>(a, blockIdx.x, blockIdx.y, sm_lds, nullptr, 0);
 }
 
 // the first encoder layer's forward (input Dense, l2, head) as one launch
@@ -889,7 +898,8 @@ constexpr int SP_MAXU = 2;           // 16-deep k groups per wave (K <= 256)
 constexpr int SP_TB = 4;             // l2 tiles reduced per LDS round
 constexpr int SP_KS = 7;             // X3: 32-deep k steps of l2 (K <= 224)
 #ifndef IWAE_SP_ABL
-#define IWAE_SP_ABL 0                // timing ablation (debug builds, WRONG results): 1 no l2 MFMAs
+#define IWAE_SP_ABL 0                // timing ablation (debug builds, WRONG results): 1 no l2 MFMAs (f32),
+                                     // 2 no l2 weight loads (bf16x3), 4 no staging of l2's A
 #endif
 
 template <bool X3>
@@ -914,18 +924,22 @@ __global__ __launch_bounds__(SM_WAVES * 64) void smpair_kernel(SmArgs l2, SmArgs
   // 8 k values of each 32-deep step of its two column tiles), the head's tile
   const __amdgpu_buffer_rsrc_t rW = buf_rsrc(l2.W), rH = buf_rsrc(hd.W);
   float4 bq[SP_NT][SP_MAXU], bh[SP_MAXU];
-  float bx[2][SP_KS][8];
+  typedef unsigned sp_u32x4 __attribute__((ext_vector_type(4)));
+  sp_u32x4 bxh[2][SP_KS], bxl[2][SP_KS];
   if constexpr (X3) {
+    // B fragments straight from the FX copy: one 16-byte load per lane and
+    // plane per (column tile, k step), 1 KiB contiguous per wave instruction
+    const __amdgpu_buffer_rsrc_t rxh = buf_rsrc(l2.wx_hi), rxl = buf_rsrc(l2.wx_lo);
+    const int nst = Kp >> 5;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const int n = (wave + 8 * q) * 16 + r;
+      const int ct = wave + 8 * q;
 #pragma unroll
-      for (int st = 0; st < SP_KS; ++st)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = 32 * st + 8 * g + j;
-          bx[q][st][j] = bld1(rW, (n < l2.N && k < Kb) ? (unsigned)(k * l2.ldw + n) * 4u : kOOB);
-        }
+      for (int st = 0; st < SP_KS; ++st) {
+        const unsigned o = (ct < nt2 && st < nst && !(IWAE_SP_ABL & 2)) ? (unsigned)(((ct * l2.wx_steps + st) * 64 + lane) * 16) : kOOB;
+        bxh[q][st] = __builtin_amdgcn_raw_buffer_load_b128(rxh, o, 0, 0);
+        bxl[q][st] = __builtin_amdgcn_raw_buffer_load_b128(rxl, o, 0, 0);
+      }
     }
   } else {
 #pragma unroll
@@ -955,7 +969,7 @@ __global__ __launch_bounds__(SM_WAVES * 64) void smpair_kernel(SmArgs l2, SmArgs
     }
   }
   // l2's activations (workgroup 0 writes y1 while staging)
-  sm_stage(l2, t, 0, As, 0, Kb, Kp, lds_ld);
+  if (!(IWAE_SP_ABL & 4)) sm_stage(l2, t, 0, As, 0, Kb, Kp, lds_ld);
   // the head's A past l2's tiles: ones column at K2 - 1, zeros after
   for (int e = threadIdx.x; e < 32 * Kp2; e += blockDim.x) {
     const int row = e / Kp2, k = e - row * Kp2;
@@ -990,11 +1004,8 @@ __global__ __launch_bounds__(SM_WAVES * 64) void smpair_kernel(SmArgs l2, SmArgs
       }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        bf16x4 h0, l0, h1, l1;
-        split4(make_float4(bx[q][st][0], bx[q][st][1], bx[q][st][2], bx[q][st][3]), h0, l0);
-        split4(make_float4(bx[q][st][4], bx[q][st][5], bx[q][st][6], bx[q][st][7]), h1, l1);
-        const bf16x8 bh8 = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-        const bf16x8 bl8 = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+        const bf16x8 bh8 = __builtin_bit_cast(bf16x8, bxh[q][st]);
+        const bf16x8 bl8 = __builtin_bit_cast(bf16x8, bxl[q][st]);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           if (h == 1 && !two) break;
@@ -1113,7 +1124,8 @@ static size_t smpair_lds(const SmArgs& l2, const SmArgs& hd) {
 }
 
 bool smpair_fits(const SmArgs& l2, const SmArgs& hd, bool x3) {
-  if (x3 && (l2.K > 32 * SP_KS || l2.N > 16 * 16)) return false;
+  if (x3 && (l2.K > 32 * SP_KS || l2.N > 16 * 16 || !l2.wx_hi || !l2.wx_lo || (l2.K + 31) / 32 > l2.wx_steps))
+    return false;
   return !l2.bt && !hd.bt && l2.kslabs <= 1 && hd.kslabs <= 1 && hd.a_slabs == 0 && l2.act == 1 && hd.act == 0 &&
          l2.M > 0 && l2.M <= 32 && hd.M == l2.M && l2.N > 0 && l2.N <= 16 * SP_NT && hd.N > 0 && hd.K == l2.N + 1 &&
          l2.K <= SM_WAVES * 16 * SP_MAXU && hd.K <= SM_WAVES * 16 * SP_MAXU && l2.a_slabs <= SM_MAX_ASLABS &&
@@ -1136,10 +1148,15 @@ hipError_t launch_smallm(hipStream_t st, const SmArgs& a) {
   if (a.M > 32 || KC > SM_WAVES * 16 * SM_MAXU || a.a_slabs > SM_MAX_ASLABS) return hipErrorInvalidValue;
   const int Kp = (KC + 15) & ~15;
   const size_t lds = (size_t)(32 * (Kp + 4) + SM_WAVES * 2 * 4 * 64) * sizeof(float);
-  if (a.bt)
-    hipLaunchKernelGGL(smallm_kernel<true>, dim3((a.N + 15) / 16, ksl), dim3(SM_WAVES * 64), lds, st, a);
-  else
-    hipLaunchKernelGGL(smallm_kernel<false>, dim3((a.N + 15) / 16, ksl), dim3(SM_WAVES * 64), lds, st, a);
+  const dim3 grid((a.N + 15) / 16, ksl), blk(SM_WAVES * 64);
+  if (IWAE_SM_NARROW && KC <= SM_WAVES * 16 * 2) {
+    if (a.bt) hipLaunchKernelGGL((smallm_kernel<true, 2, 0>), grid, blk, lds, st, a);
+    else if (a.a_slabs > 0) hipLaunchKernelGGL((smallm_kernel<false, 2, 2>), grid, blk, lds, st, a);
+    else hipLaunchKernelGGL((smallm_kernel<false, 2, 1>), grid, blk, lds, st, a);
+  } else {
+    if (a.bt) hipLaunchKernelGGL((smallm_kernel<true, SM_MAXU, 0>), grid, blk, lds, st, a);
+    else hipLaunchKernelGGL((smallm_kernel<false, SM_MAXU, 0>), grid, blk, lds, st, a);
+  }
   return hipGetLastError();
 }
 
@@ -1178,11 +1195,13 @@ hipError_t smallm_setup_attributes() {
   hipError_t e0 = hipFuncSetAttribute((const void*)smchain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024);
   if (e0 != hipSuccess) return e0;
-  hipError_t e = hipFuncSetAttribute((const void*)smallm_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     160 * 1024);
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)smallm_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             160 * 1024);
+  for (const void* f : {(const void*)smallm_kernel<true, SM_MAXU, 0>, (const void*)smallm_kernel<false, SM_MAXU, 0>,
+                        (const void*)smallm_kernel<true, 2, 0>, (const void*)smallm_kernel<false, 2, 1>,
+                        (const void*)smallm_kernel<false, 2, 2>}) {
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_gemm(hipStream_t st, GemmKind kind, GemmEpi epi, int tile, int splits, bool ks,

@@ -190,6 +190,9 @@ struct SmArgs {
   // workgroups of column tile 0 also store the staged rows (ones column
   // included) to a_copy for the later readers of A
   int a_ones; unsigned a_bytes; float* a_copy; int a_copy_ld;
+  // the layer's fragment-major split copy (FX: hi / lo planes, wx_steps 32-deep
+  // k steps per 16-column tile; smpair_kernel's bf16x3 form reads its B there)
+  const __bf16* wx_hi; const __bf16* wx_lo; int wx_steps;
 };
 hipError_t launch_smallm(hipStream_t st, const SmArgs& a);
 // l2 (bt 0, tanh) and the head (act 0, K = l2.N + 1) of the first encoder

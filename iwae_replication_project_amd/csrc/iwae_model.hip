@@ -1197,6 +1197,7 @@ static int enc0_forward(iwae_handle* h, const Plan& P, bool l1_only = false) {
     } else {
       b = smallm_args(h, h->eb[0].y1, P.Bimg, d2, false, 1, nullptr, h->eb[0].y2);
     }
+    b.wx_hi = h->fx_hi + d2.fx_off; b.wx_lo = h->fx_lo + d2.fx_off; b.wx_steps = d2.fx_steps;
     const SmArgs hd = smallm_args(h, h->eb[0].y2, P.Bimg, h->dense[S0.head], false, 0, nullptr, h->eb[0].P);
     if (h->sm_pair && smpair_fits(b, hd, h->sm_pair == 2)) {
       // l2 and head in one launch: every workgroup computes the whole l2 into

@@ -360,14 +360,16 @@ def test_first_encoder_layer_chain_and_pair_equal_three_launches(B):
         for u, v in zip(runs[0], r):
             np.testing.assert_array_equal(u, v)
     # sm_pair 2: the pair launch with l2's products in bf16x3 (the engine's
-    # arithmetic): close to the exact-f32 runs, not bitwise
+    # arithmetic, B fragments from the FX copy): close to the exact-f32 runs,
+    # not bitwise (Adam's first steps move a weight by up to lr wherever its
+    # gradient is near zero, so the weights get lr-scale slack)
     m = _model(ARCH2, "IWAE", 50, tuning={"sm_chain": 0, "sm_pair": 2})
     X = torch.from_numpy(xs).to(m.device)
     losses = [m.train_step(X[i * B + i:(i + 1) * B + i])["IWAE"] for i in range(3)]
     losses += list(m.train_steps(X[3 * B + 3:6 * B + 3], B))
     assert m._lib.iwae_debug_count(m._h, 12) > 0
     np.testing.assert_allclose(np.asarray(losses, np.float32), runs[0][0], rtol=2e-5)
-    np.testing.assert_allclose(_flat(m.get_weights()), runs[0][1], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(_flat(m.get_weights()), runs[0][1], rtol=0, atol=1e-3)
 
 
 def test_train_steps_losses_copy_node_repointed_and_null():

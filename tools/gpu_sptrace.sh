@@ -10,7 +10,7 @@ n=0
 for lib in "" "$@"; do
   if [ -n "$lib" ]; then export IWAE_HIP_LIB=$lib; else unset IWAE_HIP_LIB; fi
   timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/p$n -o run -- \
-    python -u tools/steps_b20.py 64 > $O/p$n.log 2>&1 || exit $?
+    python -u tools/steps_b20.py 64 ${SP_TUNE:-} > $O/p$n.log 2>&1 || exit $?
   F=$(find $O/p$n -name "*kernel_trace.csv" | head -1)
   echo "== ${lib:-in-tree}"; python tools/kernel_by_grid.py "$F" | head -12
   n=$((n+1))
