@@ -23,6 +23,6 @@ python tools/pmc_to_json.py $O/pmc "tc_kernel<" $J "tc_kernel backward (train en
 python tools/pmc_to_json.py $O/pmc "upd_kernel" $J "upd_kernel (weight gradients + Adam + FX copies, bf16x3)" max &&
 python tools/pmc_to_json.py $O/pmc "tcu_kernel" $J "tcu_kernel (job I' + weight gradients + Adam + FX copies, one launch)" max &&
 python tools/pmc_summary.py $O/pmc > $O/pmc_summary.txt &&
-PROF_OUT=$O/pstep NK=7 FIRST="smallm_kernel<false>@52" bash tools/prof_step.sh > /dev/null
+PROF_OUT=$O/pstep NK=7 FIRST="smallm_kernel<false, 2, 1>@52" bash tools/prof_step.sh > /dev/null
 T=$(find $O/prof -name "*kernel_trace.csv" | head -1); python tools/kernel_by_grid.py "$T" > $O/kernel_by_grid.txt
 echo measure done
