@@ -700,8 +700,17 @@ struct TcPlan {              // device resident (built once per shape)
   TcJob job[kTcMaxJobs]; int njobs;
   int acc_off;               // float offset of the per-row accumulators + reduction scratch
 };
+// op kinds an engine launch's plan uses (bit 1 << TcKind): the launch picks the
+// kernel instantiation compiled for the smallest of these sets that covers them
+// (fewer epilogue kinds inlined at the op loop's call sites: less code to fetch)
+constexpr unsigned kTcKindsFwd = (1u << TC_TANH) | (1u << TC_SAMPLE) | (1u << TC_PRIOR) | (1u << TC_BERN) |
+                                 (1u << TC_HEADP) | (1u << TC_SAMPLE0) | (1u << TC_LOADSLAB);
+constexpr unsigned kTcKindsBwd = (1u << TC_TGRAD) | (1u << TC_LIN) | (1u << TC_GBWD_PRIOR) | (1u << TC_GBWD_ENC) |
+                                 (1u << TC_LOADG) | (1u << TC_GBWD0);
+constexpr unsigned kTcKindsAll = 0x1FFFu;
 struct TcArgs {
   const TcPlan* plan;
+  unsigned kinds;             // op kinds of the plan's jobs (host-computed; 0: all)
   int block_start[kTcMaxJobs + 1];
   int rows, kS;
   int row_step;                             // rows per workgroup (0: 16 * RT; image-row launches: 1)

@@ -187,6 +187,7 @@ struct iwae_handle {
     size_t lds = 0;
     int acc_off = 0;                 // float offset of the per-row accumulators in LDS
     double flop = 0.0;               // algorithmic FLOPs of one launch (weight products, no bias rows)
+    unsigned kinds = 0;              // op kinds of the plan's jobs (TcArgs::kinds)
   };
   std::map<std::vector<long long>, TcRec> tc_plans;
   int engine = 1;                    // train step on the row-chain engine when it applies (iwae_set_path)
@@ -2149,7 +2150,10 @@ static int tc_prepare_one(iwae_handle* h, const Plan& P, int which) {
       std::memset(&plan, 0, sizeof(plan));
       plan.njobs = (int)jobs.size();
       plan.acc_off = acc_off;
-      for (size_t j = 0; j < jobs.size(); ++j) plan.job[j] = jobs[j].J;
+      for (size_t j = 0; j < jobs.size(); ++j) {
+        plan.job[j] = jobs[j].J;
+        for (int o = 0; o < jobs[j].J.nop; ++o) rec.kinds |= 1u << jobs[j].J.op[o].kind;
+      }
       HIPCHK(hipMalloc(&rec.dev, sizeof(TcPlan)));
       HIPCHK(hipMemcpy(rec.dev, &plan, sizeof(TcPlan), hipMemcpyHostToDevice));
       const int nb = (int)cdiv(rows, row_step > 0 ? row_step : 16 * rt);
@@ -2191,6 +2195,7 @@ static int tc_run(iwae_handle* h, const Plan& P, const EpsSet& E, int which, con
   TcArgs a;
   std::memset(&a, 0, sizeof(a));
   a.plan = rec.dev;
+  a.kinds = rec.kinds;
   int tot = 0;
   for (int j = 0; j < kTcMaxJobs; ++j) {
     a.block_start[j] = tot;

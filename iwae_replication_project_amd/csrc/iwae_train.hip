@@ -33,6 +33,10 @@
 #include "iwae_bound.h"
 #include "iwae_update_dev.h"
 
+#ifndef IWAE_TC_KM
+#define IWAE_TC_KM 1          // engine launches on the instantiation of their plan's op-kind set (0: all kinds)
+#endif
+
 namespace iwae {
 
 typedef float tc_f32x4 __attribute__((ext_vector_type(4)));
@@ -612,7 +616,7 @@ __device__ __forceinline__ int tc_prefetch(COp& Sn, TcSets& F) {
 // epilogue switches on the kind).  npre: how many of the op's first units (in
 // X, Y) the previous op already requested; Sn: the next op when it is a Dense
 // op whose first units this op requests.  Returns the next op's npre.
-template <int RT>
+template <int RT, unsigned KM = kTcKindsAll>
 __device__ __forceinline__ int tc_dense(const TcArgs& A, CJob& J, COp& S, const int kind, uint64_t base,
                                         TcRows<RT>& R, int row0, int nrows, TcSets& F, int npre, COp* Sn,
                                         int utr = -1) {
@@ -647,9 +651,9 @@ __device__ __forceinline__ int tc_dense(const TcArgs& A, CJob& J, COp& S, const 
 #endif
     if (x.first) {
       switch (kind) {
-        case TC_BERN: tc_epi_loads<RT, TC_BERN>(A, S, x.t, R, row0, nrows, ov, tv); break;
-        case TC_TGRAD: tc_epi_loads<RT, TC_TGRAD>(A, S, x.t, R, row0, nrows, ov, tv); break;
-        case TC_PRIOR: tc_epi_loads<RT, TC_PRIOR>(A, S, x.t, R, row0, nrows, ov, tv); break;
+        case TC_BERN: if constexpr ((KM >> TC_BERN) & 1u) tc_epi_loads<RT, TC_BERN>(A, S, x.t, R, row0, nrows, ov, tv); break;
+        case TC_TGRAD: if constexpr ((KM >> TC_TGRAD) & 1u) tc_epi_loads<RT, TC_TGRAD>(A, S, x.t, R, row0, nrows, ov, tv); break;
+        case TC_PRIOR: if constexpr ((KM >> TC_PRIOR) & 1u) tc_epi_loads<RT, TC_PRIOR>(A, S, x.t, R, row0, nrows, ov, tv); break;
         default: break;
       }
 #pragma unroll
@@ -681,13 +685,13 @@ __device__ __forceinline__ int tc_dense(const TcArgs& A, CJob& J, COp& S, const 
     if (x.last) {
 #endif
       switch (kind) {
-        case TC_TANH: tc_epilogue<RT, TC_TANH>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        case TC_TGRAD: tc_epilogue<RT, TC_TGRAD>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        case TC_LIN: tc_epilogue<RT, TC_LIN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        case TC_BERN: tc_epilogue<RT, TC_BERN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        case TC_SAMPLE: tc_epilogue<RT, TC_SAMPLE>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        case TC_HEADP: tc_epilogue<RT, TC_HEADP>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        default: tc_epilogue<RT, TC_PRIOR>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_TANH: if constexpr ((KM >> TC_TANH) & 1u) tc_epilogue<RT, TC_TANH>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_TGRAD: if constexpr ((KM >> TC_TGRAD) & 1u) tc_epilogue<RT, TC_TGRAD>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_LIN: if constexpr ((KM >> TC_LIN) & 1u) tc_epilogue<RT, TC_LIN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_BERN: if constexpr ((KM >> TC_BERN) & 1u) tc_epilogue<RT, TC_BERN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_SAMPLE: if constexpr ((KM >> TC_SAMPLE) & 1u) tc_epilogue<RT, TC_SAMPLE>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_HEADP: if constexpr ((KM >> TC_HEADP) & 1u) tc_epilogue<RT, TC_HEADP>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        default: if constexpr ((KM >> TC_PRIOR) & 1u) tc_epilogue<RT, TC_PRIOR>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
       }
     }
 #ifdef IWAE_TC_TRACE
@@ -715,7 +719,7 @@ __device__ __forceinline__ int tc_dense(const TcArgs& A, CJob& J, COp& S, const 
 // so both stay statically named), unit u + 1 is requested before unit u is
 // multiplied.  No cross-op prefetch (the four-set pipeline of tc_dense spills
 // at these tile counts); an op's first unit waits one round trip.
-template <int RT>
+template <int RT, unsigned KM = kTcKindsAll>
 __device__ __forceinline__ void tc_dense2(const TcArgs& A, CJob& J, COp& S, const int kind, uint64_t base,
                                          TcRows<RT>& R, int row0, int nrows) {
   const TcStream q = tc_stream(S);
@@ -731,9 +735,9 @@ __device__ __forceinline__ void tc_dense2(const TcArgs& A, CJob& J, COp& S, cons
     const TcUnit x = tc_unit(S, u, q.nch);
     if (x.first) {
       switch (kind) {
-        case TC_BERN: tc_epi_loads<RT, TC_BERN>(A, S, x.t, R, row0, nrows, ov, tv); break;
-        case TC_TGRAD: tc_epi_loads<RT, TC_TGRAD>(A, S, x.t, R, row0, nrows, ov, tv); break;
-        case TC_PRIOR: tc_epi_loads<RT, TC_PRIOR>(A, S, x.t, R, row0, nrows, ov, tv); break;
+        case TC_BERN: if constexpr ((KM >> TC_BERN) & 1u) tc_epi_loads<RT, TC_BERN>(A, S, x.t, R, row0, nrows, ov, tv); break;
+        case TC_TGRAD: if constexpr ((KM >> TC_TGRAD) & 1u) tc_epi_loads<RT, TC_TGRAD>(A, S, x.t, R, row0, nrows, ov, tv); break;
+        case TC_PRIOR: if constexpr ((KM >> TC_PRIOR) & 1u) tc_epi_loads<RT, TC_PRIOR>(A, S, x.t, R, row0, nrows, ov, tv); break;
         default: break;
       }
 #pragma unroll
@@ -745,13 +749,13 @@ __device__ __forceinline__ void tc_dense2(const TcArgs& A, CJob& J, COp& S, cons
     tc_mma<RT>(IN, x.k0, x.ns, cur, acc);
     if (x.last) {
       switch (kind) {
-        case TC_TANH: tc_epilogue<RT, TC_TANH>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        case TC_TGRAD: tc_epilogue<RT, TC_TGRAD>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        case TC_LIN: tc_epilogue<RT, TC_LIN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        case TC_BERN: tc_epilogue<RT, TC_BERN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        case TC_SAMPLE: tc_epilogue<RT, TC_SAMPLE>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        case TC_HEADP: tc_epilogue<RT, TC_HEADP>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        default: tc_epilogue<RT, TC_PRIOR>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_TANH: if constexpr ((KM >> TC_TANH) & 1u) tc_epilogue<RT, TC_TANH>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_TGRAD: if constexpr ((KM >> TC_TGRAD) & 1u) tc_epilogue<RT, TC_TGRAD>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_LIN: if constexpr ((KM >> TC_LIN) & 1u) tc_epilogue<RT, TC_LIN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_BERN: if constexpr ((KM >> TC_BERN) & 1u) tc_epilogue<RT, TC_BERN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_SAMPLE: if constexpr ((KM >> TC_SAMPLE) & 1u) tc_epilogue<RT, TC_SAMPLE>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_HEADP: if constexpr ((KM >> TC_HEADP) & 1u) tc_epilogue<RT, TC_HEADP>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        default: if constexpr ((KM >> TC_PRIOR) & 1u) tc_epilogue<RT, TC_PRIOR>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
       }
     }
   };
@@ -1114,7 +1118,7 @@ __device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int r
 }
 
 // ----------------------------------------------------------------- kernel
-template <int RT>
+template <int RT, unsigned KM = kTcKindsAll>
 __device__ __forceinline__ void tc_body(const TcArgs& A, const int bid) {
   constexpr int R = 16 * RT;
   CPlan* plan = (CPlan*)A.plan;
@@ -1222,18 +1226,18 @@ __device__ __forceinline__ void tc_body(const TcArgs& A, const int bid) {
       case TC_TGRAD:
       case TC_LIN:
       case TC_HEADP:
-        if constexpr (RT == 1) nx = tc_dense<RT>(A, J, S, kind, base, Rw, r0, nr, F, npre, Sn, UTR);
-        else tc_dense2<RT>(A, J, S, kind, base, Rw, r0, nr);
+        if constexpr (RT == 1) nx = tc_dense<RT, KM>(A, J, S, kind, base, Rw, r0, nr, F, npre, Sn, UTR);
+        else tc_dense2<RT, KM>(A, J, S, kind, base, Rw, r0, nr);
         break;
 #ifdef IWAE_TC_SKIPELEM    // timing experiment only
       default: break;
 #else
-      case TC_SAMPLE0: tc_sample0<RT>(A, J, S, base, row0, nrows, rq, rp); break;
-      case TC_GBWD_PRIOR: tc_gbwd<RT, TC_GBWD_PRIOR>(A, J, S, row0, nrows); break;
-      case TC_GBWD_ENC: tc_gbwd<RT, TC_GBWD_ENC>(A, J, S, row0, nrows); break;
-      case TC_LOADG: tc_loadg<RT>(A, J, S, row0, nrows); break;
-      case TC_LOADSLAB: tc_loadslab<RT>(J, S, r0, nr); break;
-      default: tc_gbwd0<RT>(A, J, S, row0, nrows); break;
+      case TC_SAMPLE0: if constexpr ((KM >> TC_SAMPLE0) & 1u) tc_sample0<RT>(A, J, S, base, row0, nrows, rq, rp); break;
+      case TC_GBWD_PRIOR: if constexpr ((KM >> TC_GBWD_PRIOR) & 1u) tc_gbwd<RT, TC_GBWD_PRIOR>(A, J, S, row0, nrows); break;
+      case TC_GBWD_ENC: if constexpr ((KM >> TC_GBWD_ENC) & 1u) tc_gbwd<RT, TC_GBWD_ENC>(A, J, S, row0, nrows); break;
+      case TC_LOADG: if constexpr ((KM >> TC_LOADG) & 1u) tc_loadg<RT>(A, J, S, row0, nrows); break;
+      case TC_LOADSLAB: if constexpr ((KM >> TC_LOADSLAB) & 1u) tc_loadslab<RT>(J, S, r0, nr); break;
+      default: if constexpr ((KM >> TC_GBWD0) & 1u) tc_gbwd0<RT>(A, J, S, row0, nrows); break;
 #endif
     }
 #ifdef IWAE_TC_TRACE
@@ -1280,12 +1284,12 @@ __device__ __forceinline__ void tc_body(const TcArgs& A, const int bid) {
   }
 }
 
-template <int RT>
+template <int RT, unsigned KM>
 __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
 #ifdef IWAE_PS_TC     // experiment: one wave per SIMD (waves 0-3) at raised priority, so the SIMD's two waves drift apart
   if ((threadIdx.x >> 6) < 4) __builtin_amdgcn_s_setprio(IWAE_PS_TC);
 #endif
-  tc_body<RT>(A, (int)blockIdx.x);
+  tc_body<RT, KM>(A, (int)blockIdx.x);
 }
 
 // The first encoder layer's image-row backward (job I', one row tile per
@@ -1295,6 +1299,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
 // blocks from n_tc_pad run upd_kernel's body, whose first-encoder-layer tiles
 // (the jobs in W.wait_mask) wait on that counter -- the sample-row tiles, the
 // bulk of the launch, run beside job I' instead of after it.
+template <unsigned KM>
 __global__ __launch_bounds__(TC_NW * 64) void tcu_kernel(TcArgs A, UpdArgs U, UpdWait W, int n_tc, int n_tc_pad) {
   const int b = (int)blockIdx.x;
 #ifdef IWAE_TCU_TRACE
@@ -1302,7 +1307,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tcu_kernel(TcArgs A, UpdArgs U, Up
 #endif
   if (b < n_tc_pad) {
     if (b >= n_tc) return;
-    tc_body<1>(A, b);
+    tc_body<1, KM>(A, b);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's stores done
     __syncthreads();
 #ifdef IWAE_TCU_TRACE
@@ -1329,25 +1334,39 @@ hipError_t launch_tcu(hipStream_t st, const TcArgs& a, const UpdArgs& u, const U
   const int n_tc = a.block_start[kTcMaxJobs];
   const int n_pad = (n_tc + 7) & ~7;                      // the update's blocks keep their b % 8 XCD groups
   const int grid = n_pad + 8 * (u.per_xcd + u.per_xcd2);
-  hipLaunchKernelGGL(tcu_kernel, dim3(grid), dim3(TC_NW * 64), lds_bytes, st, a, u, w, n_tc, n_pad);
+  if (IWAE_TC_KM && a.kinds && !(a.kinds & ~kTcKindsBwd))
+    hipLaunchKernelGGL((tcu_kernel<kTcKindsBwd>), dim3(grid), dim3(TC_NW * 64), lds_bytes, st, a, u, w, n_tc, n_pad);
+  else
+    hipLaunchKernelGGL((tcu_kernel<kTcKindsAll>), dim3(grid), dim3(TC_NW * 64), lds_bytes, st, a, u, w, n_tc, n_pad);
   return hipGetLastError();
 }
 
 hipError_t launch_tc(hipStream_t st, const TcArgs& a, int rt, size_t lds_bytes) {
   const int nb = (a.xcd_slots > 0 ? 8 * a.xcd_slots : a.block_start[kTcMaxJobs]) + (a.bnd_block >= 0 ? 1 : 0);
   if (nb <= 0) return hipSuccess;
+  // the smallest compiled op-kind set covering the plan's (IWAE_TC_KM 0: always all)
+  const int km = (IWAE_TC_KM && a.kinds) ? (!(a.kinds & ~kTcKindsFwd) ? 1 : !(a.kinds & ~kTcKindsBwd) ? 2 : 0) : 0;
+#define TC_LAUNCH(R)                                                                                           \
+  if (km == 1) hipLaunchKernelGGL((tc_kernel<R, kTcKindsFwd>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a); \
+  else if (km == 2) hipLaunchKernelGGL((tc_kernel<R, kTcKindsBwd>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a); \
+  else hipLaunchKernelGGL((tc_kernel<R, kTcKindsAll>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a);
   switch (rt) {
-    case 1: hipLaunchKernelGGL((tc_kernel<1>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a); break;
-    case 2: hipLaunchKernelGGL((tc_kernel<2>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a); break;
-    case 4: hipLaunchKernelGGL((tc_kernel<4>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a); break;
+    case 1: TC_LAUNCH(1); break;
+    case 2: TC_LAUNCH(2); break;
+    case 4: TC_LAUNCH(4); break;
     default: return hipErrorInvalidValue;
   }
+#undef TC_LAUNCH
   return hipGetLastError();
 }
 
 hipError_t tc_setup_attributes() {
-  const void* fns[] = {(const void*)tc_kernel<1>, (const void*)tc_kernel<2>, (const void*)tc_kernel<4>,
-                       (const void*)tcu_kernel};
+  const void* fns[] = {(const void*)tc_kernel<1, kTcKindsAll>, (const void*)tc_kernel<2, kTcKindsAll>,
+                       (const void*)tc_kernel<4, kTcKindsAll>, (const void*)tc_kernel<1, kTcKindsFwd>,
+                       (const void*)tc_kernel<2, kTcKindsFwd>, (const void*)tc_kernel<4, kTcKindsFwd>,
+                       (const void*)tc_kernel<1, kTcKindsBwd>, (const void*)tc_kernel<2, kTcKindsBwd>,
+                       (const void*)tc_kernel<4, kTcKindsBwd>, (const void*)tcu_kernel<kTcKindsAll>,
+                       (const void*)tcu_kernel<kTcKindsBwd>};
   for (const void* f : fns) {
     const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
