@@ -708,6 +708,11 @@ constexpr unsigned kTcKindsFwd = (1u << TC_TANH) | (1u << TC_SAMPLE) | (1u << TC
 constexpr unsigned kTcKindsBwd = (1u << TC_TGRAD) | (1u << TC_LIN) | (1u << TC_GBWD_PRIOR) | (1u << TC_GBWD_ENC) |
                                  (1u << TC_LOADG) | (1u << TC_GBWD0);
 constexpr unsigned kTcKindsAll = 0x1FFFu;
+// (16-row backward launches also have narrower sets: the sample-row backward
+// without job I' op, job I' alone)
+constexpr unsigned kTcKindsBwdRows = (1u << TC_TGRAD) | (1u << TC_LIN) | (1u << TC_GBWD_PRIOR) | (1u << TC_GBWD_ENC) |
+                                     (1u << TC_LOADG);
+constexpr unsigned kTcKindsImgBwd = (1u << TC_TGRAD) | (1u << TC_LIN) | (1u << TC_GBWD0);
 struct TcArgs {
   const TcPlan* plan;
   unsigned kinds;             // op kinds of the plan's jobs (host-computed; 0: all)

@@ -36,6 +36,9 @@
 #ifndef IWAE_TC_KM
 #define IWAE_TC_KM 1          // engine launches on the instantiation of their plan's op-kind set (0: all kinds)
 #endif
+#ifndef IWAE_TC_NARROW
+#define IWAE_TC_NARROW 1      // ... 16-row backward launches and job I' on the narrower sets too
+#endif
 
 namespace iwae {
 
@@ -1334,7 +1337,9 @@ hipError_t launch_tcu(hipStream_t st, const TcArgs& a, const UpdArgs& u, const U
   const int n_tc = a.block_start[kTcMaxJobs];
   const int n_pad = (n_tc + 7) & ~7;                      // the update's blocks keep their b % 8 XCD groups
   const int grid = n_pad + 8 * (u.per_xcd + u.per_xcd2);
-  if (IWAE_TC_KM && a.kinds && !(a.kinds & ~kTcKindsBwd))
+  if (IWAE_TC_NARROW && IWAE_TC_KM && a.kinds && !(a.kinds & ~kTcKindsImgBwd))
+    hipLaunchKernelGGL((tcu_kernel<kTcKindsImgBwd>), dim3(grid), dim3(TC_NW * 64), lds_bytes, st, a, u, w, n_tc, n_pad);
+  else if (IWAE_TC_KM && a.kinds && !(a.kinds & ~kTcKindsBwd))
     hipLaunchKernelGGL((tcu_kernel<kTcKindsBwd>), dim3(grid), dim3(TC_NW * 64), lds_bytes, st, a, u, w, n_tc, n_pad);
   else
     hipLaunchKernelGGL((tcu_kernel<kTcKindsAll>), dim3(grid), dim3(TC_NW * 64), lds_bytes, st, a, u, w, n_tc, n_pad);
@@ -1350,8 +1355,17 @@ hipError_t launch_tc(hipStream_t st, const TcArgs& a, int rt, size_t lds_bytes) 
   if (km == 1) hipLaunchKernelGGL((tc_kernel<R, kTcKindsFwd>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a); \
   else if (km == 2) hipLaunchKernelGGL((tc_kernel<R, kTcKindsBwd>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a); \
   else hipLaunchKernelGGL((tc_kernel<R, kTcKindsAll>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a);
+  const bool cov = IWAE_TC_KM && a.kinds;
   switch (rt) {
-    case 1: TC_LAUNCH(1); break;
+    case 1:
+      // (no narrower forward set: without the folded image-row ops hipcc inlines
+      // differently and the forward kernel grows, 79.9 vs 77.6 KB)
+      if (IWAE_TC_NARROW && cov && !(a.kinds & ~kTcKindsBwdRows))
+        hipLaunchKernelGGL((tc_kernel<1, kTcKindsBwdRows>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a);
+      else if (IWAE_TC_NARROW && cov && !(a.kinds & ~kTcKindsImgBwd))
+        hipLaunchKernelGGL((tc_kernel<1, kTcKindsImgBwd>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a);
+      else TC_LAUNCH(1);
+      break;
     case 2: TC_LAUNCH(2); break;
     case 4: TC_LAUNCH(4); break;
     default: return hipErrorInvalidValue;
@@ -1366,7 +1380,8 @@ hipError_t tc_setup_attributes() {
                        (const void*)tc_kernel<2, kTcKindsFwd>, (const void*)tc_kernel<4, kTcKindsFwd>,
                        (const void*)tc_kernel<1, kTcKindsBwd>, (const void*)tc_kernel<2, kTcKindsBwd>,
                        (const void*)tc_kernel<4, kTcKindsBwd>, (const void*)tcu_kernel<kTcKindsAll>,
-                       (const void*)tcu_kernel<kTcKindsBwd>};
+                       (const void*)tcu_kernel<kTcKindsBwd>, (const void*)tc_kernel<1, kTcKindsBwdRows>, (const void*)tc_kernel<1, kTcKindsImgBwd>,
+                       (const void*)tcu_kernel<kTcKindsImgBwd>};
   for (const void* f : fns) {
     const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
