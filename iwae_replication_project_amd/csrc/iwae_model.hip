@@ -2344,8 +2344,10 @@ static int launch_pending(iwae_handle* h) {
     const UpdArgs& u = h->pend_upd;
     const int n_tc = a.block_start[kTcMaxJobs];
     const int grid = ((n_tc + 7) & ~7) + 8 * (u.per_xcd + u.per_xcd2);
+    bool one_split = true;                         // (tcu_kernel's update has no split-K path)
+    for (int j = 0; j < u.njobs; ++j) one_split = one_split && u.job[j].nsplit <= 1;
     const bool ok = h->pend_tc_rt == 1 && a.xcd_slots == 0 && a.bnd_block < 0 && !u.search && !u.apply &&
-                    grid <= 256 && n_tc > 0 && h->pend_upd_cons > 0;
+                    one_split && grid <= 256 && n_tc > 0 && h->pend_upd_cons > 0;
     if (ok) {
       UpdWait w;
       w.ctr = h->tcu_ctr; w.wait_mask = h->pend_upd_mask; w.n_prod = n_tc; w.n_cons = h->pend_upd_cons;

@@ -36,6 +36,9 @@
 #ifndef IWAE_TC_KM
 #define IWAE_TC_KM 1          // engine launches on the instantiation of their plan's op-kind set (0: all kinds)
 #endif
+#ifndef IWAE_TCU_LEAN
+#define IWAE_TCU_LEAN 1       // the combined launch's update without the split-K and slab-apply code
+#endif
 #ifndef IWAE_TC_NARROW
 #define IWAE_TC_NARROW 1      // ... 16-row backward launches and job I' on the narrower sets too
 #endif
@@ -1326,7 +1329,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tcu_kernel(TcArgs A, UpdArgs U, Up
 #endif
     return;
   }
-  upd_body<TC_NW>(U, b - n_tc_pad, &W);
+  upd_body<TC_NW, !IWAE_TCU_LEAN>(U, b - n_tc_pad, &W);
 #ifdef IWAE_TCU_TRACE
   __syncthreads();
   if (threadIdx.x == 0 && b < 512) g_tcu_trace[b * 4 + 2] = wall_clock64();

@@ -255,7 +255,9 @@ __device__ __forceinline__ void upd_wait(const UpdWait& w) {
 
 // One 64 x TN tile (TN = 64, or 32 for the sample-row layers: more
 // workgroups, half the MFMA and a quarter less staging per workgroup).
-template <int TN, int NW>
+// (FULL false: the combined launch's update -- no slab apply modes, which
+// launch_pending rules out; less code for its workgroups to fetch)
+template <int TN, int NW, bool FULL = true>
 __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, const AdamState& st, int b, int lt,
                                          const UpdWait* w = nullptr) {
   constexpr int NT = UpCfg<NW>::NT, TPR = NT / 64;   // threads per epilogue row
@@ -380,7 +382,7 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
 
   float g[EJ];
   float wsc = a.gscale;
-  if (a.apply == 2) {
+  if (FULL && a.apply == 2) {
     // the large-batch step: the tile's gradient is the sum of the gradient
     // pass's split-K slabs (dw_kernel / the grouped GEMMs), in slab order like
     // adam_kernel's, times the launch's scale; eight slabs' loads in flight
@@ -403,7 +405,7 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
       g[4 * q + 2] = acc.z * a.gscale; g[4 * q + 3] = acc.w * a.gscale;
     }
     wsc = 1.f;
-  } else if (a.apply) {
+  } else if (FULL && a.apply) {
     // data parallel, after the all-reduce: the summed gradient of the tile's
     // elements times 1 / (sum of the ranks' batch sizes)
     const float sc = a.scale_dev ? 1.f / *a.scale_dev : a.gscale;
@@ -536,7 +538,9 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
 
 // The update of workgroup b (upd_kernel's body; tcu_kernel runs it behind its
 // image-row workgroups).
-template <int NW>
+// FULL false (the combined launch): every job has nsplit 1 and no apply mode
+// (launch_pending checks), so neither the split-K path nor the apply code is compiled
+template <int NW, bool FULL = true>
 __device__ __forceinline__ void upd_body(const UpdArgs& a, int b, const UpdWait* w) {
   // tile of this workgroup: consecutive tiles (sharing an operand slice) on one XCD
   // (the long reductions -- tiles [0, nheavy) -- are spread evenly over the
@@ -562,7 +566,7 @@ __device__ __forceinline__ void upd_body(const UpdArgs& a, int b, const UpdWait*
   // now: in flight during the reduction
   const AdamState st = *a.state;
   const UpdWait* wj = (w && ((w->wait_mask >> jb) & 1u)) ? w : nullptr;    // (upd_tile waits)
-  if (J.nsplit > 1) {
+  if (FULL && J.nsplit > 1) {
     // split s of the rows: this tile's partial sum into slab s
     const int per = J.tiles_m * J.tiles_n, lt = T - J.tile0, s = lt / per;
     const long long r0 = (long long)s * J.chunk;
@@ -576,9 +580,9 @@ __device__ __forceinline__ void upd_body(const UpdArgs& a, int b, const UpdWait*
     upd_tile<64, NW>(a, Js, st, b, lt - s * per);
   } else if (NW == 4 && J.tn == 32) {
     if (wj) upd_wait(*wj);
-    upd_tile<32, 4>(a, J, st, b, T - J.tile0);
+    upd_tile<32, 4, FULL>(a, J, st, b, T - J.tile0);
   } else {
-    upd_tile<64, NW>(a, J, st, b, T - J.tile0, wj);
+    upd_tile<64, NW, FULL>(a, J, st, b, T - J.tile0, wj);
   }
 }
 
