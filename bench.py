@@ -461,6 +461,8 @@ def main():
     captures_timed = model.graph_captures() - cap0
     if captures_timed:
         raise SystemExit(f"[bench] {captures_timed} graph capture(s) inside the timed region")
+    # no in-launch wait of the timed steps gave up (their gradients would be invalid)
+    model.check_kernel_status()
     if world > 1:
         t = torch.tensor([el], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -587,6 +589,7 @@ def main():
         el3 = time.perf_counter() - t2
         if model.graph_captures() != cap1:
             raise SystemExit("[bench] graph capture inside the large-batch timed region")
+        model.check_kernel_status()
         if world > 1:
             t = torch.tensor([el3], device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -91,7 +91,17 @@ void iwae_destroy(iwae_handle* h);
 const char* iwae_last_error(const iwae_handle* h);
 /* Enqueue on this stream (hipStream_t); NULL = the handle's own stream. */
 int iwae_set_stream(iwae_handle* h, void* hip_stream);
+/* Waits for the handle's stream, then reports kernel failures as iwae_status. */
 int iwae_synchronize(iwae_handle* h);
+/* IWAE_EHIP (with iwae_last_error naming the kernel) once a kernel of this
+ * handle has reported a failure it could not recover from -- an in-launch
+ * wait of the combined image-row backward + update launch (tcu_kernel) that
+ * ran out of spins, so that train step's gradients and Adam update were
+ * computed from stale data -- else IWAE_OK.  Reads a host-mapped word the
+ * kernel writes: no synchronization, so call it after the step's results were
+ * read (or after iwae_synchronize).  Sticky until iwae_set_params; the train
+ * entry points also return it before enqueueing more work. */
+int iwae_status(iwae_handle* h);
 int iwae_set_seed(iwae_handle* h, unsigned long long seed);
 /* Noise stream of this handle (one per rank): the Philox key becomes
  * splitmix64(seed ^ splitmix64(stream)) for stream != 0 (stream 0: the seed
@@ -119,7 +129,6 @@ enum iwae_knob {
   IWAE_KNOB_TC_RT = 7,         /* 16-row tiles per engine workgroup below WIDE_ROWS: 1, 2 or 4 (1) */
   IWAE_KNOB_UPD = 8,           /* fused weight-gradient + Adam + FX update launch (1) */
   IWAE_KNOB_UPD_ROWS = 9,      /* ... up to this many sample rows per step (4096) */
-  IWAE_KNOB_UPD_TN32 = 10,     /* ... sample-row layers in 64 x 32 tiles (0) */
   IWAE_KNOB_UPD_SLABS = 11,    /* beyond UPD_ROWS: its split-K gradient pass into the Adam slabs (1) */
   IWAE_KNOB_UPD_SLAB_WG = 12,  /* ... sample-row workgroups of that pass (512) */
   IWAE_KNOB_DW_TARGET = 13,    /* split-K workgroups per layer of the grouped weight-gradient GEMMs (768) */
@@ -139,7 +148,7 @@ enum iwae_knob {
   IWAE_KNOB_WIDE_RT = 25           /* row tiles of 16 per workgroup of the engine's backward launches from
                                       WIDE_ROWS: 1, 2 or 4 (2; the forward launch: 4) */,
   IWAE_KNOB_UPD_WAVES = 26,        /* update kernel workgroup: 16 waves (four per SIMD, each a quarter of a tile's
-                                      columns for one k step), 8 or 4 (16) */
+                                      columns for one k step), 8 or 4 (16; the combined launch of TCU always 8) */
   IWAE_KNOB_NLL_IMGS = 27,         /* images per NLL chunk where the call passes chunk 0 (iwae_nll_eps too);
                                       with NLL_ROWS < imgs * k the chunk's samples split into sample chunks (0: auto) */
   IWAE_KNOB_DW_WG = 28,            /* workgroups the DW_WIDE weight-gradient pass balances its row chunks over (256) */
@@ -152,19 +161,14 @@ enum iwae_knob {
   IWAE_KNOB_X_DIRECT = 33,         /* 1: a large-batch engine step's input GEMM reads the caller's x (default); 0: staged copy */
   IWAE_KNOB_TCU = 34,              /* the first encoder layer's image-row backward (job I') and the fused update in one
                                       launch, its tiles of that layer waiting in-launch for job I' (1) */
-  IWAE_KNOB_UPD_APPLY = 35,        /* beyond UPD_ROWS: the gradient pass's slabs summed, Adam and the FX / GX copies
+  IWAE_KNOB_UPD_APPLY = 35,       /* beyond UPD_ROWS: the gradient pass's slabs summed, Adam and the FX / GX copies
                                       in one update-kernel launch instead of the Adam and FX-refresh launches (1) */
-  IWAE_KNOB_STEPS_FIRST = 36,     /* iwae_train_steps: steps in a call's first captured graph, then up to 32 per
-                                      graph (0: 32 from the start) */
-  IWAE_KNOB_SM_CHAIN = 37,        /* up to SMALLM_ROWS images: the first encoder layer's three few-row launches as
-                                      one launch, each layer waiting in-launch for the one before (0: measured
-                                      slower) */
-  IWAE_KNOB_DW_SCALE_COST = 38,   /* weight-gradient pass (dw_kernel) cost model: extra tile units per k step of a
-                                      row-scaled dZ (0) */
-  IWAE_KNOB_DW_WIDE_COST = 39,     /* ... and of a wide block (0) */
-  IWAE_KNOB_SM_PAIR = 40           /* up to SMALLM_ROWS images: the first encoder layer's l2 and head as one launch,
-                                      every workgroup computing the whole l2 into its LDS: 1 exact f32 (bitwise the
-                                      two launches), 2 l2's products bf16x3 (0) */
+  IWAE_KNOB_TCU_WAIT_TEST = 41    /* fault injection for tests (0): every in-launch wait of the TCU launch waits
+                                      for one producer more than exists, with a short spin bound, so it gives up and
+                                      the failure must surface through iwae_status (results of that step invalid) */
+  /* 10, 36-40: removed variants measured slower (64 x 32 update tiles, a short
+     first graph, the chained / paired first-encoder-layer launches, dw_kernel
+     cost-model terms); iwae_set_tuning rejects them with IWAE_EINVAL */
 };
 int iwae_set_tuning(iwae_handle* h, int knob, long long value);
 /* Matrix-product precision of the tiled GEMM kernels: 1 (default) bf16x3 --
@@ -210,12 +214,12 @@ int iwae_train_step(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
  * (x [dev] holds nsteps*B images); loss_dev [dev, may be NULL] receives
  * nsteps losses.  Same arithmetic as nsteps iwae_train_step calls; with graphs
  * on, consecutive steps replay from captured graphs of up to 32 steps (no
- * launch gap between them; IWAE_KNOB_STEPS_FIRST > 0 shortens the first). */
+ * launch gap between them). */
 int iwae_train_steps(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B, int nsteps,
                      float* loss_dev);
 /* Capture, without launching anything, every graph an iwae_train_steps call
  * with these arguments would capture (its chunk lengths: up to 32 steps
- * each, the first one IWAE_KNOB_STEPS_FIRST long when that is set), so that the call itself only replays; the parameters, Adam
+ * each), so that the call itself only replays; the parameters, Adam
  * state and noise position are untouched.  Data parallelism with the library
  * communicator included (each captured step carries its all-reduces). */
 int iwae_train_steps_prepare(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B, int nsteps);
@@ -329,11 +333,9 @@ double iwae_workspace_bytes(const iwae_handle* h);
  * iwae_train_steps, iwae_train_steps_prepare; bench.py asserts it stays flat
  * across its timed region), 8 in-launch waits of the combined image-row
  * backward + update launch that gave up (synchronous; 0 unless the GPU was
- * shared with a kernel that held CUs for ~1 s), 9 such combined launches
- * issued (a captured step counts once, at capture), 10 in-launch waits of the
- * chained first-encoder-layer launch (smchain_kernel) that gave up
- * (synchronous), 11 such chained launches issued, 12 first-encoder-layer l2 +
- * head launches (smpair_kernel) issued; -1 for an unknown id. */
+ * shared with a kernel that held CUs for ~1 s, or IWAE_KNOB_TCU_WAIT_TEST;
+ * each also sets the error iwae_status reports), 9 such combined launches
+ * issued (a captured step counts once, at capture); -1 for an unknown id. */
 long long iwae_debug_count(const iwae_handle* h, int what);
 /* Live kernel timing: bracket every launch of one kernel class with HIP events
  * on the handle's stream -- a GEMM class (kind: 0 forward, 1 backward-data,

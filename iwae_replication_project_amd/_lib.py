@@ -17,12 +17,11 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # include/iwae.h enum iwae_knob (iwae_set_tuning)
 KNOBS = {
     "engine": 1, "tc_img": 2, "tc_imgbwd": 3, "tc_fold0": 4, "tc_xcd": 5, "tc_bound": 6, "tc_rt": 7,
-    "upd": 8, "upd_rows": 9, "upd_tn32": 10, "upd_slabs": 11, "upd_slab_wg": 12, "dw_target": 13,
+    "upd": 8, "upd_rows": 9, "upd_slabs": 11, "upd_slab_wg": 12, "dw_target": 13,
     "smallm_rows": 14, "out_x3_rows": 15, "mg_waves": 16, "nll_rows": 17, "wide_rows": 18, "dw_wide": 19, "ld_align": 20,
     "nring": 21, "nring_train": 22, "nring_train_rows": 23, "nring_bwd": 24, "wide_rt": 25, "upd_waves": 26,
     "nll_imgs": 27, "dw_wg": 28, "piwae_one": 29, "dw_alpha": 30,
-    "img_rows_fwd": 31, "img_rows_bwd": 32, "x_direct": 33, "tcu": 34, "upd_apply": 35, "steps_first": 36,
-    "sm_chain": 37, "dw_scale_cost": 38, "dw_wide_cost": 39, "sm_pair": 40,
+    "img_rows_fwd": 31, "img_rows_bwd": 32, "x_direct": 33, "tcu": 34, "upd_apply": 35, "tcu_wait_test": 41,
 }
 LOSS_IDS = {
     "VAE": 0, "IWAE": 1, "VAE_V1": 2, "L_alpha": 3, "L_power_p": 4,
@@ -60,6 +59,7 @@ SIGNATURES = {
     "iwae_last_error": (c_char_p, [H]),
     "iwae_set_stream": (c_int, [H, c_void_p]),
     "iwae_synchronize": (c_int, [H]),
+    "iwae_status": (c_int, [H]),
     "iwae_set_seed": (c_int, [H, c_ulonglong]),
     "iwae_set_noise_stream": (c_int, [H, c_ulonglong]),
     "iwae_set_graphs": (c_int, [H, c_int]),

@@ -658,48 +658,6 @@ constexpr int SM_MAX_ASLABS = 4;    // partial slabs a reader sums while staging
 // activation rows in batches of SM_STAGE quads per thread.
 constexpr int SM_STAGE = 4;
 
-// In-launch chaining of the few-row layers (smchain_kernel): a later stage's
-// workgroups request their weights first, then wait for every workgroup of the
-// stage before it (agent scope: each producer drains its stores, barrier,
-// release fence, counter add; one consumer thread polls relaxed, then acquire
-// fence; the stages' workgroups are dispatched in stage order, so a waiting
-// workgroup never holds back one it waits for).  Bounded spins, give-ups
-// counted in ctr[3]; the last workgroup of the last stage through its wait
-// resets ctr[0..2] (every wait of the launch has passed by then).
-__device__ __forceinline__ void sm_wait(const SmChainArgs& c, int stage) {
-  if (threadIdx.x == 0) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(c.ctr + stage - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-           (unsigned)c.nb[stage - 1]) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 24)) {
-        __hip_atomic_fetch_add(c.ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (stage == c.nstage - 1) {
-      const unsigned k = __hip_atomic_fetch_add(c.ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (k + 1 == (unsigned)c.nb[stage]) {
-        __hip_atomic_store(c.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(c.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(c.ctr + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  __syncthreads();
-}
-__device__ __forceinline__ void sm_publish(const SmChainArgs& c, int stage) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(c.ctr + stage, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // A's rows -> LDS As[32][lds_ld] (rows >= M and k >= K zero; partial slabs summed,
 // activation and ones column applied when a_slabs > 0): one workgroup's K range
 // [kb0, kb0 + Kb) of column tile t, slab ks (t == 0 && ks == 0 write a_out / a_copy)
@@ -779,11 +737,9 @@ __device__ __forceinline__ void sm_stage(const SmArgs& a, int t, int ks, float* 
   }
 }
 
-// one workgroup (column tile t, K slab ks) of a few-row Dense; ch: the chain it
-// is stage `stage` of (nullptr: a plain smallm_kernel launch)
+// one workgroup (column tile t, K slab ks) of a few-row Dense
 template <bool BT, int MU = SM_MAXU, int SL = 0>
-__device__ __forceinline__ void smallm_body(const SmArgs& a, int t, int ks, float* sm_lds, const SmChainArgs* ch,
-                                            int stage) {
+__device__ __forceinline__ void smallm_body(const SmArgs& a, int t, int ks, float* sm_lds) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int n = t * 16 + r;
@@ -815,8 +771,6 @@ __device__ __forceinline__ void smallm_body(const SmArgs& a, int t, int ks, floa
       bq[u] = make_float4(e[0], e[1], e[2], e[3]);
     }
   }
-  // (chained: the activations are the previous stage's output)
-  if (ch && stage > 0) sm_wait(*ch, stage);
   // activations -> LDS (rows >= M and k >= K zero)
   sm_stage<SL>(a, t, ks, As, kb0, Kb, Kp, lds_ld);
   __syncthreads();
@@ -864,7 +818,6 @@ __device__ __forceinline__ void smallm_body(const SmArgs& a, int t, int ks, floa
       a.C[(size_t)row * a.ldc + col] = v;
     }
   }
-  if (ch && stage < ch->nstage - 1) sm_publish(*ch, stage);
 }
 
 // MU: 16-deep k groups per wave the instantiation unrolls (2: K <= 256 per
@@ -873,272 +826,7 @@ __device__ __forceinline__ void smallm_body(const SmArgs& a, int t, int ks, floa
 template <bool BT, int MU, int SL>
 __global__ __launch_bounds__(SM_WAVES * 64) void smallm_kernel(SmArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm_lds[];
-  smallm_body<BT, MU, SL>(a, blockIdx.x, blockIdx.y, sm_lds, nullptr, 0);
-}
-
-// the first encoder layer's forward (input Dense, l2, head) as one launch
-__global__ __launch_bounds__(SM_WAVES * 64) void smchain_kernel(SmChainArgs c) {
-  extern __shared__ __attribute__((aligned(16))) float sm_lds[];
-  int b = blockIdx.x, stage = 0;
-  while (stage < c.nstage - 1 && b >= c.nb[stage]) b -= c.nb[stage++];
-  smallm_body<false>(c.s[stage], b % c.gx[stage], b / c.gx[stage], sm_lds, &c, stage);
-}
-
-// The first encoder layer's l2 and head as ONE launch without an in-launch
-// handoff (smpair_kernel): each workgroup owns one head column tile and first
-// computes the WHOLE l2 output itself (the 13 tiles of a 200-wide layer, its
-// 160 KB of weights read from L2 by every workgroup) into LDS, where the head
-// reads it.  Workgroup 0 also stores y1 (while staging) and y2 for the
-// backward.  Per tile the same per-wave K ranges, MFMA order and fixed-order
-// sum over the waves as smallm_body, so the results equal the two launches'
-// bit for bit.  l2: K <= 256 (<= 2 16-deep k groups per wave), N <= 16 * SP_NT;
-// head: K = l2.N + 1 <= 256 (launch_smpair checks).
-constexpr int SP_NT = 13;            // l2 column tiles (N <= 208)
-constexpr int SP_MAXU = 2;           // 16-deep k groups per wave (K <= 256)
-constexpr int SP_TB = 4;             // l2 tiles reduced per LDS round
-constexpr int SP_KS = 7;             // X3: 32-deep k steps of l2 (K <= 224)
-#ifndef IWAE_SP_ABL
-#define IWAE_SP_ABL 0                // timing ablation (debug builds, WRONG results): 1 no l2 MFMAs (f32),
-                                     // 2 no l2 weight loads (bf16x3), 4 no staging of l2's A
-#endif
-
-template <bool X3>
-__global__ __launch_bounds__(SM_WAVES * 64) void smpair_kernel(SmArgs l2, SmArgs hd) {
-  extern __shared__ __attribute__((aligned(16))) float sm_lds[];
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  const int t = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r = lane & 15, g = lane >> 4;
-  // l2 and head geometry (smallm_body's, one K slab)
-  const int Kb = l2.K, Kp = X3 ? (Kb + 31) & ~31 : (Kb + 15) & ~15, lds_ld = Kp + 4;
-  const int kc = (((Kb + SM_WAVES - 1) / SM_WAVES) + 15) & ~15, kb = wave * kc;
-  const int nu = min(SP_MAXU, max(0, (min(kc, Kp - kb) + 15) >> 4));
-  const int Kb2 = hd.K, Kp2 = (Kb2 + 15) & ~15, lds_ld2 = Kp2 + 4;
-  const int kc2 = (((Kb2 + SM_WAVES - 1) / SM_WAVES) + 15) & ~15, kb2 = wave * kc2;
-  const int nu2 = min(SP_MAXU, max(0, (min(kc2, Kp2 - kb2) + 15) >> 4));
-  const int nt2 = (l2.N + 15) >> 4;
-  float* As = sm_lds;                          // [32][lds_ld]: l2's A (tanh(y1 slabs summed) | 1)
-  float* A2 = As + 32 * lds_ld;                // [32][lds_ld2]: the head's A (y2 | 1)
-  float* part = A2 + 32 * lds_ld2;             // [SP_TB][wave][rt][i][lane]
-  // every weight of this wave's k ranges first: l2's for all tiles (X3: the
-  // 8 k values of each 32-deep step of its two column tiles), the head's tile
-  const __amdgpu_buffer_rsrc_t rW = buf_rsrc(l2.W), rH = buf_rsrc(hd.W);
-  float4 bq[SP_NT][SP_MAXU], bh[SP_MAXU];
-  typedef unsigned sp_u32x4 __attribute__((ext_vector_type(4)));
-  sp_u32x4 bxh[2][SP_KS], bxl[2][SP_KS];
-  if constexpr (X3) {
-    // B fragments straight from the FX copy: one 16-byte load per lane and
-    // plane per (column tile, k step), 1 KiB contiguous per wave instruction
-    const __amdgpu_buffer_rsrc_t rxh = buf_rsrc(l2.wx_hi), rxl = buf_rsrc(l2.wx_lo);
-    const int nst = Kp >> 5;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int ct = wave + 8 * q;
-#pragma unroll
-      for (int st = 0; st < SP_KS; ++st) {
-        const unsigned o = (ct < nt2 && st < nst && !(IWAE_SP_ABL & 2)) ? (unsigned)(((ct * l2.wx_steps + st) * 64 + lane) * 16) : kOOB;
-        bxh[q][st] = __builtin_amdgcn_raw_buffer_load_b128(rxh, o, 0, 0);
-        bxl[q][st] = __builtin_amdgcn_raw_buffer_load_b128(rxl, o, 0, 0);
-      }
-    }
-  } else {
-#pragma unroll
-    for (int tt = 0; tt < SP_NT; ++tt) {
-      const int n = tt * 16 + r;
-#pragma unroll
-      for (int u = 0; u < SP_MAXU; ++u) {
-        const int k0 = kb + 16 * u + 4 * g;
-        const bool ok = u < nu && n < l2.N;
-        float e[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) e[j] = bld1(rW, (ok && k0 + j < Kb) ? (unsigned)((k0 + j) * l2.ldw + n) * 4u : kOOB);
-        bq[tt][u] = make_float4(e[0], e[1], e[2], e[3]);
-      }
-    }
-  }
-  {
-    const int n = t * 16 + r;
-#pragma unroll
-    for (int u = 0; u < SP_MAXU; ++u) {
-      const int k0 = kb2 + 16 * u + 4 * g;
-      const bool ok = u < nu2 && n < hd.N;
-      float e[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) e[j] = bld1(rH, (ok && k0 + j < Kb2) ? (unsigned)((k0 + j) * hd.ldw + n) * 4u : kOOB);
-      bh[u] = make_float4(e[0], e[1], e[2], e[3]);
-    }
-  }
-  // l2's activations (workgroup 0 writes y1 while staging)
-  if (!(IWAE_SP_ABL & 4)) sm_stage(l2, t, 0, As, 0, Kb, Kp, lds_ld);
-  // the head's A past l2's tiles: ones column at K2 - 1, zeros after
-  for (int e = threadIdx.x; e < 32 * Kp2; e += blockDim.x) {
-    const int row = e / Kp2, k = e - row * Kp2;
-    if (k >= 16 * nt2) A2[row * lds_ld2 + k] = (row < hd.M && k == Kb2 - 1) ? 1.f : 0.f;
-  }
-  __syncthreads();
-  const bool two = l2.M > 16;
-  const int e = threadIdx.x, rt = e >> 8, ii = (e >> 6) & 3, l = e & 63;
-  const int row = rt * 16 + 4 * (l >> 4) + ii;
-  if constexpr (X3) {
-    // wave w: l2 column tiles w and w + 8, both row tiles, the whole K (no
-    // cross-wave sum); bf16x3 on v_mfma_f32_16x16x32_bf16 like the engine
-    f4v acc[2][2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) acc[q][h] = f4v{0.f, 0.f, 0.f, 0.f};
-    const int nst = Kp >> 5;
-#pragma unroll
-    for (int st = 0; st < SP_KS; ++st) {
-      if (st >= nst) break;
-      bf16x8 ah[2], al[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const float* ap = &As[(16 * h + r) * lds_ld + 32 * st + 8 * g];
-        const float4 v0 = *reinterpret_cast<const float4*>(ap), v1 = *reinterpret_cast<const float4*>(ap + 4);
-        bf16x4 h0, l0, h1, l1;
-        split4(v0, h0, l0);
-        split4(v1, h1, l1);
-        ah[h] = bf16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-        al[h] = bf16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
-      }
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const bf16x8 bh8 = __builtin_bit_cast(bf16x8, bxh[q][st]);
-        const bf16x8 bl8 = __builtin_bit_cast(bf16x8, bxl[q][st]);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          if (h == 1 && !two) break;
-          acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[h], bh8, acc[q][h], 0, 0, 0);
-          acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[h], bl8, acc[q][h], 0, 0, 0);
-          acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[h], bh8, acc[q][h], 0, 0, 0);
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int ct = wave + 8 * q;
-      if (ct >= nt2) break;
-      const int col = ct * 16 + r;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int rw = 16 * h + 4 * g + i;
-          const float v = ftanh(acc[q][h][i]);
-          const bool in = rw < l2.M && col < l2.N;
-          if (in && t == 0) l2.C[(size_t)rw * l2.ldc + col] = v;
-          if (col < Kp2) A2[rw * lds_ld2 + col] = in ? v : (rw < hd.M && col == Kb2 - 1) ? 1.f : 0.f;
-        }
-    }
-    __syncthreads();
-  } else {
-#pragma unroll
-  for (int b0 = 0; b0 < SP_NT; b0 += SP_TB) {
-#pragma unroll
-    for (int tb = 0; tb < SP_TB; ++tb) {
-      const int tt = b0 + tb;
-      if (tt >= SP_NT) break;
-      f4v c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int u = 0; u < SP_MAXU; ++u) {
-        if (u >= nu || (IWAE_SP_ABL & 1)) break;
-        const int k0 = kb + 16 * u + 4 * g;
-        const float4 a0 = *reinterpret_cast<const float4*>(&As[r * lds_ld + k0]);
-        const float4 a1 = *reinterpret_cast<const float4*>(&As[(16 + r) * lds_ld + k0]);
-        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, bq[tt][u].x, c0, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, bq[tt][u].y, c0, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, bq[tt][u].z, c0, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, bq[tt][u].w, c0, 0, 0, 0);
-        if (two) {
-          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, bq[tt][u].x, c1, 0, 0, 0);
-          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, bq[tt][u].y, c1, 0, 0, 0);
-          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, bq[tt][u].z, c1, 0, 0, 0);
-          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, bq[tt][u].w, c1, 0, 0, 0);
-        }
-      }
-      float* pt = part + tb * (SM_WAVES * 2 * 4 * 64);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        pt[((wave * 2 + 0) * 4 + i) * 64 + lane] = c0[i];
-        pt[((wave * 2 + 1) * 4 + i) * 64 + lane] = c1[i];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int tb = 0; tb < SP_TB; ++tb) {
-      const int tt = b0 + tb;
-      if (tt >= SP_NT || tt >= nt2) break;
-      const float* pt = part + tb * (SM_WAVES * 2 * 4 * 64);
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < SM_WAVES; ++w) v += pt[((w * 2 + rt) * 4 + ii) * 64 + l];
-      const int col = tt * 16 + (l & 15);
-      v = ftanh(v);
-      const bool in = row < l2.M && col < l2.N;
-      if (in && t == 0) l2.C[(size_t)row * l2.ldc + col] = v;
-      // (the head's A: y2, the ones column at K2 - 1 = l2.N, zeros elsewhere)
-      if (col < Kp2) A2[row * lds_ld2 + col] = in ? v : (row < hd.M && col == Kb2 - 1) ? 1.f : 0.f;
-    }
-    __syncthreads();
-  }
-  }
-  // the head's column tile t on y2 (act 0)
-  {
-    f4v c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-    const bool two2 = hd.M > 16;
-#pragma unroll
-    for (int u = 0; u < SP_MAXU; ++u) {
-      if (u >= nu2) break;
-      const int k0 = kb2 + 16 * u + 4 * g;
-      const float4 a0 = *reinterpret_cast<const float4*>(&A2[r * lds_ld2 + k0]);
-      const float4 a1 = *reinterpret_cast<const float4*>(&A2[(16 + r) * lds_ld2 + k0]);
-      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, bh[u].x, c0, 0, 0, 0);
-      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, bh[u].y, c0, 0, 0, 0);
-      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, bh[u].z, c0, 0, 0, 0);
-      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, bh[u].w, c0, 0, 0, 0);
-      if (two2) {
-        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, bh[u].x, c1, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, bh[u].y, c1, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, bh[u].z, c1, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, bh[u].w, c1, 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      part[((wave * 2 + 0) * 4 + i) * 64 + lane] = c0[i];
-      part[((wave * 2 + 1) * 4 + i) * 64 + lane] = c1[i];
-    }
-    __syncthreads();
-    float v = 0.f;
-#pragma unroll
-    for (int w = 0; w < SM_WAVES; ++w) v += part[((w * 2 + rt) * 4 + ii) * 64 + l];
-    const int col = t * 16 + (l & 15);
-    if (row < hd.M && col < hd.N) hd.C[(size_t)row * hd.ldc + col] = v;
-  }
-}
-
-static size_t smpair_lds(const SmArgs& l2, const SmArgs& hd) {
-  const int Kp = (l2.K + 31) & ~31, Kp2 = (hd.K + 15) & ~15;
-  return (size_t)(32 * (Kp + 4) + 32 * (Kp2 + 4) + SP_TB * SM_WAVES * 2 * 4 * 64) * sizeof(float);
-}
-
-bool smpair_fits(const SmArgs& l2, const SmArgs& hd, bool x3) {
-  if (x3 && (l2.K > 32 * SP_KS || l2.N > 16 * 16 || !l2.wx_hi || !l2.wx_lo || (l2.K + 31) / 32 > l2.wx_steps))
-    return false;
-  return !l2.bt && !hd.bt && l2.kslabs <= 1 && hd.kslabs <= 1 && hd.a_slabs == 0 && l2.act == 1 && hd.act == 0 &&
-         l2.M > 0 && l2.M <= 32 && hd.M == l2.M && l2.N > 0 && l2.N <= 16 * SP_NT && hd.N > 0 && hd.K == l2.N + 1 &&
-         l2.K <= SM_WAVES * 16 * SP_MAXU && hd.K <= SM_WAVES * 16 * SP_MAXU && l2.a_slabs <= SM_MAX_ASLABS &&
-         l2.a_ones == 0 && l2.a_copy == nullptr && smpair_lds(l2, hd) <= 160 * 1024;
-}
-
-hipError_t launch_smpair(hipStream_t st, const SmArgs& l2, const SmArgs& hd, bool x3) {
-  if (!smpair_fits(l2, hd, x3)) return hipErrorInvalidValue;
-  if (x3)
-    hipLaunchKernelGGL(smpair_kernel<true>, dim3((hd.N + 15) / 16), dim3(SM_WAVES * 64), smpair_lds(l2, hd), st, l2, hd);
-  else
-    hipLaunchKernelGGL(smpair_kernel<false>, dim3((hd.N + 15) / 16), dim3(SM_WAVES * 64), smpair_lds(l2, hd), st, l2, hd);
-  return hipGetLastError();
+  smallm_body<BT, MU, SL>(a, blockIdx.x, blockIdx.y, sm_lds);
 }
 
 hipError_t launch_smallm(hipStream_t st, const SmArgs& a) {
@@ -1160,41 +848,7 @@ hipError_t launch_smallm(hipStream_t st, const SmArgs& a) {
   return hipGetLastError();
 }
 
-static size_t smallm_lds(const SmArgs& a) {
-  const int ksl = a.kslabs > 1 ? a.kslabs : 1;
-  const int KC = ksl > 1 ? (((a.K + ksl - 1) / ksl) + 15) & ~15 : a.K;
-  const int Kp = (KC + 15) & ~15;
-  return (size_t)(32 * (Kp + 4) + SM_WAVES * 2 * 4 * 64) * sizeof(float);
-}
-
-hipError_t launch_smchain(hipStream_t st, SmChainArgs& c) {
-  size_t lds = 0;
-  int nb = 0;
-  for (int j = 0; j < c.nstage; ++j) {
-    const SmArgs& a = c.s[j];
-    const int ksl = a.kslabs > 1 ? a.kslabs : 1;
-    const int KC = ksl > 1 ? (((a.K + ksl - 1) / ksl) + 15) & ~15 : a.K;
-    if (a.bt || a.M <= 0 || a.M > 32 || a.N <= 0 || KC > SM_WAVES * 16 * SM_MAXU || a.a_slabs > SM_MAX_ASLABS)
-      return hipErrorInvalidValue;
-    c.gx[j] = (a.N + 15) / 16;
-    c.nb[j] = c.gx[j] * ksl;
-    nb += c.nb[j];
-    lds = std::max(lds, smallm_lds(a));
-  }
-  // every workgroup resident at once (one per CU at most), so no wait outlives its producer's dispatch
-  if (c.nstage < 2 || c.nstage > 3 || nb > 256 || !c.ctr) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(smchain_kernel, dim3(nb), dim3(SM_WAVES * 64), lds, st, c);
-  return hipGetLastError();
-}
-
 hipError_t smallm_setup_attributes() {
-  for (const void* f : {(const void*)smpair_kernel<false>, (const void*)smpair_kernel<true>}) {
-    const hipError_t ep = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (ep != hipSuccess) return ep;
-  }
-  hipError_t e0 = hipFuncSetAttribute((const void*)smchain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024);
-  if (e0 != hipSuccess) return e0;
   for (const void* f : {(const void*)smallm_kernel<true, SM_MAXU, 0>, (const void*)smallm_kernel<false, SM_MAXU, 0>,
                         (const void*)smallm_kernel<true, 2, 0>, (const void*)smallm_kernel<false, 2, 1>,
                         (const void*)smallm_kernel<false, 2, 2>}) {

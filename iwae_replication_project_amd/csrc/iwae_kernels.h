@@ -190,30 +190,9 @@ struct SmArgs {
   // workgroups of column tile 0 also store the staged rows (ones column
   // included) to a_copy for the later readers of A
   int a_ones; unsigned a_bytes; float* a_copy; int a_copy_ld;
-  // the layer's fragment-major split copy (FX: hi / lo planes, wx_steps 32-deep
-  // k steps per 16-column tile; smpair_kernel's bf16x3 form reads its B there)
-  const __bf16* wx_hi; const __bf16* wx_lo; int wx_steps;
 };
 hipError_t launch_smallm(hipStream_t st, const SmArgs& a);
-// l2 (bt 0, tanh) and the head (act 0, K = l2.N + 1) of the first encoder
-// layer in one launch, one workgroup per head column tile, each computing the
-// whole l2 into LDS first (iwae_gemm.hip smpair_kernel): x3 0 exact f32 (bitwise
-// the two smallm launches), 1 l2's products bf16x3; smpair_fits: the shapes it takes
-bool smpair_fits(const SmArgs& l2, const SmArgs& hd, bool x3);
-hipError_t launch_smpair(hipStream_t st, const SmArgs& l2, const SmArgs& hd, bool x3);
 hipError_t smallm_setup_attributes();
-// two or three forward few-row layers (bt 0) in one launch, stage j reading
-// stage j - 1's output after an in-launch wait (iwae_gemm.hip smchain_kernel);
-// gx / nb are filled in place by launch_smchain (a graph node re-pointed
-// later takes the filled struct); ctr: 4 zeroed words [stage 0 done, stage 1
-// done, last stage through, spin give-ups]
-struct SmChainArgs {
-  SmArgs s[3];
-  int nstage;
-  int gx[3], nb[3];
-  unsigned* ctr;
-};
-hipError_t launch_smchain(hipStream_t st, SmChainArgs& c);
 
 // grouped backward-weight GEMMs (64x64 tiles, split over K = rows)
 constexpr int kMaxGroup = 16;
@@ -408,9 +387,12 @@ hipError_t launch_update(hipStream_t st, const UpdArgs& a);
 // in-launch wait of the update's first-encoder-layer tiles on the image-row
 // backward workgroups of tcu_kernel (iwae_update_dev.h, upd_wait)
 struct UpdWait {
-  unsigned* ctr;              // [0] producers done, [1] consumers through, [2] spin give-ups
+  unsigned* ctr;              // [0] producers done, [1] workgroups through (producers and consumers), [2] give-ups
+  unsigned* err;              // host-mapped error word: set to 1 by a wait that gave up (iwae_status reports it)
   unsigned wait_mask;         // jobs whose tiles wait
   int n_prod, n_cons;
+  int n_expect;               // ctr[0] a wait waits for (n_prod; n_prod + 1 under the fault-injection knob)
+  unsigned max_spins;         // spin bound of a wait (s_sleep 1 per spin)
 };
 hipError_t upd_setup_attributes();
 size_t upd_lds_bytes();             // dynamic LDS of an update workgroup

@@ -199,7 +199,6 @@ struct iwae_handle {
   bool adam_splits = false;          // the Adam launch being built also rewrites the split copies
   int upd = 1;                       // fused weight-gradient + Adam + FX update launch
   long long upd_rows = 4096;         // ... up to this many sample rows per step
-  int upd_tn32 = 0;                  // ... sample-row layers in 64 x 32 tiles
   int upd_slabs = 1;                 // ... and beyond upd_rows its split-K gradient pass into the slabs
   long long upd_slab_wg = 512;       // sample-row workgroups of that pass
   int dw_wide = 1;                   // ... run by the 208 x 128-block weight-gradient kernel (iwae_dwgrad.hip;
@@ -211,20 +210,15 @@ struct iwae_handle {
   int dw_wg = 256;                   // large-batch weight-gradient pass: workgroups its row chunks aim at
   int dw_alpha = 150;                // ... its cost model: a k step's fixed cost in MFMA tiles (measured: a
                                      // k step costs ~2 us whatever its tiles; alpha 0 / 45 / 90 / 200: 174 / 127 / 108 / 106 us)
-  int dw_scale_cost = 0;             // ... the extra cost of a row-scaled dZ's k step (tile units)
-  int dw_wide_cost = 0;              // ... and of a wide block's
   int img_rows_fwd = 0, img_rows_bwd = 0;   // image-row jobs I / I': rows per workgroup (0: auto)
   int x_direct = 1;                  // large-batch engine step: the input GEMM reads the caller's x (gemm_direct)
   int tcu = 1;                       // job I' and the fused update in one launch (tcu_kernel) where it fits
   int upd_apply = 1;                 // large batches: the update kernel sums the slabs, Adam, FX / GX (one launch)
-  int steps_first = 0;               // iwae_train_steps: length of a call's first graph (0: 32 like the rest)
-  unsigned* tcu_ctr = nullptr;       // its in-launch counters (zero between launches; [2] spin give-ups);
-                                     // [4..7]: smchain_kernel's ([7] spin give-ups)
-  int sm_chain = 0;                  // the first encoder layer's three few-row launches as one (smchain_kernel;
-                                     // measured slower: B = 20 step 0.136-0.137 vs 0.114 ms, r05x)
-  long long n_smchain = 0;           // smchain_kernel launches, iwae_debug_count(h, 11)
-  int sm_pair = 0;                   // the first encoder layer's l2 and head as one launch (smpair_kernel: 1 exact f32, 2 bf16x3 l2)
-  long long n_smpair = 0;            // smpair_kernel launches, iwae_debug_count(h, 12)
+  unsigned* tcu_ctr = nullptr;       // its in-launch counters (UpdWait::ctr; zero between launches)
+  unsigned* err_host = nullptr;      // host-mapped error word a kernel sets when an in-launch wait gives up
+  unsigned* err_dev = nullptr;       // ... its device address (UpdWait::err)
+  int tcu_wait_test = 0;             // fault injection (knob TCU_WAIT_TEST): every combined-launch wait gives up
+  int n_cu = 256;                    // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   bool defer_launch = false;         // (during a step) tc_run / run_update record their launch instead
   bool pend_tc_have = false, pend_upd_have = false;
   TcArgs pend_tc{};
@@ -244,10 +238,9 @@ struct iwae_handle {
   // (x_node: that launch, re-pointed with hipGraphExecKernelNodeSetParams)
   // the input-layer launch of a captured train step, re-pointed at each call's x
   struct XLaunch {
-    int kind = 0;                      // 0: smallm_kernel (SmArgs), 1: gemm_kernel (GemmArgs), 2: smchain_kernel
+    int kind = 0;                      // 0: smallm_kernel (SmArgs), 1: gemm_kernel (GemmArgs)
     SmArgs sm{};
     GemmArgs gm{};
-    SmChainArgs sc{};
   };
   struct GraphRec {
     hipGraphExec_t exec = nullptr;
@@ -1140,7 +1133,7 @@ static int enc0_forward(iwae_handle* h, const Plan& P, bool l1_only = false) {
       a.act = 1;
     }
     // remember the launch that reads x: replays re-point it at the caller's next x
-    auto note_x = [&](int kind, const SmChainArgs* c) -> int {
+    auto note_x = [&](int kind) -> int {
       if (!(h->capturing && h->x_user)) return IWAE_OK;
       hipStreamCaptureStatus cs;
       unsigned long long cid;
@@ -1151,40 +1144,10 @@ static int enc0_forward(iwae_handle* h, const Plan& P, bool l1_only = false) {
       h->cap_x_node = nd == 1 ? deps[0] : nullptr;
       h->cap_x_args.kind = kind;
       h->cap_x_args.sm = a;
-      if (c) h->cap_x_args.sc = *c;
       return IWAE_OK;
     };
-    if (!l1_only && h->sm_chain && h->prof_kind < 0) {
-      // the three layers as ONE launch (smchain_kernel): the l2 and head
-      // workgroups request their weights at the launch's start and wait in-launch
-      // for the layer before (three launches: 6.3 + 6.9 + 5.4 us at B = 20).
-      // Off by default: the step measured 0.136-0.137 against 0.114 ms -- the
-      // agent-scope handoffs (every producer's L2 write-back, every consumer's
-      // L2 invalidate across 8 XCDs) cost more than the two launch boundaries
-      // (profiles/r05x_sm_chain_ab.txt)
-      SmChainArgs c{};
-      c.s[0] = a;
-      const DenseL& d2 = h->dense[S0.l2];
-      if (ksl > 1) {
-        SmArgs& b = c.s[1];
-        b.A = h->fslab; b.lda = a.ldc;
-        b.a_slabs = ksl; b.a_slab = a.c_slab; b.a_act = 1; b.a_out = h->eb[0].y1.p; b.a_ldo = h->eb[0].y1.ld;
-        b.W = h->params + d2.off; b.ldw = d2.ldw;
-        b.C = h->eb[0].y2.p; b.ldc = h->eb[0].y2.ld;
-        b.M = P.Bimg; b.N = d2.fout; b.K = d2.fin + 1;
-        b.act = 1;
-      } else {
-        c.s[1] = smallm_args(h, h->eb[0].y1, P.Bimg, d2, false, 1, nullptr, h->eb[0].y2);
-      }
-      c.s[2] = smallm_args(h, h->eb[0].y2, P.Bimg, h->dense[S0.head], false, 0, nullptr, h->eb[0].P);
-      c.nstage = 3;
-      c.ctr = h->tcu_ctr + 4;
-      HIPCHK(launch_smchain(h->stream, c));
-      h->n_smchain++;
-      return note_x(2, &c);
-    }
     HIPCHK(launch_smallm(h->stream, a));
-    CHK(note_x(0, nullptr));
+    CHK(note_x(0));
     if (l1_only) return IWAE_OK;
     const DenseL& d2 = h->dense[S0.l2];
     SmArgs b{};
@@ -1198,16 +1161,7 @@ static int enc0_forward(iwae_handle* h, const Plan& P, bool l1_only = false) {
     } else {
       b = smallm_args(h, h->eb[0].y1, P.Bimg, d2, false, 1, nullptr, h->eb[0].y2);
     }
-    b.wx_hi = h->fx_hi + d2.fx_off; b.wx_lo = h->fx_lo + d2.fx_off; b.wx_steps = d2.fx_steps;
     const SmArgs hd = smallm_args(h, h->eb[0].y2, P.Bimg, h->dense[S0.head], false, 0, nullptr, h->eb[0].P);
-    if (h->sm_pair && smpair_fits(b, hd, h->sm_pair == 2)) {
-      // l2 and head in one launch: every workgroup computes the whole l2 into
-      // its LDS, then its head column tile (no in-launch handoff); bitwise the
-      // two launches below
-      HIPCHK(launch_smpair(h->stream, b, hd, h->sm_pair == 2));
-      h->n_smpair++;
-      return IWAE_OK;
-    }
     HIPCHK(launch_smallm(h->stream, b));
     HIPCHK(launch_smallm(h->stream, hd));
   } else
@@ -1552,13 +1506,13 @@ static int weight_grads(iwae_handle* h, const Plan& P, bool enc, bool dec, const
 // better).
 static bool upd_tiles_ok(const iwae_handle* h) {
   long long tiles = 0;
-  for (const DenseL& d : h->dense) tiles += cdiv(d.fin + 1, 64) * cdiv(d.fout, h->upd_tn32 ? 32 : 64);
+  for (const DenseL& d : h->dense) tiles += cdiv(d.fin + 1, 64) * cdiv(d.fout, 64);
   return tiles <= kUpdMaxTiles && (int)h->dense.size() <= kUpdMaxJobs;
 }
 static bool use_update(const iwae_handle* h, const Plan& P) {
   if (!h->upd || !h->x3 || (long long)P.Bimg * P.kS > h->upd_rows) return false;
   long long tiles = 0;
-  for (const DenseL& d : h->dense) tiles += cdiv(d.fin + 1, 64) * cdiv(d.fout, h->upd_tn32 ? 32 : 64);
+  for (const DenseL& d : h->dense) tiles += cdiv(d.fin + 1, 64) * cdiv(d.fout, 64);
   return tiles <= kUpdMaxTiles && (int)h->dense.size() <= kUpdMaxJobs;
 }
 
@@ -1634,9 +1588,7 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int bucket = 0, 
     const bool fx = w.di != h->enc[0].l1;       // the input layer has no fragment-major copies
     J.fx_off = fx ? d.fx_off : -1; J.fx_steps = d.fx_steps; J.head_d = d.head_d;
     J.gx_off = d.gx_off; J.gx_steps = d.gx_steps;
-    // sample-row layers in 64 x 32 tiles (up_tn32): twice the workgroups, each
-    // with half the MFMAs and a quarter less staging over the same 1000+ rows
-    J.tn = (h->upd_tn32 && w.rows == M) ? 32 : 64;
+    J.tn = 64;
     J.tiles_m = (int)cdiv(d.fin + 1, 64); J.tiles_n = (int)cdiv(d.fout, J.tn);
     J.tile0 = tiles;
     J.nsplit = 1;
@@ -1756,9 +1708,8 @@ static int run_dw(iwae_handle* h, const Plan& P) {
     J.wide = J.mt <= 8 && J.nt > 8 ? 1 : 0;
     J.nib = (int)cdiv(J.mt, J.wide ? 8 : 13); J.mtb = (int)cdiv(J.mt, J.nib);
     J.njb = (int)cdiv(J.nt, J.wide ? 16 : 8); J.ntb = (int)cdiv(J.nt, J.njb);
-    // a k step's fixed cost in tile units, + a row-scaled dZ's and a wide block's
-    cost[q] = (double)J.mtb * J.ntb + (double)h->dw_alpha + (dz_scale(h, js[q].di, js[q].ks) ? h->dw_scale_cost : 0) +
-              (J.wide ? h->dw_wide_cost : 0);
+    // a k step's cost in tile units: its MFMA tiles + a fixed cost
+    cost[q] = (double)J.mtb * J.ntb + (double)h->dw_alpha;
     W += cost[q] * J.nib * J.njb * (double)cdiv(js[q].rows, 32);
   }
   // block-k-steps of tiles per workgroup; the grid must not exceed one workgroup
@@ -2334,8 +2285,9 @@ static bool piwae_unit(const iwae_handle* h, const Plan& P, bool ring) {
 }
 // Issue the launches tc_run / run_update recorded under defer_launch: job I'
 // and the fused update as ONE tcu_kernel launch when every workgroup of it is
-// resident at once (grid <= 256 at one 512-thread workgroup per CU: the
-// update's 147 KiB of LDS), else as the two launches they would have been.
+// resident at once (grid <= the device's CU count at one 512-thread workgroup
+// per CU: the update's 147 KiB of LDS), else as the two launches they would
+// have been.
 static int launch_pending(iwae_handle* h) {
   const bool tc = h->pend_tc_have, up = h->pend_upd_have;
   h->pend_tc_have = h->pend_upd_have = false;
@@ -2347,10 +2299,14 @@ static int launch_pending(iwae_handle* h) {
     bool one_split = true;                         // (tcu_kernel's update has no split-K path)
     for (int j = 0; j < u.njobs; ++j) one_split = one_split && u.job[j].nsplit <= 1;
     const bool ok = h->pend_tc_rt == 1 && a.xcd_slots == 0 && a.bnd_block < 0 && !u.search && !u.apply &&
-                    one_split && grid <= 256 && n_tc > 0 && h->pend_upd_cons > 0;
+                    one_split && grid <= h->n_cu && n_tc > 0 && h->pend_upd_cons > 0;
     if (ok) {
       UpdWait w;
-      w.ctr = h->tcu_ctr; w.wait_mask = h->pend_upd_mask; w.n_prod = n_tc; w.n_cons = h->pend_upd_cons;
+      w.ctr = h->tcu_ctr; w.err = h->err_dev; w.wait_mask = h->pend_upd_mask;
+      w.n_prod = n_tc; w.n_cons = h->pend_upd_cons;
+      // (fault injection: wait for a producer that does not exist, briefly)
+      w.n_expect = n_tc + (h->tcu_wait_test ? 1 : 0);
+      w.max_spins = h->tcu_wait_test ? 4096u : (1u << 24);
       const size_t lds = std::max(h->pend_tc_lds, upd_lds_bytes());
       HIPCHK(launch_tcu(h->stream, a, u, w, lds));
       h->n_tcu++;
@@ -2465,8 +2421,7 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   const bool img_bwd = img || h->engine_img_bwd;
   // job I' and the fused update as one launch (tcu_kernel): recorded here,
   // issued by launch_pending below
-  const bool tcu = img_bwd && h->tcu && use_update(h, P) && !h->dp_weighted && (h->prof_kind < 0 || h->prof_kind == 16) &&
-                   !h->upd_tn32;
+  const bool tcu = img_bwd && h->tcu && use_update(h, P) && !h->dp_weighted && (h->prof_kind < 0 || h->prof_kind == 16);
   struct DeferReset {
     iwae_handle* h;
     ~DeferReset() { h->defer_launch = false; h->pend_tc_have = h->pend_upd_have = false; }
@@ -2596,11 +2551,9 @@ static hipError_t repoint_x(hipGraphExec_t exec, hipGraphNode_t node, const iwae
   if (e != hipSuccess) return e;
   SmArgs sa = xa.sm;
   GemmArgs ga = xa.gm;
-  SmChainArgs ca = xa.sc;
   sa.A = x;
   ga.A = x;
-  ca.s[0].A = x;
-  void* args[] = {xa.kind == 1 ? (void*)&ga : xa.kind == 2 ? (void*)&ca : (void*)&sa};
+  void* args[] = {xa.kind == 1 ? (void*)&ga : (void*)&sa};
   kp.kernelParams = args;
   kp.extra = nullptr;
   return hipGraphExecKernelNodeSetParams(exec, node, &kp);
@@ -2846,11 +2799,8 @@ static int do_train_steps(iwae_handle* h, const iwae_loss_config* lc, const floa
       h->in_train_step = false; h->out_x3 = false; h->x_user = nullptr; h->capturing = false; h->loss_out = nullptr;
     }
   } reset_flag{h};
-  // steps_first > 0 makes the call's first graph short, so it reaches the GPU
-  // while the host issues the rest (measured: no change in the per-call fixed
-  // cost, profiles/r05r_steps_first.txt; off by default)
   for (int i0 = 0, S = 0; i0 < nsteps; i0 += S) {
-    S = std::min(i0 == 0 && h->steps_first > 0 ? h->steps_first : kGraphSteps, nsteps - i0);
+    S = std::min(kGraphSteps, nsteps - i0);
     const float* xi = x + i0 * xstride;
     iwae_handle::GraphRec* gp = nullptr;
     CHK(steps_graph(h, lc, P, E, B, S, xi, &gp));
@@ -2957,6 +2907,9 @@ iwae_handle* iwae_create(const iwae_config* cfg, int device) {
   if (e == hipSuccess) e = hipMalloc(&h->ds, sizeof(DevState));
   if (e == hipSuccess) e = hipMalloc(&h->tcu_ctr, 8 * sizeof(unsigned));
   if (e == hipSuccess) e = hipMemset(h->tcu_ctr, 0, 8 * sizeof(unsigned));
+  if (e == hipSuccess) e = hipHostMalloc((void**)&h->err_host, 64, hipHostMallocMapped);
+  if (e == hipSuccess) { *(volatile unsigned*)h->err_host = 0u; e = hipHostGetDevicePointer((void**)&h->err_dev, h->err_host, 0); }
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device);
   if (e == hipSuccess) e = hipMalloc(&h->wsplit_hi, (size_t)(2 * h->wsplit_elems) * sizeof(__bf16));
   if (e == hipSuccess) e = hipMalloc(&h->fx_hi, (size_t)(2 * h->fx_elems) * sizeof(__bf16));
   if (e == hipSuccess) e = hipMemset(h->fx_hi, 0, (size_t)(2 * h->fx_elems) * sizeof(__bf16));
@@ -3009,6 +2962,7 @@ void iwae_destroy(iwae_handle* h) {
   if (h->grad_own) (void)hipFree(h->grad_own);
   if (h->ds) (void)hipFree(h->ds);
   if (h->tcu_ctr) (void)hipFree(h->tcu_ctr);
+  if (h->err_host) (void)hipHostFree(h->err_host);
   if (h->loss_slots) (void)hipFree(h->loss_slots);
   if (h->nr_units) (void)hipFree(h->nr_units);
   if (h->nrb_units) (void)hipFree(h->nrb_units);
@@ -3033,10 +2987,26 @@ int iwae_set_stream(iwae_handle* h, void* s) {
   return IWAE_OK;
 }
 
+// A kernel-reported failure (an in-launch wait of the combined image-row
+// backward + update launch that gave up: that step's gradients were computed
+// from stale job-I' outputs).  Sticky until iwae_set_params.
+static int kernel_status(iwae_handle* h) {
+  if (h->err_host && *(volatile unsigned*)h->err_host)
+    return fail(h, IWAE_EHIP, "tcu_kernel: an in-launch wait for the first encoder layer's image-row backward gave "
+                              "up; the weight gradients and Adam update of that train step are invalid "
+                              "(reload the parameters)");
+  return IWAE_OK;
+}
+
 int iwae_synchronize(iwae_handle* h) {
   if (!h) return IWAE_EINVAL;
   HIPCHK(hipStreamSynchronize(h->stream));
-  return IWAE_OK;
+  return kernel_status(h);
+}
+
+int iwae_status(iwae_handle* h) {
+  if (!h) return IWAE_EINVAL;
+  return kernel_status(h);
 }
 
 static uint64_t splitmix64(uint64_t z) {
@@ -3129,8 +3099,8 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
       h->tc_rt = (int)value;
       break;
     case IWAE_KNOB_UPD: h->upd = on; break;
+    case IWAE_KNOB_TCU_WAIT_TEST: h->tcu_wait_test = on; break;
     case IWAE_KNOB_UPD_ROWS: h->upd_rows = std::max(0LL, value); break;
-    case IWAE_KNOB_UPD_TN32: h->upd_tn32 = on; break;
     case IWAE_KNOB_UPD_SLABS: h->upd_slabs = on; break;
     case IWAE_KNOB_UPD_SLAB_WG: h->upd_slab_wg = std::max(1LL, value); break;
     case IWAE_KNOB_DW_TARGET:
@@ -3155,11 +3125,6 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
     case IWAE_KNOB_X_DIRECT: h->x_direct = on; break;
     case IWAE_KNOB_TCU: h->tcu = on; break;
     case IWAE_KNOB_UPD_APPLY: h->upd_apply = on; break;
-    case IWAE_KNOB_STEPS_FIRST: h->steps_first = (int)std::max(0LL, std::min(value, (long long)kGraphSteps)); break;
-    case IWAE_KNOB_SM_CHAIN: h->sm_chain = value ? 1 : 0; break;
-    case IWAE_KNOB_SM_PAIR: h->sm_pair = (int)std::max(0LL, std::min(value, 2LL)); break;
-    case IWAE_KNOB_DW_SCALE_COST: h->dw_scale_cost = (int)std::max(0LL, std::min(value, 1000LL)); break;
-    case IWAE_KNOB_DW_WIDE_COST: h->dw_wide_cost = (int)std::max(0LL, std::min(value, 1000LL)); break;
     case IWAE_KNOB_NRING: h->nring = on; break;
     case IWAE_KNOB_NRING_TRAIN: h->nring_train = on; break;
     case IWAE_KNOB_NRING_TRAIN_ROWS: h->nr_train_rows = std::max(0LL, value); break;
@@ -3234,6 +3199,7 @@ int iwae_set_params(iwae_handle* h, const float* host, long long n) {
   CHK(check_n(h, n, host));
   CHK(upload(h, h->params, host));
   h->params_version++;
+  if (h->err_host) *(volatile unsigned*)h->err_host = 0u;   // (upload synchronized: the model is reset)
   return IWAE_OK;
 }
 
@@ -3283,6 +3249,7 @@ int iwae_set_adam_state(iwae_handle* h, const float* m, const float* v, long lon
 int iwae_train_step(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,
                     const float* const* eps, int n_eps, float* loss_dev) {
   if (!h) return IWAE_EINVAL;
+  CHK(kernel_status(h));
   return do_train(h, lc, x, B, eps, n_eps, loss_dev, true);
 }
 
@@ -3290,7 +3257,9 @@ int iwae_train_steps(iwae_handle* h, const iwae_loss_config* lc, const float* x,
                      float* loss_dev) {
   if (!h) return IWAE_EINVAL;
   if (!lc) return fail(h, IWAE_EINVAL, "loss config is NULL");
-  return do_train_steps(h, lc, x, B, nsteps, loss_dev);
+  CHK(kernel_status(h));
+  CHK(do_train_steps(h, lc, x, B, nsteps, loss_dev));
+  return kernel_status(h);
 }
 
 int iwae_train_steps_prepare(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B, int nsteps) {
@@ -3302,6 +3271,7 @@ int iwae_train_steps_prepare(iwae_handle* h, const iwae_loss_config* lc, const f
 int iwae_forward_backward(iwae_handle* h, const iwae_loss_config* lc, const float* x, int B,
                           const float* const* eps, int n_eps, float* loss_dev) {
   if (!h) return IWAE_EINVAL;
+  CHK(kernel_status(h));
   return do_train(h, lc, x, B, eps, n_eps, loss_dev, false);
 }
 
@@ -4034,14 +4004,6 @@ long long iwae_debug_count(const iwae_handle* h, int what) {
       return v[2];
     }
     case 9: return h->n_tcu;
-    case 10: {                          // smchain_kernel spin give-ups so far (synchronous read)
-      unsigned v[8] = {};
-      if (hipStreamSynchronize(h->stream) != hipSuccess ||
-          hipMemcpy(v, h->tcu_ctr, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-      return v[7];
-    }
-    case 11: return h->n_smchain;
-    case 12: return h->n_smpair;
     default: return -1;
   }
 }

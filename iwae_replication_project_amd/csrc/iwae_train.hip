@@ -1322,7 +1322,9 @@ __global__ __launch_bounds__(TC_NW * 64) void tcu_kernel(TcArgs A, UpdArgs U, Up
     if (threadIdx.x == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the XCD's L2 written back
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(W.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned p = __hip_atomic_fetch_add(W.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("" ::"v"(p));                              // (the add has returned: performed at L2)
+      upd_arrive(W);
     }
 #ifdef IWAE_TCU_TRACE
     if (threadIdx.x == 0) g_tcu_trace[b * 4 + 2] = wall_clock64();

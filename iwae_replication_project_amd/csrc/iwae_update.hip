@@ -43,12 +43,10 @@ __global__ __launch_bounds__(NW * 64) void upd_kernel(UpdArgs a) {
 hipError_t launch_update(hipStream_t st, const UpdArgs& a) {
   if (a.ntiles <= 0) return hipSuccess;
   const unsigned grid = 8u * (unsigned)(a.per_xcd + a.per_xcd2);
-  // 8 waves (two per SIMD, each half the tile's columns) unless a job uses 64 x 32 tiles
-  bool tn32 = false;
-  for (int j = 0; j < a.njobs; ++j) tn32 = tn32 || a.job[j].tn == 32;
-  if (a.waves == 16 && !tn32)
+  // 16 waves (four per SIMD, each a quarter of the tile's columns for one k step), 8 or 4
+  if (a.waves == 16)
     hipLaunchKernelGGL(upd_kernel<16>, dim3(grid), dim3(16 * 64), (size_t)2 * UP_BUF * sizeof(float), st, a);
-  else if (a.waves == 8 && !tn32)
+  else if (a.waves == 8)
     hipLaunchKernelGGL(upd_kernel<8>, dim3(grid), dim3(8 * 64), (size_t)2 * UP_BUF * sizeof(float), st, a);
   else
     hipLaunchKernelGGL(upd_kernel<4>, dim3(grid), dim3(4 * 64), (size_t)2 * UP_BUF * sizeof(float), st, a);

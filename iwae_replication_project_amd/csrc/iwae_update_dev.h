@@ -227,25 +227,41 @@ __device__ __forceinline__ int up_fx_pos(int j, int head_d) {
 __device__ unsigned long long g_tcu_trace[512 * 4];
 #endif
 
+// Every workgroup of the hand-off (producer or consumer), once it is done with
+// ctr[0], counts itself in ctr[1] (its ctr[0] add or last poll has returned by
+// then); the last of all n_prod + n_cons resets both words.  So a producer that
+// finishes after a consumer gave up still adds before the reset, and the next
+// launch starts from zero.
+__device__ __forceinline__ void upd_arrive(const UpdWait& w) {
+  const unsigned k = __hip_atomic_fetch_add(w.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (k + 1 == (unsigned)(w.n_prod + w.n_cons)) {
+    __hip_atomic_store(w.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(w.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// A wait that runs out of spins does not compute silently on stale data: it
+// counts a give-up (ctr[2], iwae_debug_count 8) and sets the host-mapped error
+// word, which iwae_status / iwae_synchronize / the next train call report as
+// IWAE_EHIP (the step's gradients and Adam update are then invalid).
 __device__ __forceinline__ void upd_wait(const UpdWait& w) {
   if (threadIdx.x == 0) {
     unsigned spins = 0;
-    while (__hip_atomic_load(w.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)w.n_prod) {
+    bool gave_up = false;
+    while (__hip_atomic_load(w.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)w.n_expect) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 24)) {
-        __hip_atomic_fetch_add(w.ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (++spins > w.max_spins) {
+        gave_up = true;
         break;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // the last consumer through resets the words (every producer has counted and
-    // every consumer has read ctr[0]: nothing in this launch reads them again)
-    const unsigned k = __hip_atomic_fetch_add(w.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (k + 1 == (unsigned)w.n_cons) {
-      __hip_atomic_store(w.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(w.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (gave_up) {
+      __hip_atomic_fetch_add(w.ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(w.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    upd_arrive(w);
 #ifdef IWAE_TCU_TRACE
     if (blockIdx.x < 512) { g_tcu_trace[blockIdx.x * 4 + 1] = wall_clock64(); g_tcu_trace[blockIdx.x * 4 + 3] = 2; }
 #endif
@@ -578,9 +594,6 @@ __device__ __forceinline__ void upd_body(const UpdArgs& a, int b, const UpdWait*
     Js.off = J.off + s * J.slab_stride;
     if (wj) upd_wait(*wj);
     upd_tile<64, NW>(a, Js, st, b, lt - s * per);
-  } else if (NW == 4 && J.tn == 32) {
-    if (wj) upd_wait(*wj);
-    upd_tile<32, 4, FULL>(a, J, st, b, T - J.tile0);
   } else {
     upd_tile<64, NW, FULL>(a, J, st, b, T - J.tile0, wj);
   }

@@ -368,7 +368,9 @@ class Flexible_Model:
         if not sync:
             return {self.loss_function: self._loss_buf}
         self._stream.synchronize()
-        return {self.loss_function: float(self._loss_buf.item())}
+        loss = float(self._loss_buf.item())
+        self._call(self._lib.iwae_status(self._h))      # an in-launch wait that gave up raises
+        return {self.loss_function: loss}
 
     def train_steps(self, x, batch_size, sync=True):
         """len(x) // batch_size consecutive train steps (F:221-F:247 each) on the
@@ -398,7 +400,9 @@ class Flexible_Model:
         if not sync:
             return losses
         self._stream.synchronize()
-        return losses.cpu().numpy()
+        out = losses.cpu().numpy()
+        self._call(self._lib.iwae_status(self._h))      # an in-launch wait that gave up raises
+        return out
 
     def prepare_train_steps(self, x, batch_size):
         """Capture every graph train_steps(x, batch_size) will replay, without
@@ -417,6 +421,15 @@ class Flexible_Model:
     def graph_captures(self):
         """Train-step graphs captured so far (iwae_debug_count id 7)."""
         return int(self._lib.iwae_debug_count(self._h, 7))
+
+    def check_kernel_status(self):
+        """Synchronize and raise if a kernel reported a failure: an in-launch
+        wait of the combined image-row backward + update launch that gave up
+        (iwae_status; give-ups counted by iwae_debug_count id 8)."""
+        self._call(self._lib.iwae_synchronize(self._h))
+        n = int(self._lib.iwae_debug_count(self._h, 8))
+        if n:
+            raise _lib.IwaeError(f"{n} in-launch wait(s) gave up")
 
     def fit(self, x, epochs=1, batch_size=100, shuffle=True, verbose=0, seed=None):
         """Keras-style loop (E:82): per epoch shuffle, batches of batch_size

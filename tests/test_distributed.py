@@ -158,3 +158,98 @@ def test_data_parallel_weighted_merge_unequal_shards_equals_full_batch():
         _, gr = O.objective_and_grads(params, spec, x[a:b], [e[:, a:b] for e in eps], "IWAE", eps[0].shape[0])
         lo.append(O.flatten_params(spec, gr))
     assert np.abs((lo[0] + lo[1]) / 2 - ref).max() > 1e-6
+
+
+# ---- world size 8: the arithmetic of the 8-GPU SCALE run (configs[2] / [4]),
+# rehearsed with gloo on CPU before any 8-rank run happens on hardware
+
+def _model8(n_img, k):
+    """A small oracle model over n_img images (the sharding arithmetic does not
+    depend on the layer widths; the small model keeps 8 ranks' compute short)."""
+    from oracle import iwae_oracle as O
+    rng = np.random.default_rng(8)
+    spec = O.ModelSpec([12, 6], [6, 12], [6, 3], [6, 16], x_dim=16)
+    params = O.glorot_init(spec, rng, out_bias=rng.normal(size=16) * 0.3)
+    x = (rng.random((n_img, 16)) < 0.3).astype(np.float64)
+    eps = O.draw_eps(spec, k, n_img, rng)
+    return O, spec, params, x, eps
+
+
+def nll_image_shard_10k(rank, world):
+    """configs[2]: 10,000 test images sharded by image over the ranks (1,250
+    each at world 8); each rank's per-image log p(x) and one all-reduce of
+    (sum, count) give the mean NLL."""
+    from iwae_replication_project_amd import distributed as D
+    O, spec, params, x, eps = _model8(10_000, 6)
+    lo, hi = D.shard_range(x.shape[0], rank, world)
+    lp = O.L_k_per_image(O.forward(params, spec, x[lo:hi], [e[:, lo:hi] for e in eps])["lw"])
+    tot = torch.tensor([lp.sum(), float(hi - lo)], dtype=torch.float64)
+    dist.all_reduce(tot)
+    return [float(-(tot[0] / tot[1])), hi - lo]
+
+
+def nll_sample_shard_8(rank, world, k=43):
+    """The sample-chunk split: k = 43 samples of every image over the ranks
+    (ragged: 6 + 6 + 6 + 5 * 5 at world 8), per-image LSE partials merged."""
+    from iwae_replication_project_amd import distributed as D
+    O, spec, params, x, eps = _model8(9, k)
+    lo, hi = D.shard_range(k, rank, world)
+    lw = O.forward(params, spec, x, [e[lo:hi] for e in eps])["lw"]
+    m = torch.tensor(lw.max(0))
+    s = torch.tensor(np.exp(lw - lw.max(0)).sum(0))
+    M, S = D.merge_lse_partials(m, s)
+    return (M + torch.log(S) - math.log(k)).numpy().tolist()
+
+
+# configs[4]: 4,096 images over 8 ranks with one ragged shard (the last rank
+# holds 509 images, the first 515): the batch-size-weighted merge of one
+# all-reduce gives the full-batch gradient of the batch-mean loss
+DP8_SHARDS = [515, 512, 512, 512, 512, 512, 512, 509]
+
+
+def dp_grads_weighted_8(rank, world):
+    from iwae_replication_project_amd import distributed as D
+    O, spec, params, x, eps = _model8(sum(DP8_SHARDS), 3)
+    lo = sum(DP8_SHARDS[:rank])
+    hi = lo + DP8_SHARDS[rank]
+    _, g = O.objective_and_grads(params, spec, x[lo:hi], [e[:, lo:hi] for e in eps], "IWAE", eps[0].shape[0])
+    t = torch.tensor(np.concatenate([O.flatten_params(spec, g), [0.0]]))
+    return D.weighted_grad_merge_(t, hi - lo).numpy().tolist()
+
+
+def test_world8_image_sharded_nll_10k_images():
+    out = spawn(nll_image_shard_10k, world=8)
+    O, spec, params, x, eps = _model8(10_000, 6)
+    ref = -np.mean(O.L_k_per_image(O.forward(params, spec, x, eps)["lw"]))
+    for r in range(8):
+        assert not isinstance(out[r], str), out[r]
+        assert out[r][1] == 1250
+        assert out[r][0] == pytest.approx(ref, rel=1e-12)
+
+
+def test_world8_sample_chunk_lse_merge_ragged():
+    out = spawn(nll_sample_shard_8, world=8)
+    O, spec, params, x, eps = _model8(9, 43)
+    ref = O.L_k_per_image(O.forward(params, spec, x, eps)["lw"])
+    from iwae_replication_project_amd.distributed import shard_range
+    assert sorted({shard_range(43, r, 8)[1] - shard_range(43, r, 8)[0] for r in range(8)}) == [5, 6]
+    for r in range(8):
+        assert not isinstance(out[r], str), out[r]
+        np.testing.assert_allclose(out[r], ref, rtol=1e-10)
+
+
+def test_world8_weighted_dp_merge_4096_images_one_ragged_shard():
+    out = spawn(dp_grads_weighted_8, world=8)
+    O, spec, params, x, eps = _model8(sum(DP8_SHARDS), 3)
+    _, g = O.objective_and_grads(params, spec, x, eps, "IWAE", eps[0].shape[0])
+    ref = O.flatten_params(spec, g)
+    for r in range(8):
+        assert not isinstance(out[r], str), out[r]
+        np.testing.assert_allclose(out[r], ref, rtol=1e-9, atol=1e-12)
+    # the plain 1/world mean of the ranks' gradients is off with the ragged shard
+    parts = []
+    for r in range(8):
+        lo = sum(DP8_SHARDS[:r]); hi = lo + DP8_SHARDS[r]
+        _, gr = O.objective_and_grads(params, spec, x[lo:hi], [e[:, lo:hi] for e in eps], "IWAE", 3)
+        parts.append(O.flatten_params(spec, gr))
+    assert np.abs(np.mean(parts, axis=0) - ref).max() > 1e-9

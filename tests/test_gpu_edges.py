@@ -262,11 +262,10 @@ def test_train_steps_equal_single_step_calls(B, n):
         assert runs[0][3] == r[3] == 2 * n
 
 
-@pytest.mark.parametrize("B,n,first", [(20, 20, 0), (20, 45, 0), (512, 3, 0), (20, 45, 2), (512, 3, 2)])
-def test_prepared_train_steps_capture_nothing_more_and_equal_unprepared(B, n, first):
+@pytest.mark.parametrize("B,n", [(20, 20), (20, 45), (512, 3)])
+def test_prepared_train_steps_capture_nothing_more_and_equal_unprepared(B, n):
     """iwae_train_steps_prepare captures the graphs of a later train_steps call
-    (one per chunk length: 45 = 32 + 13 gives two; with a first graph of 2
-    steps, knob steps_first, 45 = 2 + 32 + 11 gives three) without running anything:
+    (one per chunk length: 45 = 32 + 13 gives two) without running anything:
     weights, Adam step and an evaluation on injected noise are those of an
     unprepared model; the call then captures nothing (capture counter, id 7)
     and its losses, weights and Adam state equal the unprepared run bit for
@@ -278,14 +277,13 @@ def test_prepared_train_steps_capture_nothing_more_and_equal_unprepared(B, n, fi
     eps = [rng.standard_normal((5, 4, d)).astype(np.float32) for d in ARCH2[2]]
     runs = []
     for prep in (False, True):
-        m = _model(ARCH2, "IWAE", 50, tuning={"steps_first": first})
+        m = _model(ARCH2, "IWAE", 50)
         X = torch.from_numpy(xs).to(m.device)
         w0 = _flat(m.get_weights())
         if prep:
             c0 = m.graph_captures()
             m.prepare_train_steps(X, B)
-            r = n - min(first, n)
-            lens = ({min(first, n)} if first else set()) | ({32} if r >= 32 else set()) | ({r % 32} if r % 32 else set())
+            lens = ({32} if n >= 32 else set()) | ({n % 32} if n % 32 else set())
             assert m.graph_captures() - c0 == len(lens), (lens, m.graph_captures() - c0)
             np.testing.assert_array_equal(_flat(m.get_weights()), w0)
             assert m.get_optimizer_state()[2] == 0
@@ -324,52 +322,6 @@ def test_input_gemm_on_the_callers_x_equals_the_staged_copy(B):
     for r in runs[1:]:
         for u, v in zip(runs[0], r):
             np.testing.assert_array_equal(u, v)
-
-
-@pytest.mark.parametrize("B", [20, 7, 32, 16, 17])
-def test_first_encoder_layer_chain_and_pair_equal_three_launches(B):
-    """Up to 32 images the first encoder layer (input Dense split over K, l2,
-    head) runs on few-row launches.  Two fused forms: smchain_kernel (knob
-    sm_chain: all three layers in ONE launch, the l2 and head workgroups
-    waiting in-launch for the layer before, agent-scope release / counter /
-    acquire) and smpair_kernel (knob sm_pair, the default: l2 and head in one
-    launch, every workgroup computing the whole l2 into its LDS, no handoff).
-    Same arithmetic and summation order as the three launches (both knobs 0):
-    losses, weights and Adam state equal bit for bit over graph replays with a
-    moving batch (the launch that reads x re-pointed at each call's x), a
-    multi-step train_steps call and eager steps; no wait gave up
-    (iwae_debug_count 10); the launch counters (11, 12) show which form ran."""
-    import torch
-    rng = np.random.default_rng(91 + B)
-    xs = (rng.random((6 * B + 5, 784)) < 0.3).astype(np.float32)
-    runs = []
-    for chain, pair in ((1, 0), (0, 1), (0, 0)):
-        for graphs in (True, False):
-            m = _model(ARCH2, "IWAE", 50, use_graphs=graphs, tuning={"sm_chain": chain, "sm_pair": pair})
-            X = torch.from_numpy(xs).to(m.device)
-            losses = [m.train_step(X[i * B + i:(i + 1) * B + i])["IWAE"] for i in range(3)]
-            losses += list(m.train_steps(X[3 * B + 3:6 * B + 3], B))
-            mm, vv, st = m.get_optimizer_state()
-            n_chain = m._lib.iwae_debug_count(m._h, 11)
-            n_pair = m._lib.iwae_debug_count(m._h, 12)
-            assert (n_chain > 0) == bool(chain), (chain, n_chain)
-            assert (n_pair > 0) == bool(pair), (pair, n_pair)
-            assert m._lib.iwae_debug_count(m._h, 10) == 0
-            runs.append((np.asarray(losses, np.float32), _flat(m.get_weights()), mm, vv))
-    for r in runs[1:]:
-        for u, v in zip(runs[0], r):
-            np.testing.assert_array_equal(u, v)
-    # sm_pair 2: the pair launch with l2's products in bf16x3 (the engine's
-    # arithmetic, B fragments from the FX copy): close to the exact-f32 runs,
-    # not bitwise (Adam's first steps move a weight by up to lr wherever its
-    # gradient is near zero, so the weights get lr-scale slack)
-    m = _model(ARCH2, "IWAE", 50, tuning={"sm_chain": 0, "sm_pair": 2})
-    X = torch.from_numpy(xs).to(m.device)
-    losses = [m.train_step(X[i * B + i:(i + 1) * B + i])["IWAE"] for i in range(3)]
-    losses += list(m.train_steps(X[3 * B + 3:6 * B + 3], B))
-    assert m._lib.iwae_debug_count(m._h, 12) > 0
-    np.testing.assert_allclose(np.asarray(losses, np.float32), runs[0][0], rtol=2e-5)
-    np.testing.assert_allclose(_flat(m.get_weights()), runs[0][1], rtol=0, atol=1e-3)
 
 
 def test_train_steps_losses_copy_node_repointed_and_null():
