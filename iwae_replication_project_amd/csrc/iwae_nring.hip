@@ -317,6 +317,16 @@ __device__ __forceinline__ nr_f32x4 nr_mma(const __bf16* slot, const NrFrag& IN,
   return acc;
 #endif
   auto rd = [&](int s) {
+#ifdef IWAE_NRE_ABL
+    if (IWAE_NRE_ABL & 8) {                // (debug: no fragment reads)
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 z = {(unsigned)(uintptr_t)slot, (unsigned)s, (unsigned)lane, 0u};
+      asm volatile("" : "+v"(z));
+      wh[s % 3] = __builtin_bit_cast(nr_bf16x8, z);
+      wl[s % 3] = __builtin_bit_cast(nr_bf16x8, z);
+      return;
+    }
+#endif
     wh[s % 3] = *reinterpret_cast<const nr_bf16x8*>(slot + s * 1024 + lane * 8);
     wl[s % 3] = *reinterpret_cast<const nr_bf16x8*>(slot + s * 1024 + 512 + lane * 8);
   };
@@ -1395,6 +1405,26 @@ struct NreShapeDef {
 };
 constexpr NreShapeDef kNreShape = {7, 7, 4, 7, 4, 4, 4, 7, 4, 7, 4, 7};   // 2L 784-200-200-100-100-50
 
+// LDS-phase ablations (debug builds only, -DIWAE_NRE_ABL=<mask>; WRONG
+// results), to attribute SQ_LDS_BANK_CONFLICT to an instruction group:
+// 1 E1's staged operand reads (nre_gbwd_enc), 2 P1's staged (mu | zs) reads
+// (nre_gbwd_prior), 4 the C-layout writes of E1's dL/dh2 source, 8 the ring's
+// fragment reads (nr_mma), 16 the row-contiguous staging writes (NreRows::store)
+#ifndef IWAE_NRE_ABL
+#define IWAE_NRE_ABL 0
+#endif
+constexpr int kNreAbl = IWAE_NRE_ABL;
+// an LDS read the ablation replaces by a value the compiler cannot fold
+__device__ __forceinline__ float nre_fake(const float* p) {
+  float v = __uint_as_float((unsigned)(uintptr_t)p);
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ float4 nre_fake(const float4* p) {
+  const float* q = reinterpret_cast<const float*>(p);
+  return make_float4(nre_fake(q), nre_fake(q + 1), nre_fake(q + 2), nre_fake(q + 3));
+}
+
 // backward Dense stage (nr_dense_tanh's pipelining): v = acc (1 - y^2) (TG, y
 // of the lane's four features in registers) or acc; stored (N % 4 == 0, or
 // the padding columns get zeros), packed into OUT's NSO k steps, kept in C
@@ -1459,9 +1489,9 @@ __device__ __forceinline__ auto nre_dense(NrCtx& C, const NrFrag& IN, NrFrag& OU
 // 16 scattered 16-byte pieces per instruction.  Rows past the launch repeat
 // the last one.  Only where no DMA is in flight (hipcc waits vmcnt(0) before
 // an LDS access it cannot tell from the DMA targets).
-template <int V, int N>
+template <int V, int N, int LD = N>
 struct NreRows {
-  static_assert(N % V == 0, "row width");
+  static_assert(N % V == 0 && LD % V == 0 && LD >= N, "row width / stride");
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
   static constexpr int PER = N / V, NI = (16 * PER + 63) / 64;
   nr_u32x4 v4[V == 4 ? NI : 1];
@@ -1481,13 +1511,14 @@ struct NreRows {
     }
   }
   __device__ __forceinline__ void store(float* dst) const {
+    if (kNreAbl & 16) return;
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
       const int e = lane + 64 * k, rr = e / PER, c = (e - rr * PER) * V;
       if (e < 16 * PER) {
-        if constexpr (V == 4) *reinterpret_cast<nr_u32x4*>(dst + rr * N + c) = v4[k];
-        else *reinterpret_cast<u32x2*>(dst + rr * N + c) = v2[k];
+        if constexpr (V == 4) *reinterpret_cast<nr_u32x4*>(dst + rr * LD + c) = v4[k];
+        else *reinterpret_cast<u32x2*>(dst + rr * LD + c) = v2[k];
       }
     }
   }
@@ -1523,8 +1554,10 @@ __device__ __forceinline__ void nre_gbwd_prior(const NreLaunch& A, const NrRow& 
       if (t < NT) {
         const bool mu_part = f0 < d, ok = R.valid && f0 < 2 * d;
         const int c0 = min(mu_part ? f0 : f0 - d, d - 4);
-        const float4 mu = *reinterpret_cast<const float4*>(stg + r * 2 * d + c0);
-        const float4 zs = *reinterpret_cast<const float4*>(stg + r * 2 * d + d + c0);
+        const float4 mu = (kNreAbl & 2) ? nre_fake(reinterpret_cast<const float4*>(stg + r * 2 * d + c0))
+                                         : *reinterpret_cast<const float4*>(stg + r * 2 * d + c0);
+        const float4 zs = (kNreAbl & 2) ? nre_fake(reinterpret_cast<const float4*>(stg + r * 2 * d + d + c0))
+                                         : *reinterpret_cast<const float4*>(stg + r * 2 * d + d + c0);
         float dh[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1548,6 +1581,14 @@ __device__ __forceinline__ void nre_gbwd_prior(const NreLaunch& A, const NrRow& 
   }
 }
 
+// E1's staging in a wave's 16 KiB: (mu | zs) [16][102], h [16][50], eps
+// [16][50], the dL/dh2 source [16][54] (4096 floats).  Row strides that are 2
+// mod 4 floats: the per-element ds_read_b32 of lanes (row r, features 4g + i)
+// is then 2-way on the 32 banks of a 32-lane group (stride 100 / 52: 4-way;
+// these reads were 98 % of the kernel's SQ_LDS_BANK_CONFLICT cycles,
+// IWAE_NRE_ABL 1); every copy into it is 8-byte pieces.
+constexpr int kNreLdP = 102, kNreLdH = 50, kNreLdG = 54;
+
 // E1: the encoder head's Gaussian backward of h2 (tc_gbwd<GBWD_ENC>'s
 // arithmetic, the top layer: + dl d log N(h; 0, 1)/dh), per element (d = 50:
 // a quad may straddle dmu | dzs), every operand from this wave's LDS region
@@ -1558,9 +1599,9 @@ __device__ __forceinline__ void nre_gbwd_enc(const NreLaunch& A, const NrRow& R,
                                              NrFrag& X) {
   const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15, d = A.de;
   const float* sP = stg;
-  const float* sH = stg + 16 * 2 * d;
-  const float* sE = sH + 16 * d;
-  const float* sG = sE + 16 * d;
+  const float* sH = stg + 16 * kNreLdP;
+  const float* sE = sH + 16 * kNreLdH;
+  const float* sG = sE + 16 * kNreLdH;
   float va[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < 2 * NSO; ++t) {
@@ -1572,8 +1613,12 @@ __device__ __forceinline__ void nre_gbwd_enc(const NreLaunch& A, const NrRow& R,
         const int f = f0 + i;
         const bool mu_part = f < d, ok = R.valid && f < 2 * d;
         const int c = mu_part ? f : min(f - d, d - 1);
-        const float mu = sP[r * 2 * d + c], zs = sP[r * 2 * d + d + c];
-        const float h = sH[r * d + c], e = sE[r * d + c], G0 = sG[r * 52 + c];
+        const bool fk = kNreAbl & 1;
+        const float mu = fk ? nre_fake(sP + r * kNreLdP + c) : sP[r * kNreLdP + c];
+        const float zs = fk ? nre_fake(sP + r * kNreLdP + d + c) : sP[r * kNreLdP + d + c];
+        const float h = fk ? nre_fake(sH + r * kNreLdH + c) : sH[r * kNreLdH + c];
+        const float e = fk ? nre_fake(sE + r * kNreLdH + c) : sE[r * kNreLdH + c];
+        const float G0 = fk ? nre_fake(sG + r * kNreLdG + c) : sG[r * kNreLdG + c];
         const float ez = fexp(zs);
         const float rs = frcp(ez + kScaleEps);
         const float z = h * rs - mu * rs;
@@ -1619,7 +1664,8 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
   constexpr NreShapeDef P = kNreShape;
   constexpr int NA = P.NTPH + P.NTP2 + P.NTP1;          // phase A's units
   static_assert(NA % NR_G == 0 && NA >= 2, "phase B starts a ring group");
-  static_assert(16 * 200 <= NR_SLOT_BF16 / 2 && 16 * (4 * 50 + 52) <= NR_SLOT_BF16 / 2, "staging in a wave's slot");
+  static_assert(16 * 200 <= NR_SLOT_BF16 / 2 && 16 * (kNreLdP + 2 * kNreLdH + kNreLdG) <= NR_SLOT_BF16 / 2,
+                "staging in a wave's slot");
   static_assert(kNreGap == NR_D - NR_G, "empty units between the ring phases");
   const int t = threadIdx.x, lane = t & 63, wave = nr_wave();
   const int r = lane & 15, g = lane >> 4;
@@ -1691,21 +1737,23 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
     const int de = A.de;
     float* stg = nrs + wave * (NR_SLOT_BF16 / 2);
     // one batch of loads: the encoder head's rows, h2, eps2, and phase B's y
-    NreRows<4, 100> pe;                                   // (de == 50: nre_shape_ok)
-    NreRows<2, 50> ph, pe2;
+    NreRows<2, 100, kNreLdP> pe;                          // (de == 50: nre_shape_ok)
+    NreRows<2, 50, kNreLdH> ph, pe2;
     pe.load(A.Pe, A.ld_Pe, A.rows);
     ph.load(A.h2, A.ld_h2, A.rows);
     pe2.load(A.e2, A.ld_e2, A.rows);
     nre_load_y(A.ey2, A.ld_ey2, A.He, R, ey2);
     nre_load_y(A.ey1, A.ld_ey1, A.He, R, ey1);
     pe.store(stg);
-    ph.store(stg + 16 * 2 * de);
-    pe2.store(stg + 16 * 3 * de);
-    float* sG = stg + 16 * 4 * de;                     // [16][52]: p1^T's output, features < 52
+    ph.store(stg + 16 * kNreLdP);
+    pe2.store(stg + 16 * (kNreLdP + kNreLdH));
+    float* sG = stg + 16 * (kNreLdP + 2 * kNreLdH);    // [16][54]: p1^T's output, features < 52
 #pragma unroll
     for (int tt = 0; tt < P.NTP1; ++tt)
-      if (16 * tt + 4 * g < 52)
-        *reinterpret_cast<float4*>(sG + r * 52 + 16 * tt + 4 * g) = make_float4(kp[tt][0], kp[tt][1], kp[tt][2], kp[tt][3]);
+      if (!(kNreAbl & 4) && 16 * tt + 4 * g < 52) {
+        *reinterpret_cast<float2*>(sG + r * kNreLdG + 16 * tt + 4 * g) = make_float2(kp[tt][0], kp[tt][1]);
+        *reinterpret_cast<float2*>(sG + r * kNreLdG + 16 * tt + 4 * g + 2) = make_float2(kp[tt][2], kp[tt][3]);
+      }
     nre_gbwd_enc<(2 * 50 + 15) / 16, P.NSEH>(A, R, dl, stg, X);
   }
   nre_touch(ey2);
