@@ -65,11 +65,6 @@ constexpr int DW_TASKS = 3072 / DW_NT;        // 16-byte pieces per thread and k
 #define IWAE_DW_ABL 0
 #endif
 constexpr int kDwAbl = IWAE_DW_ABL;
-// stream slots whose fragments are read ahead of the slot being multiplied
-#ifndef IWAE_DW_PF
-#define IWAE_DW_PF 1
-#endif
-constexpr int DW_PF = IWAE_DW_PF;
 
 extern __shared__ __attribute__((aligned(16))) unsigned char dws[];
 
@@ -231,24 +226,19 @@ __device__ __forceinline__ void dw_blocks(const DwJob& J, const DwTask<>& T, DwS
   auto mul = [&](int img, const DwSet<>& Sn, unsigned char* wimg) __attribute__((always_inline)) {
     const int xh = img, xl = img + DW_XP, zh = img + 2 * DW_XP, zl = zh + DW_ZP;
     const int sh_p = WIDE ? zh : xh, sl_p = WIDE ? zl : xl, hh_p = WIDE ? xh : zh, hl_p = WIDE ? xl : zl;
-    // stream slots' fragments DW_PF slots ahead of their MFMAs (DW_PF + 1 sets)
-    constexpr int PF = DW_PF, NB = DW_PF + 1;
-    dw_bf16x8 hh[DW_NH], hl[DW_NH], sh[NB], sl[NB];
+    dw_bf16x8 hh[DW_NH], hl[DW_NH], sh[2], sl[2];
 #pragma unroll
     for (int h = 0; h < DW_NH; ++h) {
       hh[h] = dw_frag(hh_p, oh[h][0], oh[h][1]);
       hl[h] = dw_frag(hl_p, oh[h][0], oh[h][1]);
     }
-#pragma unroll
-    for (int q = 0; q < PF && q < NS; ++q) {
-      sh[q] = dw_frag(sh_p, os[q][0], os[q][1]);
-      sl[q] = dw_frag(sl_p, os[q][0], os[q][1]);
-    }
+    sh[0] = dw_frag(sh_p, os[0][0], os[0][1]);
+    sl[0] = dw_frag(sl_p, os[0][0], os[0][1]);
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
-      if (q + PF < NS) {                                  // a later stream slot's fragments in flight
-        sh[(q + PF) % NB] = dw_frag(sh_p, os[q + PF][0], os[q + PF][1]);
-        sl[(q + PF) % NB] = dw_frag(sl_p, os[q + PF][0], os[q + PF][1]);
+      if (q + 1 < NS) {                                   // the next stream slot's fragments in flight
+        sh[(q + 1) & 1] = dw_frag(sh_p, os[q + 1][0], os[q + 1][1]);
+        sl[(q + 1) & 1] = dw_frag(sl_p, os[q + 1][0], os[q + 1][1]);
       }
       // (unconditional: a slot past the block multiplies image columns that exist
       // and its accumulator is never stored -- branches around the MFMAs kept the
@@ -258,10 +248,10 @@ __device__ __forceinline__ void dw_blocks(const DwJob& J, const DwTask<>& T, DwS
         for (int h = 0; h < DW_NH; ++h) {
           {
             // bf16x3: A = X^T (i), B = dZ (j): a_hi b_hi + a_hi b_lo + a_lo b_hi
-            const dw_bf16x8& ahi = WIDE ? hh[h] : sh[q % NB];
-            const dw_bf16x8& alo = WIDE ? hl[h] : sl[q % NB];
-            const dw_bf16x8& bhi = WIDE ? sh[q % NB] : hh[h];
-            const dw_bf16x8& blo = WIDE ? sl[q % NB] : hl[h];
+            const dw_bf16x8& ahi = WIDE ? hh[h] : sh[q & 1];
+            const dw_bf16x8& alo = WIDE ? hl[h] : sl[q & 1];
+            const dw_bf16x8& bhi = WIDE ? sh[q & 1] : hh[h];
+            const dw_bf16x8& blo = WIDE ? sl[q & 1] : hl[h];
             acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi, acc[q][h], 0, 0, 0);
             acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo, acc[q][h], 0, 0, 0);
             acc[q][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi, acc[q][h], 0, 0, 0);
