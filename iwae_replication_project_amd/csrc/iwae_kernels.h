@@ -384,7 +384,6 @@ struct UpdArgs {
   int waves;                                          // 4, or 8 (64-column tiles: two waves per SIMD)
 };
 hipError_t launch_update(hipStream_t st, const UpdArgs& a);
-constexpr int kUpdGroupRows = 1024;   // rows of one unrolled group of the update kernel's reduction
 // in-launch wait of the update's first-encoder-layer tiles on the image-row
 // backward workgroups of tcu_kernel (iwae_update_dev.h, upd_wait)
 struct UpdWait {

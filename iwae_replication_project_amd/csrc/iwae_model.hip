@@ -302,6 +302,12 @@ struct iwae_handle {
     if (_r != IWAE_OK) return _r;                                              \
   } while (0)
 
+// split-K slabs of the first encoder layer's input GEMM (image rows): at most
+// this many 64-deep k chunks (A/B builds)
+#ifndef IWAE_FSLAB_MAX
+#define IWAE_FSLAB_MAX 16
+#endif
+
 static int fail(iwae_handle* h, int code, const std::string& msg) {
   h->err = msg;
   return code;
@@ -438,7 +444,7 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
   vec(h->ebern, (size_t)rows * 4);
   vec(h->ebce, (size_t)rows * 4);
   vec(h->ones, rows);
-  h->fslab_S = (int)std::min<long long>(16, cdiv(h->xdim + 1, 64));
+  h->fslab_S = (int)std::min<long long>(IWAE_FSLAB_MAX, cdiv(h->xdim + 1, 64));
   vec(h->fslab, (size_t)h->fslab_S * Bimg * r4(h->enc[0].H + 1));
   if (train && rows <= 65536) {
     h->oslab_S = 4;

@@ -1489,9 +1489,9 @@ __device__ __forceinline__ auto nre_dense(NrCtx& C, const NrFrag& IN, NrFrag& OU
 // 16 scattered 16-byte pieces per instruction.  Rows past the launch repeat
 // the last one.  Only where no DMA is in flight (hipcc waits vmcnt(0) before
 // an LDS access it cannot tell from the DMA targets).
-template <int V, int N, int LD = N>
+template <int V, int N>
 struct NreRows {
-  static_assert(N % V == 0 && LD % V == 0 && LD >= N, "row width / stride");
+  static_assert(N % V == 0, "row width");
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
   static constexpr int PER = N / V, NI = (16 * PER + 63) / 64;
   nr_u32x4 v4[V == 4 ? NI : 1];
@@ -1517,8 +1517,8 @@ struct NreRows {
     for (int k = 0; k < NI; ++k) {
       const int e = lane + 64 * k, rr = e / PER, c = (e - rr * PER) * V;
       if (e < 16 * PER) {
-        if constexpr (V == 4) *reinterpret_cast<nr_u32x4*>(dst + rr * LD + c) = v4[k];
-        else *reinterpret_cast<u32x2*>(dst + rr * LD + c) = v2[k];
+        if constexpr (V == 4) *reinterpret_cast<nr_u32x4*>(dst + rr * N + c) = v4[k];
+        else *reinterpret_cast<u32x2*>(dst + rr * N + c) = v2[k];
       }
     }
   }
@@ -1581,14 +1581,11 @@ __device__ __forceinline__ void nre_gbwd_prior(const NreLaunch& A, const NrRow& 
   }
 }
 
-// E1's staging in a wave's 16 KiB: (mu | zs) [16][102], h [16][50], eps
-// [16][50], the dL/dh2 source [16][54] (4096 floats).  Row strides that are 2
-// mod 4 floats: the per-element ds_read_b32 of lanes (row r, features 4g + i)
-// is then 2-way on the 32 banks of a 32-lane group (stride 100 / 52: 4-way;
-// these reads were 98 % of the kernel's SQ_LDS_BANK_CONFLICT cycles,
-// IWAE_NRE_ABL 1); every copy into it is 8-byte pieces.
-constexpr int kNreLdP = 102, kNreLdH = 50, kNreLdG = 54;
-
+// E1's operands are 98 % of this kernel's SQ_LDS_BANK_CONFLICT cycles (the
+// per-element ds_read_b32 below: lanes (row r, features 4g + i) on row strides
+// 100 / 52 floats are 4-way, 50 2-way; IWAE_NRE_ABL 1 removes them, at 3.4 %
+// of the kernel's wave cycles).  Strides 2 mod 4 (2-way) need 8-byte staging
+// pieces: conflicts halved, the kernel 4 us slower (profiles/r06f_nre_e1_strides_ab.txt).
 // E1: the encoder head's Gaussian backward of h2 (tc_gbwd<GBWD_ENC>'s
 // arithmetic, the top layer: + dl d log N(h; 0, 1)/dh), per element (d = 50:
 // a quad may straddle dmu | dzs), every operand from this wave's LDS region
@@ -1599,9 +1596,9 @@ __device__ __forceinline__ void nre_gbwd_enc(const NreLaunch& A, const NrRow& R,
                                              NrFrag& X) {
   const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15, d = A.de;
   const float* sP = stg;
-  const float* sH = stg + 16 * kNreLdP;
-  const float* sE = sH + 16 * kNreLdH;
-  const float* sG = sE + 16 * kNreLdH;
+  const float* sH = stg + 16 * 2 * d;
+  const float* sE = sH + 16 * d;
+  const float* sG = sE + 16 * d;
   float va[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < 2 * NSO; ++t) {
@@ -1614,11 +1611,11 @@ __device__ __forceinline__ void nre_gbwd_enc(const NreLaunch& A, const NrRow& R,
         const bool mu_part = f < d, ok = R.valid && f < 2 * d;
         const int c = mu_part ? f : min(f - d, d - 1);
         const bool fk = kNreAbl & 1;
-        const float mu = fk ? nre_fake(sP + r * kNreLdP + c) : sP[r * kNreLdP + c];
-        const float zs = fk ? nre_fake(sP + r * kNreLdP + d + c) : sP[r * kNreLdP + d + c];
-        const float h = fk ? nre_fake(sH + r * kNreLdH + c) : sH[r * kNreLdH + c];
-        const float e = fk ? nre_fake(sE + r * kNreLdH + c) : sE[r * kNreLdH + c];
-        const float G0 = fk ? nre_fake(sG + r * kNreLdG + c) : sG[r * kNreLdG + c];
+        const float mu = fk ? nre_fake(sP + r * 2 * d + c) : sP[r * 2 * d + c];
+        const float zs = fk ? nre_fake(sP + r * 2 * d + d + c) : sP[r * 2 * d + d + c];
+        const float h = fk ? nre_fake(sH + r * d + c) : sH[r * d + c];
+        const float e = fk ? nre_fake(sE + r * d + c) : sE[r * d + c];
+        const float G0 = fk ? nre_fake(sG + r * 52 + c) : sG[r * 52 + c];
         const float ez = fexp(zs);
         const float rs = frcp(ez + kScaleEps);
         const float z = h * rs - mu * rs;
@@ -1664,8 +1661,7 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
   constexpr NreShapeDef P = kNreShape;
   constexpr int NA = P.NTPH + P.NTP2 + P.NTP1;          // phase A's units
   static_assert(NA % NR_G == 0 && NA >= 2, "phase B starts a ring group");
-  static_assert(16 * 200 <= NR_SLOT_BF16 / 2 && 16 * (kNreLdP + 2 * kNreLdH + kNreLdG) <= NR_SLOT_BF16 / 2,
-                "staging in a wave's slot");
+  static_assert(16 * 200 <= NR_SLOT_BF16 / 2 && 16 * (4 * 50 + 52) <= NR_SLOT_BF16 / 2, "staging in a wave's slot");
   static_assert(kNreGap == NR_D - NR_G, "empty units between the ring phases");
   const int t = threadIdx.x, lane = t & 63, wave = nr_wave();
   const int r = lane & 15, g = lane >> 4;
@@ -1737,23 +1733,21 @@ __global__ __launch_bounds__(NR_W * 64, 1) void nre_kernel(NreLaunch A) {
     const int de = A.de;
     float* stg = nrs + wave * (NR_SLOT_BF16 / 2);
     // one batch of loads: the encoder head's rows, h2, eps2, and phase B's y
-    NreRows<2, 100, kNreLdP> pe;                          // (de == 50: nre_shape_ok)
-    NreRows<2, 50, kNreLdH> ph, pe2;
+    NreRows<4, 100> pe;                                   // (de == 50: nre_shape_ok)
+    NreRows<2, 50> ph, pe2;
     pe.load(A.Pe, A.ld_Pe, A.rows);
     ph.load(A.h2, A.ld_h2, A.rows);
     pe2.load(A.e2, A.ld_e2, A.rows);
     nre_load_y(A.ey2, A.ld_ey2, A.He, R, ey2);
     nre_load_y(A.ey1, A.ld_ey1, A.He, R, ey1);
     pe.store(stg);
-    ph.store(stg + 16 * kNreLdP);
-    pe2.store(stg + 16 * (kNreLdP + kNreLdH));
-    float* sG = stg + 16 * (kNreLdP + 2 * kNreLdH);    // [16][54]: p1^T's output, features < 52
+    ph.store(stg + 16 * 2 * de);
+    pe2.store(stg + 16 * 3 * de);
+    float* sG = stg + 16 * 4 * de;                     // [16][52]: p1^T's output, features < 52
 #pragma unroll
     for (int tt = 0; tt < P.NTP1; ++tt)
-      if (!(kNreAbl & 4) && 16 * tt + 4 * g < 52) {
-        *reinterpret_cast<float2*>(sG + r * kNreLdG + 16 * tt + 4 * g) = make_float2(kp[tt][0], kp[tt][1]);
-        *reinterpret_cast<float2*>(sG + r * kNreLdG + 16 * tt + 4 * g + 2) = make_float2(kp[tt][2], kp[tt][3]);
-      }
+      if (!(kNreAbl & 4) && 16 * tt + 4 * g < 52)
+        *reinterpret_cast<float4*>(sG + r * 52 + 16 * tt + 4 * g) = make_float4(kp[tt][0], kp[tt][1], kp[tt][2], kp[tt][3]);
     nre_gbwd_enc<(2 * 50 + 15) / 16, P.NSEH>(A, R, dl, stg, X);
   }
   nre_touch(ey2);

@@ -1305,12 +1305,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tc_kernel(TcArgs A) {
 // blocks from n_tc_pad run upd_kernel's body, whose first-encoder-layer tiles
 // (the jobs in W.wait_mask) wait on that counter -- the sample-row tiles, the
 // bulk of the launch, run beside job I' instead of after it.
-#ifndef IWAE_TCU_SHORT
-#define IWAE_TCU_SHORT 1
-#endif
-// SHORT: every update job reduces at most one unrolled group of rows
-// (kUpdGroupRows: the B = 20 step), so the multi-group path is not compiled
-template <unsigned KM, bool SHORT = false>
+template <unsigned KM>
 __global__ __launch_bounds__(TC_NW * 64) void tcu_kernel(TcArgs A, UpdArgs U, UpdWait W, int n_tc, int n_tc_pad) {
   const int b = (int)blockIdx.x;
 #ifdef IWAE_TCU_TRACE
@@ -1336,7 +1331,7 @@ __global__ __launch_bounds__(TC_NW * 64) void tcu_kernel(TcArgs A, UpdArgs U, Up
 #endif
     return;
   }
-  upd_body<TC_NW, !IWAE_TCU_LEAN, SHORT>(U, b - n_tc_pad, &W);
+  upd_body<TC_NW, !IWAE_TCU_LEAN>(U, b - n_tc_pad, &W);
 #ifdef IWAE_TCU_TRACE
   __syncthreads();
   if (threadIdx.x == 0 && b < 512) g_tcu_trace[b * 4 + 2] = wall_clock64();
@@ -1347,11 +1342,7 @@ hipError_t launch_tcu(hipStream_t st, const TcArgs& a, const UpdArgs& u, const U
   const int n_tc = a.block_start[kTcMaxJobs];
   const int n_pad = (n_tc + 7) & ~7;                      // the update's blocks keep their b % 8 XCD groups
   const int grid = n_pad + 8 * (u.per_xcd + u.per_xcd2);
-  bool short_rows = IWAE_TCU_SHORT != 0;
-  for (int j = 0; j < u.njobs; ++j) short_rows = short_rows && u.job[j].rows <= kUpdGroupRows;
-  if (IWAE_TC_NARROW && IWAE_TC_KM && a.kinds && !(a.kinds & ~kTcKindsImgBwd) && short_rows)
-    hipLaunchKernelGGL((tcu_kernel<kTcKindsImgBwd, true>), dim3(grid), dim3(TC_NW * 64), lds_bytes, st, a, u, w, n_tc, n_pad);
-  else if (IWAE_TC_NARROW && IWAE_TC_KM && a.kinds && !(a.kinds & ~kTcKindsImgBwd))
+  if (IWAE_TC_NARROW && IWAE_TC_KM && a.kinds && !(a.kinds & ~kTcKindsImgBwd))
     hipLaunchKernelGGL((tcu_kernel<kTcKindsImgBwd>), dim3(grid), dim3(TC_NW * 64), lds_bytes, st, a, u, w, n_tc, n_pad);
   else if (IWAE_TC_KM && a.kinds && !(a.kinds & ~kTcKindsBwd))
     hipLaunchKernelGGL((tcu_kernel<kTcKindsBwd>), dim3(grid), dim3(TC_NW * 64), lds_bytes, st, a, u, w, n_tc, n_pad);
@@ -1395,7 +1386,7 @@ hipError_t tc_setup_attributes() {
                        (const void*)tc_kernel<1, kTcKindsBwd>, (const void*)tc_kernel<2, kTcKindsBwd>,
                        (const void*)tc_kernel<4, kTcKindsBwd>, (const void*)tcu_kernel<kTcKindsAll>,
                        (const void*)tcu_kernel<kTcKindsBwd>, (const void*)tc_kernel<1, kTcKindsBwdRows>, (const void*)tc_kernel<1, kTcKindsImgBwd>,
-                       (const void*)tcu_kernel<kTcKindsImgBwd>, (const void*)tcu_kernel<kTcKindsImgBwd, true>};
+                       (const void*)tcu_kernel<kTcKindsImgBwd>};
   for (const void* f : fns) {
     const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;

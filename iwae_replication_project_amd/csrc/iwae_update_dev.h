@@ -16,7 +16,6 @@ constexpr int UP_S = 72;                    // dwords per LDS row: 128 bf16 + 16
 constexpr int UP_PLANE = 64 * UP_S;         // dwords per plane
 constexpr int UP_BUF = 4 * UP_PLANE;        // X hi, X lo, dZ hi, dZ lo
 constexpr int UP_G = 8;                     // iterations per unrolled group (1024 rows)
-static_assert(UP_G * UP_RI == kUpdGroupRows, "iwae_kernels.h kUpdGroupRows");
 // Timing ablations (debug builds only, -DIWAE_UPD_ABLATE=<mask>; WRONG results):
 // 4 no operand loads, 8 stop after the reduction, 16 no FX / GX copies, 32 no
 // Adam, 64 no reduction (tools/upd_ablate.sh)
@@ -274,7 +273,7 @@ __device__ __forceinline__ void upd_wait(const UpdWait& w) {
 // workgroups, half the MFMA and a quarter less staging per workgroup).
 // (FULL false: the combined launch's update -- no slab apply modes, which
 // launch_pending rules out; less code for its workgroups to fetch)
-template <int TN, int NW, bool FULL = true, bool SHORT = false>
+template <int TN, int NW, bool FULL = true>
 __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, const AdamState& st, int b, int lt,
                                          const UpdWait* w = nullptr) {
   constexpr int NT = UpCfg<NW>::NT, TPR = NT / 64;   // threads per epilogue row
@@ -383,10 +382,7 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
     UpRegs<TN, NW> R0, R1;
     start(R0, R1);
     group(R0, R1, 0, false);
-  } else if (!SHORT && ngrp > 1) {
-    // (SHORT: every job of the launch has at most one group of rows -- the
-    // combined launch at B = 20 -- so this second copy of the unrolled group
-    // is not compiled: less code for the launch's workgroups to fetch)
+  } else if (ngrp > 1) {
     if (w) upd_wait(*w);
     // the sets are carried into the next group: renamed once per 1024 rows
     UpRegs<TN, NW> R0, R1;
@@ -560,7 +556,7 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
 // image-row workgroups).
 // FULL false (the combined launch): every job has nsplit 1 and no apply mode
 // (launch_pending checks), so neither the split-K path nor the apply code is compiled
-template <int NW, bool FULL = true, bool SHORT = false>
+template <int NW, bool FULL = true>
 __device__ __forceinline__ void upd_body(const UpdArgs& a, int b, const UpdWait* w) {
   // tile of this workgroup: consecutive tiles (sharing an operand slice) on one XCD
   // (the long reductions -- tiles [0, nheavy) -- are spread evenly over the
@@ -599,7 +595,7 @@ __device__ __forceinline__ void upd_body(const UpdArgs& a, int b, const UpdWait*
     if (wj) upd_wait(*wj);
     upd_tile<64, NW>(a, Js, st, b, lt - s * per);
   } else {
-    upd_tile<64, NW, FULL, SHORT>(a, J, st, b, T - J.tile0, wj);
+    upd_tile<64, NW, FULL>(a, J, st, b, T - J.tile0, wj);
   }
 }
 
