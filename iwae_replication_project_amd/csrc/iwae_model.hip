@@ -302,12 +302,6 @@ struct iwae_handle {
     if (_r != IWAE_OK) return _r;                                              \
   } while (0)
 
-// split-K slabs of the first encoder layer's input GEMM (image rows): at most
-// this many 64-deep k chunks (A/B builds)
-#ifndef IWAE_FSLAB_MAX
-#define IWAE_FSLAB_MAX 16
-#endif
-
 static int fail(iwae_handle* h, int code, const std::string& msg) {
   h->err = msg;
   return code;
@@ -444,7 +438,7 @@ static int ensure_capacity(iwae_handle* h, int Bimg, int rows, bool train) {
   vec(h->ebern, (size_t)rows * 4);
   vec(h->ebce, (size_t)rows * 4);
   vec(h->ones, rows);
-  h->fslab_S = (int)std::min<long long>(IWAE_FSLAB_MAX, cdiv(h->xdim + 1, 64));
+  h->fslab_S = (int)std::min<long long>(16, cdiv(h->xdim + 1, 64));
   vec(h->fslab, (size_t)h->fslab_S * Bimg * r4(h->enc[0].H + 1));
   if (train && rows <= 65536) {
     h->oslab_S = 4;
@@ -1101,11 +1095,21 @@ static bool smallm_ok(const iwae_handle* h, int rows) {
 // Number of partial slabs the first encoder Dense writes into fslab when only
 // that launch runs (enc0_forward(l1_only), the train engine's image-row job
 // sums them).
+// The split-K GEMM's k chunk (a multiple of 64): at most fslab_S slabs, and
+// no more than one round of the chip needs (64 x 64 tiles x slabs <= 256
+// workgroups).  B = 512: 7 slabs of 128 in 224 workgroups instead of 13 of 64
+// in 416 -- the GEMM 13.2 -> 9.9 us, job I's slab sum 26.0 -> 24.8 us
+// (profiles/r06g_input_gemm_slabs_ab.txt); the NLL chunks (<= 256 images) keep 13.
+static long long enc0_kchunk(const iwae_handle* h, int Bimg) {
+  const DenseL& d1 = h->dense[h->enc[0].l1];
+  const long long K = d1.fin + 1, tiles = cdiv(d1.fout, 64) * cdiv(Bimg, 64);
+  const long long S = std::max(1LL, std::min<long long>(h->fslab_S, 256 / std::max(1LL, tiles)));
+  return cdiv(cdiv(K, S), 64) * 64;
+}
 static int enc0_nslab(const iwae_handle* h, int Bimg) {
   const DenseL& d1 = h->dense[h->enc[0].l1];
   if (smallm_ok(h, Bimg)) return (int)std::min<long long>(std::min(4, h->fslab_S), cdiv(d1.fin + 1, 128));
-  const long long K = d1.fin + 1, kchunk = cdiv(cdiv(K, h->fslab_S), 64) * 64;
-  return (int)cdiv(K, kchunk);
+  return (int)cdiv(d1.fin + 1, enc0_kchunk(h, Bimg));
 }
 
 // First encoder layer on the images (Stochastic_layer 0, F:58): y1, y2 and
@@ -1181,7 +1185,7 @@ static int enc0_forward(iwae_handle* h, const Plan& P, bool l1_only = false) {
     a.C = h->fslab; a.ldc = h->eb[0].y1.ld;
     a.M = P.Bimg; a.N = d.fout; a.K = d.fin + 1;
     if (use_split_b(h)) { a.Bhi = h->wsplit_hi + d.f_off; a.Blo = h->wsplit_lo + d.f_off; a.ldbx = d.ldF; }
-    a.kchunk = (int)(cdiv(cdiv(a.K, h->fslab_S), 64) * 64);
+    a.kchunk = (int)enc0_kchunk(h, P.Bimg);
     const int S = (int)cdiv(a.K, a.kchunk);
     a.c_split_stride = (long long)P.Bimg * a.ldc;
     if (h->x_user) {
