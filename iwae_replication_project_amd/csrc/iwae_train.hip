@@ -1032,30 +1032,30 @@ __device__ __forceinline__ void tc_gbwd0_p(const TcArgs& A, CJob& J, COp& S, int
   __amdgpu_buffer_rsrc_t rsrc[NSRC];
 #pragma unroll
   for (int u = 0; u < NSRC; ++u) rsrc[u] = buf_rsrc(S.src[u]);
-  const __amdgpu_buffer_rsrc_t rh = buf_rsrc(S.h), re = buf_rsrc(S.eps), rd = buf_rsrc(A.dlw);
+  const __amdgpu_buffer_rsrc_t re = buf_rsrc(S.eps), rd = buf_rsrc(A.dlw);
   const int c0 = 4 * qi;
   for (int r0 = 0; r0 < nrows; r0 += IPP) {
     const int rr = r0 + ii;
     const int b = row0 + min(rr, nrows - 1);
     const bool live = rr < nrows && sg < nsg && c0 < d;
     const float* Pr = S.P + (size_t)b * S.ld_P;
-    float mu[4], rs4[4];
+    float mu[4], sc4[4], rs4[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int c = min(c0 + q, d - 1);
       mu[q] = Pr[c];
-      rs4[q] = frcp(fexp(Pr[d + c]) + kScaleEps);
+      sc4[q] = fexp(Pr[d + c]) + kScaleEps;
+      rs4[q] = frcp(sc4[q]);
     }
     float dmu[4] = {0.f, 0.f, 0.f, 0.f}, dsc[4] = {0.f, 0.f, 0.f, 0.f};
     for (int s0 = sg; s0 < kS; s0 += nsg * SPT) {
-      float4 hv[SPT], ev[SPT], gs[SPT][NSRC];
+      float4 ev[SPT], gs[SPT][NSRC];
       float dl[SPT];
 #pragma unroll
       for (int i = 0; i < SPT; ++i) {
         const int s = s0 + i * nsg;
         const bool ok = live && s < kS;
         const long long r = (long long)b * kS + min(s, kS - 1);
-        hv[i] = bld4(rh, ok ? (unsigned)(r * S.ld_h + c0) * 4u : kOOB);
         ev[i] = bld4(re, ok ? (unsigned)(r * S.ld_eps + c0) * 4u : kOOB);
         dl[i] = bld1(rd, ok ? (unsigned)r * 4u : kOOB);
 #pragma unroll
@@ -1066,7 +1066,10 @@ __device__ __forceinline__ void tc_gbwd0_p(const TcArgs& A, CJob& J, COp& S, int
       for (int i = 0; i < SPT; ++i) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float h = f4_at(hv[i], q), e = f4_at(ev[i], q);
+          // h = eps * scale + mu, recomputed from eps and the image's (mu, zs)
+          // exactly as the forward formed it (h1 is not read: 4 of the op's
+          // ~20 bytes per sample and column, the large-batch step's h1 slab)
+          const float e = f4_at(ev[i], q), h = e * sc4[q] + mu[q];
           float G = (f4_at(gs[i][0], q) + f4_at(gs[i][1], q)) + f4_at(gs[i][2], q);
           if (A.unit_w) G *= dl[i];            // sources from a unit-weight chain: this sample's weight
           const float z = h * rs4[q] - mu[q] * rs4[q];
