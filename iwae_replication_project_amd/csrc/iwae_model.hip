@@ -2430,8 +2430,12 @@ static int engine_train_body(iwae_handle* h, const Plan& P, const EpsSet& E, boo
   // against the row-block Gaussian backward + two few-row launches)
   const bool img_bwd = img || h->engine_img_bwd;
   // job I' and the fused update as one launch (tcu_kernel): recorded here,
-  // issued by launch_pending below
-  const bool tcu = img_bwd && h->tcu && use_update(h, P) && !h->dp_weighted && (h->prof_kind < 0 || h->prof_kind == 16);
+  // issued by launch_pending below.  From 256 sample rows: below, the update's
+  // sample-row tiles are too short to cover job I' and the in-launch hand-off
+  // costs more than the launch boundary (configs[0], 100 rows: 0.0958 vs
+  // 0.0968 ms per step as two launches; profiles/r06j_tcu_rows_ab.txt)
+  const bool tcu = img_bwd && h->tcu && use_update(h, P) && !h->dp_weighted && (h->prof_kind < 0 || h->prof_kind == 16) &&
+                   (long long)P.Bimg * P.kS >= 256;
   struct DeferReset {
     iwae_handle* h;
     ~DeferReset() { h->defer_launch = false; h->pend_tc_have = h->pend_upd_have = false; }
