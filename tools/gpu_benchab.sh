@@ -22,6 +22,6 @@ for rep in $(seq 1 ${REPS:-2}); do
     if [ -n "$lib" ]; then export IWAE_HIP_LIB=$lib; else unset IWAE_HIP_LIB; fi
     timeout -k 10 200 python -u bench.py --steps 300 --warmup 20 --no-cpu --no-stats --nll-images ${NLL_N:-6000} ${EXTRA:-} \
       > $O/r$i.json 2> $O/r$i.err || { tail -5 $O/r$i.err; exit 1; }
-    python -c "import json; d=json.loads(open('$O/r$i.json').read().strip().splitlines()[-1]); lb=d.get('large_batch') or {}; print('${lib:-in-tree}', 'b20', d['ms_per_step'], 'c0', d['configs0_train']['ms_per_step'], 'nll', (d.get('nll') or {}).get('value'), 'b512', lb.get('ms_per_step'))" | tee -a $O/summary.txt
+    python -c "import json; d=json.loads(open('$O/r$i.json').read().strip().splitlines()[-1]); lb=d.get('large_batch') or {}; print('${lib:-in-tree}', 'b20', d['ms_per_step'], 'c0', (d.get('configs0_train') or {}).get('ms_per_step'), 'nll', (d.get('nll') or {}).get('value'), 'b512', lb.get('ms_per_step'))" | tee -a $O/summary.txt
   done
 done
