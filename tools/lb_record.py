@@ -24,7 +24,9 @@ KERNELS = [
     ("encoder / prior backward-data (nre_kernel)", r"nre_kernel", None, "nre"),
     ("ring backward-data, output MLP + encoder / prior (nrbe_kernel)", r"nrbe_kernel", None, "nrbe"),
     ("weight gradients (dw_kernel)", r"dw_kernel", None, "dw"),
-    ("weight gradients (upd_kernel slab pass)", r"upd_kernel", 600, "dw"),
+    ("first-layer weight gradients + Adam + FX copies (upd_kernel)", r"upd_kernel", None, None),
+    ("first encoder layer input GEMM, split-K slabs (gemm_kernel)", r"gemm_kernel", None, None),
+    ("bound / loss reduction (bound_kernel)", r"bound_kernel", None, None),
     ("first encoder layer l2 / head, image rows (tc_kernel I)", r"tc_kernel<1>#0", 256, "img_fwd"),
     ("first encoder layer backward, image rows (tc_kernel I')", r"tc_kernel<1>#1", 256, "img_bwd"),
     ("Adam over the slabs (adam_kernel)", r"adam_kernel", None, None),
@@ -47,10 +49,12 @@ def main():
         g = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)
         w = int(r.get("Workgroup_Size_X", r.get("Workgroup_Size", 1)) or 1)
         name = r["Kernel_Name"].split("(")[0]
-        if name.endswith("tc_kernel<1>") and g // max(1, w) == 256:
-            # the step's two image-row launches alternate: job I (forward) then job I' (backward)
-            name += f"#{seen[name] % 2}"
-            seen[r["Kernel_Name"].split("(")[0]] += 1
+        if re.search(r"tc_kernel<1(, \d+u)?>$", name) and g // max(1, w) == 256:
+            # the step's two image-row launches alternate: job I (forward) then job I' (backward);
+            # the kind-mask template argument (kTcKindsFwd / kTcKindsImgBwd) is dropped from the label
+            base = re.sub(r"tc_kernel<1(, \d+u)?>$", "tc_kernel<1>", name)
+            name = base + f"#{seen[base] % 2}"
+            seen[base] += 1
         dur[(name, g // max(1, w))].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     pmc = json.load(open(pmc_path)) if pmc_path != "-" else {}
     rec = {}
