@@ -139,8 +139,8 @@ def roofline_of(flop, nbytes, us, peak_tflops=None, hbm_gbs=None):
                 flop_per_byte=round(ai, 1), ridge=round(pk * 1e3 / hb, 1), alg_bytes=nbytes, flop=flop)
 
 
-LB_RECORD = "r05_large_batch_kernels.json"     # the large-batch step's committed kernel record
-PMC_RECORD = "r05_pmc_traffic.json"            # the B = 20 step's committed per-launch HBM traffic (PMC)
+LB_RECORD = "r06_large_batch_kernels.json"     # the large-batch step's committed kernel record
+PMC_RECORD = "r06_pmc_traffic.json"            # the B = 20 step's committed per-launch HBM traffic (PMC)
 
 
 PRECISION = ("fp32 values and fp32 accumulation everywhere; every sample-row matrix product of the train step "
