@@ -163,9 +163,13 @@ enum iwae_knob {
                                       launch, its tiles of that layer waiting in-launch for job I' (1) */
   IWAE_KNOB_UPD_APPLY = 35,       /* beyond UPD_ROWS: the gradient pass's slabs summed, Adam and the FX / GX copies
                                       in one update-kernel launch instead of the Adam and FX-refresh launches (1) */
-  IWAE_KNOB_TCU_WAIT_TEST = 41    /* fault injection for tests (0): every in-launch wait of the TCU launch waits
+  IWAE_KNOB_TCU_WAIT_TEST = 41,   /* fault injection for tests (0): every in-launch wait of the TCU launch waits
                                       for one producer more than exists, with a short spin bound, so it gives up and
                                       the failure must surface through iwae_status (results of that step invalid) */
+  IWAE_KNOB_TCU_WT = 42           /* the TCU launch's hand-off write-through where every waiting tile is one
+                                      reduction iteration (1): job I' stores its outputs sc1 and adds to the counter
+                                      without a release fence, the waiting tiles poll and load dZ sc1 without an
+                                      acquire; 0: release / acquire fences */
   /* 10, 36-40: removed variants measured slower (64 x 32 update tiles, a short
      first graph, the chained / paired first-encoder-layer launches, dw_kernel
      cost-model terms); iwae_set_tuning rejects them with IWAE_EINVAL */

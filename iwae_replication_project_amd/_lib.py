@@ -21,7 +21,7 @@ KNOBS = {
     "smallm_rows": 14, "out_x3_rows": 15, "mg_waves": 16, "nll_rows": 17, "wide_rows": 18, "dw_wide": 19, "ld_align": 20,
     "nring": 21, "nring_train": 22, "nring_train_rows": 23, "nring_bwd": 24, "wide_rt": 25, "upd_waves": 26,
     "nll_imgs": 27, "dw_wg": 28, "piwae_one": 29, "dw_alpha": 30,
-    "img_rows_fwd": 31, "img_rows_bwd": 32, "x_direct": 33, "tcu": 34, "upd_apply": 35, "tcu_wait_test": 41,
+    "img_rows_fwd": 31, "img_rows_bwd": 32, "x_direct": 33, "tcu": 34, "upd_apply": 35, "tcu_wait_test": 41, "tcu_wt": 42,
 }
 LOSS_IDS = {
     "VAE": 0, "IWAE": 1, "VAE_V1": 2, "L_alpha": 3, "L_power_p": 4,

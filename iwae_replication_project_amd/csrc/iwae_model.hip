@@ -217,6 +217,7 @@ struct iwae_handle {
   unsigned* tcu_ctr = nullptr;       // its in-launch counters (UpdWait::ctr; zero between launches)
   unsigned* err_host = nullptr;      // host-mapped error word a kernel sets when an in-launch wait gives up
   unsigned* err_dev = nullptr;       // ... its device address (UpdWait::err)
+  int tcu_wt = 1;                    // the combined launch's hand-off write-through (knob TCU_WT; launch_tcu decides)
   int tcu_wait_test = 0;             // fault injection (knob TCU_WAIT_TEST): every combined-launch wait gives up
   int n_cu = 256;                    // compute units of the device (hipDeviceAttributeMultiprocessorCount)
   bool defer_launch = false;         // (during a step) tc_run / run_update record their launch instead
@@ -1547,7 +1548,7 @@ static int run_update(iwae_handle* h, const Plan& P, bool adam, int bucket = 0, 
                       const float* scale_dev = nullptr, bool from_slabs = false) {
   if (!st) st = h->stream;
   const int L = h->L, M = P.Bimg * P.kS;
-  constexpr long long UP_ROWS_ITER = 128;      // rows per reduction iteration of the update kernel
+  constexpr long long UP_ROWS_ITER = kUpdRowsPerIter;   // rows per reduction iteration of the update kernel
   struct WJ { int di; const Mat* A; const Mat* dZ; int rows; const float* ks; };
   std::vector<WJ> js;
   for (int i = 0; i < L; ++i) {
@@ -2317,6 +2318,12 @@ static int launch_pending(iwae_handle* h) {
       // (fault injection: wait for a producer that does not exist, briefly)
       w.n_expect = n_tc + (h->tcu_wait_test ? 1 : 0);
       w.max_spins = h->tcu_wait_test ? 4096u : (1u << 24);
+      // write-through hand-off where every waiting tile takes the update's
+      // one-iteration path (its dZ loads are the sc1 ones): launch_tcu keeps it
+      // only on the write-through instantiation
+      w.wt = h->tcu_wt;
+      for (int j = 0; j < u.njobs; ++j)
+        if ((w.wait_mask >> j) & 1u) w.wt = w.wt && u.job[j].rows > 0 && u.job[j].rows <= kUpdRowsPerIter;
       const size_t lds = std::max(h->pend_tc_lds, upd_lds_bytes());
       HIPCHK(launch_tcu(h->stream, a, u, w, lds));
       h->n_tcu++;
@@ -3114,6 +3121,7 @@ int iwae_set_tuning(iwae_handle* h, int knob, long long value) {
       break;
     case IWAE_KNOB_UPD: h->upd = on; break;
     case IWAE_KNOB_TCU_WAIT_TEST: h->tcu_wait_test = on; break;
+    case IWAE_KNOB_TCU_WT: h->tcu_wt = on; break;
     case IWAE_KNOB_UPD_ROWS: h->upd_rows = std::max(0LL, value); break;
     case IWAE_KNOB_UPD_SLABS: h->upd_slabs = on; break;
     case IWAE_KNOB_UPD_SLAB_WG: h->upd_slab_wg = std::max(1LL, value); break;

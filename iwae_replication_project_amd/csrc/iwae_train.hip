@@ -39,6 +39,9 @@
 #ifndef IWAE_TCU_LEAN
 #define IWAE_TCU_LEAN 1       // the combined launch's update without the split-K and slab-apply code
 #endif
+#ifndef IWAE_TCU_WT
+#define IWAE_TCU_WT 1         // the combined launch's write-through hand-off (UpdWait::wt) where the host allows it
+#endif
 #ifndef IWAE_TC_NARROW
 #define IWAE_TC_NARROW 1      // ... 16-row backward launches and job I' on the narrower sets too
 #endif
@@ -130,11 +133,12 @@ __device__ __forceinline__ void tc_put1(const TcBuf& B, int o, float v) {
 // workgroups (RT >= 2, large batches) store with sc1: the lines leave the
 // XCD's L2 instead of displacing the weight fragments every workgroup
 // re-reads from it (hundreds of MB of activations stream out per launch).
+// WT: the producer side of tcu_kernel's write-through hand-off (sc1 too).
 // base must be wave-uniform; idx in floats.
-template <int RT>
+template <int RT, bool WT = false>
 __device__ __forceinline__ void tc_st4(float* base, size_t idx, float4 v) {
   const tc_u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-  __builtin_amdgcn_raw_buffer_store_b128(u, buf_rsrc(base), (unsigned)(idx * 4), 0, RT >= 2 ? 16 : 0);
+  __builtin_amdgcn_raw_buffer_store_b128(u, buf_rsrc(base), (unsigned)(idx * 4), 0, (RT >= 2 || WT) ? 16 : 0);
 }
 template <int RT>
 __device__ __forceinline__ void tc_st2(float* base, size_t idx, float a, float b) {
@@ -142,9 +146,10 @@ __device__ __forceinline__ void tc_st2(float* base, size_t idx, float a, float b
   const tc_u32x2 u = {__float_as_uint(a), __float_as_uint(b)};
   __builtin_amdgcn_raw_buffer_store_b64(u, buf_rsrc(base), (unsigned)(idx * 4), 0, RT >= 2 ? 16 : 0);
 }
-template <int RT>
+template <int RT, bool WT = false>
 __device__ __forceinline__ void tc_st1(float* base, size_t idx, float a) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(a), buf_rsrc(base), (unsigned)(idx * 4), 0, RT >= 2 ? 16 : 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(a), buf_rsrc(base), (unsigned)(idx * 4), 0,
+                                        (RT >= 2 || WT) ? 16 : 0);
 }
 
 // zero padding [width, next_k) of every row of B (ones column at width if asked)
@@ -280,7 +285,7 @@ __device__ __forceinline__ float2 tc_eps2(const TcArgs& A, int layer, int d, int
 
 // ------------------------------------------------------------ epilogues
 // TANH / TGRAD / LIN: features f0..f0+3 of row rt*16 + r
-template <int RT, int KIND>
+template <int RT, int KIND, bool WT = false>
 __device__ __forceinline__ void tc_store_act(COp& S, const TcBuf& OUT, int t, const tc_f32x4 (&acc)[RT],
                                              const float4 (&yv)[RT], int row0, int nrows) {
   const int lane = threadIdx.x & 63;
@@ -321,11 +326,11 @@ __device__ __forceinline__ void tc_store_act(COp& S, const TcBuf& OUT, int t, co
 #endif
       const size_t o = (size_t)(row0 + row) * S.ld_out + f0;
       if (full) {
-        tc_st4<RT>(S.out, o, make_float4(v[0], v[1], v[2], v[3]));
+        tc_st4<RT, WT>(S.out, o, make_float4(v[0], v[1], v[2], v[3]));
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          if (f0 + i < S.N) tc_st1<RT>(S.out, o + i, v[i]);
+          if (f0 + i < S.N) tc_st1<RT, WT>(S.out, o + i, v[i]);
       }
     }
   }
@@ -567,11 +572,12 @@ __device__ __forceinline__ void tc_epi_loads(const TcArgs& A, COp& S, int t, con
   }
 }
 
-template <int RT, int KIND>
+template <int RT, int KIND, bool WT = false>
 __device__ __forceinline__ void tc_epilogue(const TcArgs& A, COp& S, const TcBuf& OUT, int t, uint64_t base,
                                             const tc_f32x4 (&acc)[RT], const float4 (&ov)[RT],
                                             const float2 (&tv)[RT], TcRows<RT>& R, int row0, int nrows) {
-  if (KIND == TC_TANH || KIND == TC_TGRAD || KIND == TC_LIN) tc_store_act<RT, KIND>(S, OUT, t, acc, ov, row0, nrows);
+  if (KIND == TC_TANH || KIND == TC_TGRAD || KIND == TC_LIN)
+    tc_store_act<RT, KIND, WT>(S, OUT, t, acc, ov, row0, nrows);
   else if (KIND == TC_BERN) tc_bern<RT>(A, S, t, acc, ov, R, row0, nrows);
   else tc_head<RT, KIND>(A, S, OUT, t, base, acc, tv, R, row0, nrows);
 }
@@ -692,8 +698,8 @@ __device__ __forceinline__ int tc_dense(const TcArgs& A, CJob& J, COp& S, const 
 #endif
       switch (kind) {
         case TC_TANH: if constexpr ((KM >> TC_TANH) & 1u) tc_epilogue<RT, TC_TANH>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        case TC_TGRAD: if constexpr ((KM >> TC_TGRAD) & 1u) tc_epilogue<RT, TC_TGRAD>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        case TC_LIN: if constexpr ((KM >> TC_LIN) & 1u) tc_epilogue<RT, TC_LIN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_TGRAD: if constexpr ((KM >> TC_TGRAD) & 1u) tc_epilogue<RT, TC_TGRAD, (KM & kTcWriteThrough) != 0>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_LIN: if constexpr ((KM >> TC_LIN) & 1u) tc_epilogue<RT, TC_LIN, (KM & kTcWriteThrough) != 0>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
         case TC_BERN: if constexpr ((KM >> TC_BERN) & 1u) tc_epilogue<RT, TC_BERN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
         case TC_SAMPLE: if constexpr ((KM >> TC_SAMPLE) & 1u) tc_epilogue<RT, TC_SAMPLE>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
         case TC_HEADP: if constexpr ((KM >> TC_HEADP) & 1u) tc_epilogue<RT, TC_HEADP>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
@@ -756,8 +762,8 @@ __device__ __forceinline__ void tc_dense2(const TcArgs& A, CJob& J, COp& S, cons
     if (x.last) {
       switch (kind) {
         case TC_TANH: if constexpr ((KM >> TC_TANH) & 1u) tc_epilogue<RT, TC_TANH>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        case TC_TGRAD: if constexpr ((KM >> TC_TGRAD) & 1u) tc_epilogue<RT, TC_TGRAD>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
-        case TC_LIN: if constexpr ((KM >> TC_LIN) & 1u) tc_epilogue<RT, TC_LIN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_TGRAD: if constexpr ((KM >> TC_TGRAD) & 1u) tc_epilogue<RT, TC_TGRAD, (KM & kTcWriteThrough) != 0>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
+        case TC_LIN: if constexpr ((KM >> TC_LIN) & 1u) tc_epilogue<RT, TC_LIN, (KM & kTcWriteThrough) != 0>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
         case TC_BERN: if constexpr ((KM >> TC_BERN) & 1u) tc_epilogue<RT, TC_BERN>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
         case TC_SAMPLE: if constexpr ((KM >> TC_SAMPLE) & 1u) tc_epilogue<RT, TC_SAMPLE>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
         case TC_HEADP: if constexpr ((KM >> TC_HEADP) & 1u) tc_epilogue<RT, TC_HEADP>(A, S, OUT, x.t, base, acc, ov, tv, R, row0, nrows); break;
@@ -1011,7 +1017,7 @@ __device__ __forceinline__ void tc_loadslab(CJob& J, COp& S, int row0, int nrows
 // added in fixed order through LDS scratch (S.in_buf's planes, [nsg][nq][8]
 // floats; deterministic).  dP0 goes to out_buf (natural order,
 // zeros to next_k) and S.out.
-template <int RT, int SPT, int IPP>
+template <int RT, int SPT, int IPP, bool WT>
 __device__ __forceinline__ void tc_gbwd0_p(const TcArgs& A, CJob& J, COp& S, int row0, int nrows) {
   const int d = S.d, kS = A.kS;
   // 32 column quads up to d = 128 (measured: one batch of every sample at
@@ -1103,7 +1109,8 @@ __device__ __forceinline__ void tc_gbwd0_p(const TcArgs& A, CJob& J, COp& S, int
         const int col = j < 4 ? c : d + c;
         if (j >= 4) v *= fexp(S.P[(size_t)b2 * S.ld_P + d + c]);      // dzs = dscale * exp(zs)
         tc_put1(B, r2 * B.ld + col, v);
-        S.out[(size_t)b2 * S.ld_out + col] = v;
+        if constexpr (WT) tc_st1<1, true>(S.out, (size_t)b2 * S.ld_out + col, v);
+        else S.out[(size_t)b2 * S.ld_out + col] = v;
       }
     }
     tc_lds_barrier();
@@ -1120,10 +1127,10 @@ __device__ __forceinline__ void tc_gbwd0_p(const TcArgs& A, CJob& J, COp& S, int
 // loads in flight, then the groups are added in fixed order through LDS
 // scratch (S.in_buf's planes, [IPP][nsg][nq][8] floats; deterministic).  dP0
 // goes to out_buf (natural order, zeros to next_k) and S.out.
-template <int RT>
+template <int RT, bool WT = false>
 __device__ __forceinline__ void tc_gbwd0(const TcArgs& A, CJob& J, COp& S, int row0, int nrows) {
-  if (nrows >= 2 && S.d <= 128) tc_gbwd0_p<RT, 3, 2>(A, J, S, row0, nrows);
-  else tc_gbwd0_p<RT, 2, 1>(A, J, S, row0, nrows);
+  if (nrows >= 2 && S.d <= 128) tc_gbwd0_p<RT, 3, 2, WT>(A, J, S, row0, nrows);
+  else tc_gbwd0_p<RT, 2, 1, WT>(A, J, S, row0, nrows);
 }
 
 // ----------------------------------------------------------------- kernel
@@ -1246,7 +1253,7 @@ __device__ __forceinline__ void tc_body(const TcArgs& A, const int bid) {
       case TC_GBWD_ENC: if constexpr ((KM >> TC_GBWD_ENC) & 1u) tc_gbwd<RT, TC_GBWD_ENC>(A, J, S, row0, nrows); break;
       case TC_LOADG: if constexpr ((KM >> TC_LOADG) & 1u) tc_loadg<RT>(A, J, S, row0, nrows); break;
       case TC_LOADSLAB: if constexpr ((KM >> TC_LOADSLAB) & 1u) tc_loadslab<RT>(J, S, r0, nr); break;
-      default: if constexpr ((KM >> TC_GBWD0) & 1u) tc_gbwd0<RT>(A, J, S, row0, nrows); break;
+      default: if constexpr ((KM >> TC_GBWD0) & 1u) tc_gbwd0<RT, (KM & kTcWriteThrough) != 0>(A, J, S, row0, nrows); break;
 #endif
     }
 #ifdef IWAE_TC_TRACE
@@ -1323,8 +1330,13 @@ __global__ __launch_bounds__(TC_NW * 64) void tcu_kernel(TcArgs A, UpdArgs U, Up
     if (threadIdx.x == 0) g_tcu_trace[b * 4 + 1] = wall_clock64();
 #endif
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the XCD's L2 written back
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // write-through hand-off (W.wt, only on the write-through instantiation):
+      // every handed-off byte was stored sc1 and drained above, so the counter
+      // add needs no release fence (no L2 write-back on the critical path)
+      if (!((KM & kTcWriteThrough) && W.wt)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the XCD's L2 written back
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       const unsigned p = __hip_atomic_fetch_add(W.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("" ::"v"(p));                              // (the add has returned: performed at L2)
       upd_arrive(W);
@@ -1341,12 +1353,19 @@ __global__ __launch_bounds__(TC_NW * 64) void tcu_kernel(TcArgs A, UpdArgs U, Up
 #endif
 }
 
-hipError_t launch_tcu(hipStream_t st, const TcArgs& a, const UpdArgs& u, const UpdWait& w, size_t lds_bytes) {
+hipError_t launch_tcu(hipStream_t st, const TcArgs& a, const UpdArgs& u, const UpdWait& w_in, size_t lds_bytes) {
   const int n_tc = a.block_start[kTcMaxJobs];
   const int n_pad = (n_tc + 7) & ~7;                      // the update's blocks keep their b % 8 XCD groups
   const int grid = n_pad + 8 * (u.per_xcd + u.per_xcd2);
-  if (IWAE_TC_NARROW && IWAE_TC_KM && a.kinds && !(a.kinds & ~kTcKindsImgBwd))
-    hipLaunchKernelGGL((tcu_kernel<kTcKindsImgBwd>), dim3(grid), dim3(TC_NW * 64), lds_bytes, st, a, u, w, n_tc, n_pad);
+  // the write-through hand-off only on the job-I'-kinds instantiation (its
+  // stores are sc1) and only where the caller allowed it (every waiting tile
+  // takes the one-iteration path, whose dZ loads are sc1)
+  const bool narrow = IWAE_TC_NARROW && IWAE_TC_KM && a.kinds && !(a.kinds & ~kTcKindsImgBwd);
+  UpdWait w = w_in;
+  w.wt = narrow && w_in.wt && IWAE_TCU_WT;
+  if (narrow)
+    hipLaunchKernelGGL((tcu_kernel<kTcKindsImgBwd | kTcWriteThrough>), dim3(grid), dim3(TC_NW * 64), lds_bytes, st, a,
+                       u, w, n_tc, n_pad);
   else if (IWAE_TC_KM && a.kinds && !(a.kinds & ~kTcKindsBwd))
     hipLaunchKernelGGL((tcu_kernel<kTcKindsBwd>), dim3(grid), dim3(TC_NW * 64), lds_bytes, st, a, u, w, n_tc, n_pad);
   else
@@ -1389,7 +1408,7 @@ hipError_t tc_setup_attributes() {
                        (const void*)tc_kernel<1, kTcKindsBwd>, (const void*)tc_kernel<2, kTcKindsBwd>,
                        (const void*)tc_kernel<4, kTcKindsBwd>, (const void*)tcu_kernel<kTcKindsAll>,
                        (const void*)tcu_kernel<kTcKindsBwd>, (const void*)tc_kernel<1, kTcKindsBwdRows>, (const void*)tc_kernel<1, kTcKindsImgBwd>,
-                       (const void*)tcu_kernel<kTcKindsImgBwd>};
+                       (const void*)tcu_kernel<kTcKindsImgBwd | kTcWriteThrough>};
   for (const void* f : fns) {
     const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;

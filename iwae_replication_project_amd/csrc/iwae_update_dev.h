@@ -11,7 +11,7 @@ typedef __bf16 up_bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int UP_NW = 4;                    // waves
 constexpr int UP_NT = UP_NW * 64;           // threads
-constexpr int UP_RI = 128;                  // sample rows per iteration (4 k steps of 32)
+constexpr int UP_RI = kUpdRowsPerIter;                 // sample rows per iteration (4 k steps of 32)
 constexpr int UP_S = 72;                    // dwords per LDS row: 128 bf16 + 16 bf16 pad
 constexpr int UP_PLANE = 64 * UP_S;         // dwords per plane
 constexpr int UP_BUF = 4 * UP_PLANE;        // X hi, X lo, dZ hi, dZ lo
@@ -64,6 +64,10 @@ struct UpRegs {
 };
 __device__ __forceinline__ up_f32x4 up_ld4(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_bit_cast(up_f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+// sc1 load (L1 bypassed): the dZ of the write-through hand-off
+__device__ __forceinline__ up_f32x4 up_ld4_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(up_f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
 }
 __device__ __forceinline__ up_f32x2 up_ld2(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_bit_cast(up_f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
@@ -255,8 +259,12 @@ __device__ __forceinline__ void upd_wait(const UpdWait& w) {
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // write-through hand-off: the poll was an sc1 load and every load of the
+    // handed-off dZ is one too, so no acquire (MI355X_MICROARCH.md valid forms)
+    if (!w.wt) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if (gave_up) {
       __hip_atomic_fetch_add(w.ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(w.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -269,8 +277,7 @@ __device__ __forceinline__ void upd_wait(const UpdWait& w) {
   __syncthreads();
 }
 
-// One 64 x TN tile (TN = 64, or 32 for the sample-row layers: more
-// workgroups, half the MFMA and a quarter less staging per workgroup).
+// One 64 x TN tile (TN = 64).
 // (FULL false: the combined launch's update -- no slab apply modes, which
 // launch_pending rules out; less code for its workgroups to fetch)
 template <int TN, int NW, bool FULL = true>
@@ -364,10 +371,13 @@ __device__ __forceinline__ void upd_tile(const UpdArgs& a, const UpdJob& J, cons
     for (int q = 0; q < UpCfg<NW>::RPT; ++q) R0.x[q] = up_ld4(ra, O.x + q * (unsigned)J.lda * 4u);
     if (w) upd_wait(*w);
     const __amdgpu_buffer_rsrc_t rz = buf_rsrc(J.B, (unsigned)J.rows * (unsigned)J.ldb * 4u);
+    static_assert(TN == 64, "64-column tiles");
+    if (w && w->wt) {
 #pragma unroll
-    for (int q = 0; q < UpCfg<NW>::RPT; ++q) {
-      if constexpr (TN == 64) R0.z[q] = up_ld4(rz, O.z + q * (unsigned)J.ldb * 4u);
-      else R0.z[q] = up_ld2(rz, O.z + q * (unsigned)J.ldb * 4u);
+      for (int q = 0; q < UpCfg<NW>::RPT; ++q) R0.z[q] = up_ld4_sc1(rz, O.z + q * (unsigned)J.ldb * 4u);
+    } else {
+#pragma unroll
+      for (int q = 0; q < UpCfg<NW>::RPT; ++q) R0.z[q] = up_ld4(rz, O.z + q * (unsigned)J.ldb * 4u);
     }
     const __amdgpu_buffer_rsrc_t rk = buf_rsrc(J.ks, (unsigned)J.rows * 4u);
 #pragma unroll

@@ -369,7 +369,10 @@ def test_image_row_backward_and_update_in_one_launch_equal_two_launches(B, arch,
     wait in-launch for job I' through an agent-scope counter) against the two
     launches: bit-identical losses, gradients and post-Adam weights over graph-
     replayed Philox steps and an eager injected-noise step; the combined launch
-    ran (counter 9) and no in-launch wait gave up (counter 8)."""
+    ran (counter 9) and no in-launch wait gave up (counter 8).  Both hand-off
+    forms: write-through (knob tcu_wt 1, the default: job I' stores sc1 and
+    adds without a release fence, the waiting tiles load dZ sc1 without an
+    acquire) and release / acquire fences (tcu_wt 0)."""
     from iwae_replication_project_amd import Adam, Flexible_Model
     rng = np.random.default_rng(91 + B)
     k = 64 if loss == "PIWAE" else 50
@@ -378,20 +381,21 @@ def test_image_row_backward_and_update_in_one_launch_equal_two_launches(B, arch,
     eps = [rng.standard_normal((k, B, d)).astype(np.float32) for _ in range(nd) for d in arch[2]]
     kw = dict(k1=8, k2=8) if loss == "PIWAE" else dict(beta=0.5) if loss == "CIWAE" else {}
     runs = []
-    for flag in (1, 0):
-        m = Flexible_Model(*arch, dataset_bias=None, loss_function=loss, k=k, seed=17, tuning={"tcu": flag}, **kw)
+    for tune in ({"tcu": 1}, {"tcu": 1, "tcu_wt": 0}, {"tcu": 0}):
+        m = Flexible_Model(*arch, dataset_bias=None, loss_function=loss, k=k, seed=17, tuning=tune, **kw)
         m.compile(Adam(learning_rate=1e-3, epsilon=1e-4))
         n0 = m._lib.iwae_debug_count(m._h, 9)
         losses = [m.train_step(x)[loss] for _ in range(3)]
         losses.append(m.train_step(x, eps=eps)[loss])
         runs.append((np.asarray(losses, np.float32), _flat(m.get_gradients()), _flat(m.get_weights()),
                      m._lib.iwae_debug_count(m._h, 9) - n0, m._lib.iwae_debug_count(m._h, 8)))
-    (la, ga, wa, na, fa), (lb, gb, wb, nb, fb) = runs
-    assert na > 0 and nb == 0, (na, nb)
-    assert fa == 0 and fb == 0
-    np.testing.assert_array_equal(la, lb)
-    np.testing.assert_array_equal(ga, gb)
-    np.testing.assert_array_equal(wa, wb)
+    (lb, gb, wb, nb, fb) = runs[-1]
+    assert nb == 0 and fb == 0
+    for la, ga, wa, na, fa in runs[:2]:
+        assert na > 0 and fa == 0, (na, fa)
+        np.testing.assert_array_equal(la, lb)
+        np.testing.assert_array_equal(ga, gb)
+        np.testing.assert_array_equal(wa, wb)
 
 
 def test_in_launch_wait_that_gives_up_fails_loudly():
