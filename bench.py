@@ -443,9 +443,11 @@ def main():
             n -= m
             off += m
 
-    # ---- warmup: W steps, then the timed call's graphs captured (no step runs)
-    run(args.warmup)
+    # ---- the timed call's graphs captured and uploaded (no step runs), then the
+    # W warmup steps, so the timed call starts on a GPU that has just been busy
+    # (not one left idle while the host captured and instantiated its graphs)
     prepare(args.steps, args.warmup)
+    run(args.warmup)
     model._stream.synchronize()
     torch.cuda.synchronize()
     cap0 = model.graph_captures()

