@@ -361,8 +361,6 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-c0", action="store_true")
-    ap.add_argument("--headline-first", action="store_true",
-                    help="time the headline train steps before the other legs (A/B of the leg order)")
     ap.add_argument("--c0-steps", type=int, default=200)
     ap.add_argument("--tune", action="append", default=[],
                     help="library tuning knob name=value (include/iwae.h enum iwae_knob), repeatable; A/B runs only")
@@ -445,61 +443,130 @@ def main():
             n -= m
             off += m
 
-    def headline():
-        # the timed call's graphs captured and uploaded (no step runs), then the
-        # W warmup steps, so the timed call starts on a GPU that has just been busy
-        # (not one left idle while the host captured and instantiated its graphs)
-        prepare(args.steps, args.warmup)
-        run(args.warmup)
-        model._stream.synchronize()
-        torch.cuda.synchronize()
-        cap0 = model.graph_captures()
-        # ---- timed region: K train steps
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        run(args.steps, args.warmup)
-        model._stream.synchronize()
-        torch.cuda.synchronize()
-        barrier()
-        el = time.perf_counter() - t0
-        captures_timed = model.graph_captures() - cap0
-        if captures_timed:
-            raise SystemExit(f"[bench] {captures_timed} graph capture(s) inside the timed region")
-        # no in-launch wait of the timed steps gave up (their gradients would be invalid)
-        model.check_kernel_status()
-        if world > 1:
-            t = torch.tensor([el], device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        rows = world * B_PER_GPU * K * args.steps
-        value = rows / el
-        ms_per_step = 1e3 * el / args.steps
-        # the same number of steps as one train_step call each (host issue + one graph per step)
-        run_calls(min(args.warmup, 10), args.warmup + args.steps)
-        model._stream.synchronize()
-        barrier()
-        torch.cuda.synchronize()
-        tc0 = time.perf_counter()
-        run_calls(args.steps, 2 * args.warmup + args.steps)
-        model._stream.synchronize()
-        torch.cuda.synchronize()
-        barrier()
-        elc = time.perf_counter() - tc0
-        if world > 1:
-            t = torch.tensor([elc], device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elc = float(t.item())
-        loss = float(model._loss_buf.item())
-        per_call = dict(ms_per_step=round(1e3 * elc / args.steps, 5), value=round(rows / elc, 1),
-                        note="the same steps issued as one train_step (F:221) call each: one graph launch per step")
-        return el, rows, value, ms_per_step, captures_timed, per_call, loss
+    # ---- the timed call's graphs captured and uploaded (no step runs), then the
+    # W warmup steps, so the timed call starts on a GPU that has just been busy
+    # (not one left idle while the host captured and instantiated its graphs)
+    prepare(args.steps, args.warmup)
+    run(args.warmup)
+    model._stream.synchronize()
+    torch.cuda.synchronize()
+    cap0 = model.graph_captures()
+    # ---- timed region: K train steps
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps, args.warmup)
+    model._stream.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    captures_timed = model.graph_captures() - cap0
+    if captures_timed:
+        raise SystemExit(f"[bench] {captures_timed} graph capture(s) inside the timed region")
+    # no in-launch wait of the timed steps gave up (their gradients would be invalid)
+    model.check_kernel_status()
+    if world > 1:
+        t = torch.tensor([el], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    rows = world * B_PER_GPU * K * args.steps
+    value = rows / el
+    ms_per_step = 1e3 * el / args.steps
+    # the same number of steps as one train_step call each (host issue + one graph per step)
+    run_calls(min(args.warmup, 10), args.warmup + args.steps)
+    model._stream.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    tc0 = time.perf_counter()
+    run_calls(args.steps, 2 * args.warmup + args.steps)
+    model._stream.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    elc = time.perf_counter() - tc0
+    if world > 1:
+        t = torch.tensor([elc], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elc = float(t.item())
+    loss = float(model._loss_buf.item())
+    per_call = dict(ms_per_step=round(1e3 * elc / args.steps, 5), value=round(rows / elc, 1),
+                    note="the same steps issued as one train_step (F:221) call each: one graph launch per step")
 
-    # ---- the headline is timed after the workload legs below (unless
-    # --headline-first): its short timed call (the driver's --steps 20) then starts
-    # on a GPU at its working clocks, not one coming out of the process's idle start-up
-    if args.headline_first:
-        el, rows, value, ms_per_step, captures_timed, per_call, loss = headline()
+    # ---- dominant kernel live timing.  Candidates: the train engine's forward and
+    # backward launches (iwae_train.hip) and, where the step still uses it, the
+    # output-layer Bernoulli GEMM.  Each is recorded from one eager step and
+    # re-launched K times back to back between two HIP events on the library's
+    # stream (the stream it runs on); avg = elapsed / K.  The dominant one (the
+    # longest) is priced against its matrix-core peak.
+
+    def live(kind, epi):
+        model._call(model._lib.iwae_profile_gemm(model._h, kind, epi))
+        run(1, args.warmup + args.steps)
+        ms, fl = ctypes.c_double(), ctypes.c_double()
+        rc = model._lib.iwae_profile_replay(model._h, args.steps, ctypes.byref(ms), ctypes.byref(fl))
+        model._call(model._lib.iwae_profile_gemm(model._h, -1, -1))
+        if rc != 0:
+            return None
+        return ms.value / args.steps, fl.value / args.steps
+
+    # algorithmic FLOP and bytes per launch (kernel_work): the forward and backward
+    # launches each do one product per sample-row Dense layer (281,800 MACs per
+    # row, SURVEY s8(d)); the library's own count of the forward includes the
+    # output MLP's two hidden layers that its column-split jobs recompute
+    # (reported as executed).  Each kernel is priced against the roofline its
+    # FLOP / byte ratio puts it under (roofline_of).
+    rows_step = B_PER_GPU * K
+    specs = {"tc_kernel forward (train engine, bf16x3)": (10, 0, "fwd"),
+             "tc_kernel backward (train engine, bf16x3)": (11, 0, "bwd"),
+             "upd_kernel (weight gradients + Adam + FX copies, bf16x3)": (15, 0, "upd"),
+             "tcu_kernel (job I' + weight gradients + Adam + FX copies, one launch)": (16, 0, "tcu")}
+    kern = {}
+    for name, (kind, epi, wk) in specs.items():
+        v = live(kind, epi)
+        if v is None:
+            continue
+        fl, nby = kernel_work(wk, rows_step, B_PER_GPU)
+        r = roofline_of(fl, nby, v[0] * 1e3)
+        kern[name] = dict(avg_us=round(v[0] * 1e3, 3), flop_per_launch=fl, flop_executed=v[1],
+                          alg_bytes_per_launch=nby, tflops=round(fl / (v[0] * 1e-3) / 1e12, 3),
+                          bound=r["bound"], frac=r["frac"], flop_per_byte=r["flop_per_byte"])
+    dom = max(kern, key=lambda k: kern[k]["avg_us"])
+    kd = kern[dom]
+    # HBM traffic of the same kernel: committed rocprofv3 PMC record (tools/pmc_passes.sh +
+    # tools/pmc_to_json.py; FETCH_SIZE x2 per the gfx950 correction, WRITE_SIZE as is)
+    traffic, traffic_src = None, None
+    pmc_name = PMC_RECORD
+    pmc = os.path.join(ROOT, "profiles", pmc_name)
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            rec = json.load(f).get(dom)          # records keyed by the kernel label used here
+        if rec:
+            traffic = round(rec["traffic_bytes"] / 1e6, 3)
+            traffic_src = f"profiles/{pmc_name} (MB per launch: fetch {rec['fetch_bytes'] / 1e6:.2f} + " \
+                          f"write {rec['write_bytes'] / 1e6:.2f})"
+    fl, nby = kd["flop_per_launch"], kd["alg_bytes_per_launch"]
+    roofline = roofline_of(fl, nby, kd["avg_us"])
+    roofline.update(traffic=traffic, traffic_unit="MB/launch", traffic_source=traffic_src,
+                    traffic_over_alg=(round(traffic * 1e6 / nby, 2) if traffic else None),
+                    kernel=dom, avg_us=kd["avg_us"], flop_per_launch=fl, alg_MB_per_launch=round(nby / 1e6, 3),
+                    launches=args.steps,
+                    peak_basis=("mfma: bf16 dense 2.5 PFLOP/s / 3 bf16 MFMAs per bf16x3 product; hbm: 8 TB/s; "
+                                "bound = the larger of FLOP / 833.3 TFLOP/s and bytes / 8 TB/s (ridge 104 FLOP/B)"),
+                    mfma_frac=round(fl / (kd["avg_us"] * 1e-6) / 1e12 / BF16X3_PEAK_TFLOPS, 4),
+                    frac_of_bf16_dense_peak=round(fl / (kd["avg_us"] * 1e-6) / 1e12 / BF16_PEAK_TFLOPS, 4),
+                    kernels=kern, step_tflops=round(TRAIN_FLOP_PER_ROW * rows / el / 1e12, 3))
+
+    # ---- the train step's memory-bound launches (Adam, bound, FX refresh), same
+    # replay timing: algorithmic HBM bytes per launch / duration vs HBM peak
+    mem = {}
+    for kind, name in ((12, "adam_kernel"), (13, "bound_kernel"), (14, "fx_refresh_kernel")):
+        v = live(kind, 0)
+        if v is not None:
+            ms1, by = v
+            mem[name] = dict(avg_us=round(ms1 * 1e3, 3), bytes_per_launch=int(by),
+                             gbps=round(by / (ms1 * 1e-3) / 1e9, 1),
+                             frac_of_hbm_peak=round(by / (ms1 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+    roofline["memory_kernels"] = dict(peak_gbps=HBM_PEAK_GBS, kernels=mem,
+                                      note="bytes: algorithmic (each operand once); launches replayed back to back")
 
     # ---- configs[4] per-GPU share: B=512 images per GPU, k=50, same model and
     # step (RCCL gradient all-reduce for N > 1)
@@ -656,86 +723,6 @@ def main():
                   "1 stochastic layer 784-200-200-50, batch 20 per GPU", steps=args.c0_steps,
                   ms_per_step=round(1e3 * el4 / args.c0_steps, 5),
                   tflops=round(1_438_240 * c0rows / el4 / 1e12, 3))
-
-    if not args.headline_first:
-        el, rows, value, ms_per_step, captures_timed, per_call, loss = headline()
-
-    # ---- dominant kernel live timing.  Candidates: the train engine's forward and
-    # backward launches (iwae_train.hip) and, where the step still uses it, the
-    # output-layer Bernoulli GEMM.  Each is recorded from one eager step and
-    # re-launched K times back to back between two HIP events on the library's
-    # stream (the stream it runs on); avg = elapsed / K.  The dominant one (the
-    # longest) is priced against its matrix-core peak.
-
-    def live(kind, epi):
-        model._call(model._lib.iwae_profile_gemm(model._h, kind, epi))
-        run(1, args.warmup + args.steps)
-        ms, fl = ctypes.c_double(), ctypes.c_double()
-        rc = model._lib.iwae_profile_replay(model._h, args.steps, ctypes.byref(ms), ctypes.byref(fl))
-        model._call(model._lib.iwae_profile_gemm(model._h, -1, -1))
-        if rc != 0:
-            return None
-        return ms.value / args.steps, fl.value / args.steps
-
-    # algorithmic FLOP and bytes per launch (kernel_work): the forward and backward
-    # launches each do one product per sample-row Dense layer (281,800 MACs per
-    # row, SURVEY s8(d)); the library's own count of the forward includes the
-    # output MLP's two hidden layers that its column-split jobs recompute
-    # (reported as executed).  Each kernel is priced against the roofline its
-    # FLOP / byte ratio puts it under (roofline_of).
-    rows_step = B_PER_GPU * K
-    specs = {"tc_kernel forward (train engine, bf16x3)": (10, 0, "fwd"),
-             "tc_kernel backward (train engine, bf16x3)": (11, 0, "bwd"),
-             "upd_kernel (weight gradients + Adam + FX copies, bf16x3)": (15, 0, "upd"),
-             "tcu_kernel (job I' + weight gradients + Adam + FX copies, one launch)": (16, 0, "tcu")}
-    kern = {}
-    for name, (kind, epi, wk) in specs.items():
-        v = live(kind, epi)
-        if v is None:
-            continue
-        fl, nby = kernel_work(wk, rows_step, B_PER_GPU)
-        r = roofline_of(fl, nby, v[0] * 1e3)
-        kern[name] = dict(avg_us=round(v[0] * 1e3, 3), flop_per_launch=fl, flop_executed=v[1],
-                          alg_bytes_per_launch=nby, tflops=round(fl / (v[0] * 1e-3) / 1e12, 3),
-                          bound=r["bound"], frac=r["frac"], flop_per_byte=r["flop_per_byte"])
-    dom = max(kern, key=lambda k: kern[k]["avg_us"])
-    kd = kern[dom]
-    # HBM traffic of the same kernel: committed rocprofv3 PMC record (tools/pmc_passes.sh +
-    # tools/pmc_to_json.py; FETCH_SIZE x2 per the gfx950 correction, WRITE_SIZE as is)
-    traffic, traffic_src = None, None
-    pmc_name = PMC_RECORD
-    pmc = os.path.join(ROOT, "profiles", pmc_name)
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            rec = json.load(f).get(dom)          # records keyed by the kernel label used here
-        if rec:
-            traffic = round(rec["traffic_bytes"] / 1e6, 3)
-            traffic_src = f"profiles/{pmc_name} (MB per launch: fetch {rec['fetch_bytes'] / 1e6:.2f} + " \
-                          f"write {rec['write_bytes'] / 1e6:.2f})"
-    fl, nby = kd["flop_per_launch"], kd["alg_bytes_per_launch"]
-    roofline = roofline_of(fl, nby, kd["avg_us"])
-    roofline.update(traffic=traffic, traffic_unit="MB/launch", traffic_source=traffic_src,
-                    traffic_over_alg=(round(traffic * 1e6 / nby, 2) if traffic else None),
-                    kernel=dom, avg_us=kd["avg_us"], flop_per_launch=fl, alg_MB_per_launch=round(nby / 1e6, 3),
-                    launches=args.steps,
-                    peak_basis=("mfma: bf16 dense 2.5 PFLOP/s / 3 bf16 MFMAs per bf16x3 product; hbm: 8 TB/s; "
-                                "bound = the larger of FLOP / 833.3 TFLOP/s and bytes / 8 TB/s (ridge 104 FLOP/B)"),
-                    mfma_frac=round(fl / (kd["avg_us"] * 1e-6) / 1e12 / BF16X3_PEAK_TFLOPS, 4),
-                    frac_of_bf16_dense_peak=round(fl / (kd["avg_us"] * 1e-6) / 1e12 / BF16_PEAK_TFLOPS, 4),
-                    kernels=kern, step_tflops=round(TRAIN_FLOP_PER_ROW * rows / el / 1e12, 3))
-
-    # ---- the train step's memory-bound launches (Adam, bound, FX refresh), same
-    # replay timing: algorithmic HBM bytes per launch / duration vs HBM peak
-    mem = {}
-    for kind, name in ((12, "adam_kernel"), (13, "bound_kernel"), (14, "fx_refresh_kernel")):
-        v = live(kind, 0)
-        if v is not None:
-            ms1, by = v
-            mem[name] = dict(avg_us=round(ms1 * 1e3, 3), bytes_per_launch=int(by),
-                             gbps=round(by / (ms1 * 1e-3) / 1e9, 1),
-                             frac_of_hbm_peak=round(by / (ms1 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
-    roofline["memory_kernels"] = dict(peak_gbps=HBM_PEAK_GBS, kernels=mem,
-                                      note="bytes: algorithmic (each operand once); launches replayed back to back")
 
     cpu = cpu_nll = cpu_c0 = None
     if rank == 0 and world == 1 and not args.no_cpu:
