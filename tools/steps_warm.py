@@ -5,7 +5,7 @@ rocprofv3 --kernel-trace (mode "trace"): the same calls, then
     python tools/steps_warm.py analyze <run_kernel_trace.csv>
 prints the span of each step (first kernel start -> next step's first kernel
 start) by its index inside the 20-step calls, against the 200-step call's.
-    python tools/steps_warm.py run|trace"""
+    python tools/steps_warm.py run|trace|first"""
 import csv
 import os
 import sys
@@ -63,8 +63,36 @@ def main():
     xd = m._x(x)
     for n in (20, 200):
         m.prepare_train_steps(xd[:n * B], B)
+    if mode == "first":
+        m.prepare_train_steps(xd[:200 * B], B)
     m.train_steps(xd[:200 * B], B, sync=False)
     torch.cuda.synchronize()
+    if mode == "first":
+        # the first replay of a prepared (captured, uploaded, never launched)
+        # 20-step graph against its later replays, GPU hot from a 200-step call;
+        # then 20 steps as five 4-step graph launches back to back (one sync)
+        for n in (4,):
+            m.prepare_train_steps(xd[:n * B], B)
+        w = []
+        for _ in range(6):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            m.train_steps(xd[:20 * B], B, sync=False)
+            m._stream.synchronize()
+            w.append((time.perf_counter() - t) * 1e6)
+        print("20-step graph, calls 1..6 (the first = its first replay), us/step:",
+              " ".join(f"{v / 20:.2f}" for v in w), flush=True)
+        m.train_steps(xd[:4 * B], B, sync=False)
+        w = []
+        for _ in range(6):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for j in range(5):
+                m.train_steps(xd[4 * j * B:4 * (j + 1) * B], B, sync=False)
+            m._stream.synchronize()
+            w.append((time.perf_counter() - t) * 1e6)
+        print("20 steps as five 4-step graph launches, us/step:", " ".join(f"{v / 20:.2f}" for v in w), flush=True)
+        return
     reps = 6 if mode == "trace" else 20
     for n in (20, 200, 20):
         w = []
