@@ -3,7 +3,9 @@
 # slow because the GPU is cold?  (1) as is vs after extra untimed steps
 # (bench_hot_tmp.py, an experiment copy), headline-only runs; (2) the full
 # bench with the headline timed first (--headline-first) vs after the other
-# legs (default), alternating.
+# legs (default), alternating.  (Historical: the bench that had --headline-first
+# was reverted after this A/B, profiles/r06x_cold_and_leg_order_ab.txt; the hot arm
+# needs bench_hot_tmp.py, an experiment copy that is not kept.)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r06x; mkdir -p $O
