@@ -12,7 +12,9 @@ TAG=$(basename "$OUT" .so)
 OBJS=""
 for f in iwae_gemm iwae_elem iwae_fused iwae_mega iwae_nring iwae_train iwae_update iwae_dwgrad iwae_model; do
   if [[ ",$SRCS," == *",$f.hip,"* ]]; then
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -c -o build/var/${f}_${TAG}.o $S/$f.hip
+    # (the in-tree build compiles these three without the SLP vectorizer: __graft_entry__.SOURCE_FLAGS)
+    NOSLP=""; case $f in iwae_train|iwae_update|iwae_gemm) NOSLP=-fno-slp-vectorize ;; esac
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result $NOSLP "$@" -c -o build/var/${f}_${TAG}.o $S/$f.hip
     OBJS="$OBJS build/var/${f}_${TAG}.o"
   else
     OBJS="$OBJS build/obj/$f.o"
