@@ -699,6 +699,8 @@ constexpr unsigned kTcKindsAll = 0x1FFFu;
 constexpr unsigned kTcKindsBwdRows = (1u << TC_TGRAD) | (1u << TC_LIN) | (1u << TC_GBWD_PRIOR) | (1u << TC_GBWD_ENC) |
                                      (1u << TC_LOADG);
 constexpr unsigned kTcKindsImgBwd = (1u << TC_TGRAD) | (1u << TC_LIN) | (1u << TC_GBWD0);
+// job I alone (the first encoder layer's l2 / head on image rows above 32 images)
+constexpr unsigned kTcKindsImgFwd = (1u << TC_LOADSLAB) | (1u << TC_TANH) | (1u << TC_HEADP);
 // not an op kind: an engine instantiation whose activation / dZ stores are
 // write-through (sc1) -- job I' inside tcu_kernel, the producer side of the
 // write-through hand-off (UpdWait::wt)

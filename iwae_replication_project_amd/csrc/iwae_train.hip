@@ -1385,12 +1385,16 @@ hipError_t launch_tc(hipStream_t st, const TcArgs& a, int rt, size_t lds_bytes) 
   const bool cov = IWAE_TC_KM && a.kinds;
   switch (rt) {
     case 1:
-      // (no narrower forward set: without the folded image-row ops hipcc inlines
-      // differently and the forward kernel grows, 79.9 vs 77.6 KB)
+      // (no narrower sample-row forward set: without the folded image-row ops the
+      // forward kernel grew at -O3 (79.9 vs 77.6 KB); at -Os it is 63.7 vs 66.4 KB
+      // but measured no faster, profiles/r06if_narrow_engine_ab.txt.  Job I alone
+      // (B > 32 images) has its own set: 31.0 KB, the B = 512 step -1.2 %)
       if (IWAE_TC_NARROW && cov && !(a.kinds & ~kTcKindsBwdRows))
         hipLaunchKernelGGL((tc_kernel<1, kTcKindsBwdRows>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a);
       else if (IWAE_TC_NARROW && cov && !(a.kinds & ~kTcKindsImgBwd))
         hipLaunchKernelGGL((tc_kernel<1, kTcKindsImgBwd>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a);
+      else if (IWAE_TC_NARROW && cov && !(a.kinds & ~kTcKindsImgFwd))
+        hipLaunchKernelGGL((tc_kernel<1, kTcKindsImgFwd>), dim3(nb), dim3(TC_NW * 64), lds_bytes, st, a);
       else TC_LAUNCH(1);
       break;
     case 2: TC_LAUNCH(2); break;
@@ -1408,7 +1412,7 @@ hipError_t tc_setup_attributes() {
                        (const void*)tc_kernel<1, kTcKindsBwd>, (const void*)tc_kernel<2, kTcKindsBwd>,
                        (const void*)tc_kernel<4, kTcKindsBwd>, (const void*)tcu_kernel<kTcKindsAll>,
                        (const void*)tcu_kernel<kTcKindsBwd>, (const void*)tc_kernel<1, kTcKindsBwdRows>, (const void*)tc_kernel<1, kTcKindsImgBwd>,
-                       (const void*)tcu_kernel<kTcKindsImgBwd | kTcWriteThrough>};
+                       (const void*)tcu_kernel<kTcKindsImgBwd | kTcWriteThrough>, (const void*)tc_kernel<1, kTcKindsImgFwd>};
   for (const void* f : fns) {
     const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
